@@ -1,0 +1,227 @@
+#!/usr/bin/env python3
+"""Benchmark: Msamples/s of the path-tracing hot path on BASELINE config 2
+(Book-1 random spheres, 1200x800, 500 spp, depth 50).
+
+A "step" = one complete render of the configuration: every pixel x every
+sample, through the C ABI (rtw_render_rows_device) into an HBM-resident float4
+accumulator, plus (N > 1) the RCCL gather of the row-interleaved shards to
+rank 0 and their reassembly.  Scene build / BVH / upload happen once, before
+timing.  N GPUs split the same image (strong scaling): rank r renders row
+blocks b with b % N == r.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2]
+       (N > 1: torchrun --nproc-per-node N bench.py --gpus N ...)
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import importlib
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+NODE_BYTES = 32                # one BVH node / leaf record (rtw_layout.h)
+ROWS_PER_BLOCK = 16
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", default="c2", choices=["c2", "c3", "c4", "c5"])
+    ap.add_argument("--spp", type=int, default=0, help="override spp (0 = config's)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline duration")
+    ap.add_argument("--cpu-threads", type=int, default=8, help="reference uses 8 render threads (main.zig:41)")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    world_size = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world_size != args.gpus:
+        if world_size == 1 and args.gpus > 1:
+            raise SystemExit("--gpus N > 1 must be launched with torchrun --nproc-per-node N")
+    torch.cuda.set_device(local_rank)
+    distributed = world_size > 1
+    if distributed:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    pkg = importlib.import_module("zig-raytracing-weekend_amd")
+    L = pkg.lib()
+    cfg = pkg.configs.CONFIGS[args.config]
+    objs = cfg.objects()
+    arr = pkg.flatten(objs)
+    t0 = time.time()
+    world = pkg.World(arr, device=local_rank)
+    build_s = time.time() - t0
+    cam = cfg.camera()
+    if args.spp:
+        cam.samples_per_pixel = args.spp
+    cam.init()
+    W, H, spp = cam.derived.image_width, cam.derived.image_height, cam.samples_per_pixel
+    stats = world.stats()
+
+    n_blk = (H + ROWS_PER_BLOCK - 1) // ROWS_PER_BLOCK
+    max_blk = (n_blk + world_size - 1) // world_size
+    tile = torch.zeros((max_blk * ROWS_PER_BLOCK * W, 4), dtype=torch.float32, device="cuda")
+    my_rows = L.rtw_shard_rows(H, ROWS_PER_BLOCK, world_size, rank)
+    stream = torch.cuda.current_stream()
+    opts = pkg._abi.RtwRenderOpts(spp, pkg._abi.RTW_RENDER_NO_SYNC, None)   # one launch per step
+    gather_list = [torch.empty_like(tile) for _ in range(world_size)] if (distributed and rank == 0) else None
+    image = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda") if rank == 0 else None
+    # image row of every (shard, tile row) -- reassembly index for rank 0
+    src_idx, dst_idx = [], []
+    for s in range(world_size):
+        for r in range(max_blk * ROWS_PER_BLOCK):
+            y = ((r // ROWS_PER_BLOCK) * world_size + s) * ROWS_PER_BLOCK + r % ROWS_PER_BLOCK
+            if y < H:
+                src_idx.append(s * max_blk * ROWS_PER_BLOCK + r)
+                dst_idx.append(y)
+    src_idx = torch.tensor(src_idx, device="cuda")
+    dst_idx = torch.tensor(dst_idx, device="cuda")
+
+    def render_step(counters=None):
+        tile.zero_()
+        o = opts if counters is None else pkg._abi.RtwRenderOpts(spp, pkg._abi.RTW_RENDER_NO_SYNC, counters)
+        rc = L.rtw_render_rows_device(world.handle, C.byref(cam.derived), ROWS_PER_BLOCK, world_size, rank, 0, spp,
+                                      0, tile.data_ptr(), C.c_void_p(stream.cuda_stream), C.byref(o))
+        pkg._abi.check(rc, "rtw_render_rows_device")
+
+    def gather_step():
+        if distributed:
+            dist.gather(tile, gather_list=gather_list, dst=0)
+            if rank == 0:
+                allt = torch.stack(gather_list).view(-1, W, 4)
+                image.index_copy_(0, dst_idx, allt.index_select(0, src_idx))
+        else:
+            image.view(-1, W, 4).index_copy_(0, dst_idx, tile.view(-1, W, 4).index_select(0, src_idx))
+
+    # ---- algorithmic bytes of one step: counted pass (reference traversal == device traversal)
+    cnt = torch.zeros(8, dtype=torch.int64, device="cuda")
+    render_step(cnt.data_ptr())
+    torch.cuda.synchronize()
+    c = cnt.cpu().numpy()
+    nodes, leaves, rays, samples = (int(c[pkg._abi.RTW_STAT_NODES]), int(c[pkg._abi.RTW_STAT_LEAVES]),
+                                    int(c[pkg._abi.RTW_STAT_RAYS]), int(c[pkg._abi.RTW_STAT_SAMPLES]))
+    nan_count = int(c[pkg._abi.RTW_STAT_NAN])
+    pixels = my_rows * W
+    alg_bytes = NODE_BYTES * (nodes + leaves) + 32 * pixels
+
+    for _ in range(args.warmup):
+        render_step()
+        gather_step()
+    torch.cuda.synchronize()
+
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    for k in range(args.steps):
+        ev[k][0].record(stream)
+        render_step()
+        ev[k][1].record(stream)
+        gather_step()
+    torch.cuda.synchronize()
+    if distributed:
+        dist.barrier()
+    elapsed = time.perf_counter() - t_start
+    kernel_ms = [a.elapsed_time(b) for a, b in ev]
+    if distributed:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    total_samples = W * H * spp * args.steps
+    value = total_samples / elapsed / 1e6
+    avg_kernel_s = sum(kernel_ms) / len(kernel_ms) / 1e3
+    achieved = alg_bytes / avg_kernel_s / 1e9
+
+    cpu = None
+    if rank == 0 and world_size == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(pkg, arr, cam, args)
+
+    if rank == 0:
+        line = {
+            "metric": "Msamples/s (pixel·spp) on 1200×800 Book-1 random-spheres @500spp; 1→8 GPU",
+            "value": round(value, 3),
+            "unit": "Msamples/s",
+            "n_gpus": world_size,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic: seeded Book-1 random-spheres scene (seed 0, %d spheres), counter-based RNG seed 0"
+                    % len(objs),
+            "config": {"workload": cfg.description, "config_id": args.config, "width": W, "height": H,
+                       "spp": spp, "max_depth": cam.max_depth, "spheres": len(objs), "bvh_nodes": stats["n_nodes"],
+                       "bvh_depth": stats["depth"], "parallelism": f"row-interleaved tiles x{world_size}"
+                       + (" + RCCL gather" if distributed else ""), "rows_per_block": ROWS_PER_BLOCK},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                         "kernel": "render_pixels_v0", "avg_launch_ms": round(avg_kernel_s * 1e3, 3),
+                         "alg_bytes_per_launch": alg_bytes,
+                         "alg_bytes_per_sample": round(alg_bytes / max(1, samples), 2),
+                         "rays_per_sample": round(rays / max(1, samples), 4),
+                         "nodes_per_ray": round((nodes + leaves) / max(1, rays), 3)},
+            "cpu_baseline": cpu,
+            "nan_samples": nan_count,
+            "scene_build_s": round(build_s, 4),
+        }
+        print(json.dumps(line), flush=True)
+    world.close()
+    if distributed:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(pkg, arr, cam, args):
+    """The C oracle (faithful restatement, oracle/) on the host: samples-outer
+    loop over contiguous chunks with the reference's 8 render threads, on every
+    8th image row (a bounded, row-representative sample of the same scene and
+    camera), with spp scaled to ~args.cpu_seconds."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import numpy as np
+    import oracle as O
+
+    ow = O.World(arr.spheres, arr.materials, arr.textures, arr.perlins, [im.rgba for im in arr.images])
+    d = cam.derived
+    ocam = O.camera(aspect_ratio=cam.aspect_ratio, image_width=d.image_width, image_height=d.image_height,
+                    samples_per_pixel=d.samples_per_pixel, max_depth=d.max_depth, background=tuple(d.background),
+                    background_mode=d.background_mode, vfov=cam.vfov, lookfrom=cam.lookfrom, lookat=cam.lookat,
+                    vup=cam.vup, defocus_angle=cam.defocus_angle, focus_dist=cam.focus_dist,
+                    pixel_offset=d.pixel_offset)
+    W, H = d.image_width, d.image_height
+    rows = np.arange(0, H, 8)
+    pix = (rows[:, None] * W + np.arange(W)[None, :]).reshape(-1).astype(np.uint32)
+    t = time.perf_counter()
+    ow.render_pixels(ocam, 0, pix, 0, 1, threads=args.cpu_threads)
+    t1 = time.perf_counter() - t
+    spp = int(max(1, min(d.samples_per_pixel, args.cpu_seconds / max(t1, 1e-3))))
+    t = time.perf_counter()
+    ow.render_pixels(ocam, 0, pix, 0, spp, threads=args.cpu_threads)
+    dt = time.perf_counter() - t
+    return {"value": round(len(pix) * spp / dt / 1e6, 4), "unit": "Msamples/s", "cores": args.cpu_threads,
+            "kind": "port", "sample": f"every 8th row of {W}x{H} ({len(pix)} px) x {spp} spp, "
+                                      f"{args.cpu_threads} threads, {dt:.1f} s; host has {os.cpu_count()} CPUs",
+            "seconds": round(dt, 2)}
+
+
+if __name__ == "__main__":
+    main()

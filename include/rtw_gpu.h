@@ -1,0 +1,246 @@
+/*
+ * rtw_gpu.h -- C ABI of the MI355X-native path-tracing hot path.
+ *
+ * Drop-in boundary for dariooddenino/zig-raytracing-weekend's per-pixel sample
+ * loop.  The reference's only entry point into the loop is
+ *
+ *     pub fn render(self: *Camera, raytrace: *RayTraceState, context: Task) !void
+ *                                                        (src/camera.zig:93)
+ *
+ * called by RenderThread.renderFn (src/main.zig:66-68) for each of 8 Tasks
+ * spawned by startRender (src/main.zig:314-326).  It reads the Camera fields
+ * derived by Camera.init (src/camera.zig:118-154), the world (a BVHTree of
+ * Spheres, src/bvh.zig:17-104, src/objects.zig:68-148), and writes the
+ * SharedStateImageWriter float4 buffer (src/camera.zig:21-66).  The entry
+ * points below replace exactly that: a host (Zig via @cImport, C++, or Python
+ * via ctypes) describes the scene once (rtw_scene_create, replaces the
+ * pointer graph of Hittable/Material/Texture unions), derives the camera
+ * (rtw_camera_init, replaces Camera.init) and calls rtw_render for a pixel
+ * range and a sample range (replaces Camera.render for one Task).
+ *
+ * Plain C types only; no HIP or torch types cross the boundary (streams and
+ * device buffers are passed as void*).  Every function returns an RTW_* status;
+ * rtw_last_error() returns a thread-local message for the last failure.
+ * No exceptions cross the ABI.  The library never frees caller memory.
+ */
+#ifndef RTW_GPU_H
+#define RTW_GPU_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RTW_ABI_VERSION 1
+
+enum rtw_status {
+    RTW_OK = 0,
+    RTW_E_INVALID = -1,     /* bad argument / inconsistent scene */
+    RTW_E_HIP = -2,         /* HIP runtime error (message in rtw_last_error) */
+    RTW_E_OOM = -3,         /* device or host allocation failed */
+    RTW_E_CANCELLED = -4,   /* cancel flag observed between sample batches */
+    RTW_E_NODEVICE = -5     /* no gfx950 device visible */
+};
+
+/* ---------------------------------------------------------------------------
+ * Scene description (host memory, caller-owned, read once by rtw_scene_create)
+ * ------------------------------------------------------------------------- */
+
+/* Sphere.init / Sphere.initMoving (src/objects.zig:80-92).  48 bytes. */
+typedef struct rtw_sphere {
+    float center1[3];
+    float radius;
+    float center2[3];          /* used iff is_moving: center_vec = center2 - center1 */
+    uint32_t is_moving;
+    uint32_t material;         /* index into materials[] */
+    uint32_t _pad[3];
+} rtw_sphere;
+
+/* Material union (src/material.zig:11-144).  32 bytes. */
+enum rtw_material_kind {
+    RTW_MAT_LAMBERTIAN = 0,    /* albedo = textures[texture] */
+    RTW_MAT_METAL = 1,         /* albedo[3], fuzz (already clamped <= 1 as Metal.fromColor does) */
+    RTW_MAT_DIELECTRIC = 2,    /* ir */
+    RTW_MAT_DIFFUSE_LIGHT = 3, /* emit = textures[texture] */
+    RTW_MAT_ISOTROPIC = 4      /* albedo = textures[texture] (needs ConstantMedium; not in the sphere path) */
+};
+typedef struct rtw_material {
+    uint32_t kind;
+    uint32_t texture;
+    float fuzz;
+    float ir;
+    float albedo[3];
+    float _pad;
+} rtw_material;
+
+/* Texture union (src/textures.zig:10-124).  48 bytes. */
+enum rtw_texture_kind {
+    RTW_TEX_SOLID = 0,         /* even[] = color_value */
+    RTW_TEX_CHECKER = 1,       /* scale = inv_scale, even[], odd[] */
+    RTW_TEX_IMAGE = 2,         /* image = index into images[] */
+    RTW_TEX_NOISE = 3          /* perlin = index into perlins[], scale */
+};
+typedef struct rtw_texture {
+    uint32_t kind;
+    uint32_t image;
+    uint32_t perlin;
+    float scale;
+    float even[3];
+    float _p0;
+    float odd[3];
+    float _p1;
+} rtw_texture;
+
+/* zstbi.Image as used by RtwImage (src/rtw_image.zig:5-62): RGBA8, 4 B/texel. */
+typedef struct rtw_image {
+    const uint8_t* data;
+    uint32_t width, height, bytes_per_row, _pad;
+} rtw_image;
+
+/* Perlin tables (src/perlin.zig:76-101).  4608 bytes. */
+typedef struct rtw_perlin {
+    float ranvec[256][3];
+    uint16_t perm_x[256], perm_y[256], perm_z[256];
+} rtw_perlin;
+
+enum rtw_bvh_mode {
+    RTW_BVH_REFERENCE = 0      /* BVHTree.constructTree (src/bvh.zig:43-71): random axis from the
+                                  seeded build stream, std.sort.heap by box min, median split */
+};
+
+typedef struct rtw_scene_desc {
+    const rtw_sphere* spheres;     uint32_t n_spheres;
+    const rtw_material* materials; uint32_t n_materials;
+    const rtw_texture* textures;   uint32_t n_textures;
+    const rtw_image* images;       uint32_t n_images;
+    const rtw_perlin* perlins;     uint32_t n_perlins;
+    uint64_t bvh_seed;
+    uint32_t bvh_mode;
+    uint32_t _pad;
+} rtw_scene_desc;
+
+/* ---------------------------------------------------------------------------
+ * Camera (src/camera.zig:69-91 fields; rtw_camera_init restates Camera.init)
+ * ------------------------------------------------------------------------- */
+enum rtw_background_mode {
+    RTW_BG_CONSTANT = 0,       /* Camera.background (camera.zig:80, 207); HEAD default black */
+    RTW_BG_GRADIENT = 1        /* Book-1 sky, the commented camera.zig:204-206 */
+};
+
+typedef struct rtw_camera_params {
+    float aspect_ratio;
+    uint32_t image_width;
+    uint32_t image_height;     /* 0 -> round(width / aspect) (camera.zig:119-121) */
+    uint32_t samples_per_pixel;
+    uint32_t max_depth;
+    uint32_t background_mode;
+    float background[3];
+    float vfov;
+    float lookfrom[3];
+    float lookat[3];
+    float vup[3];
+    float defocus_angle;
+    float focus_dist;
+    uint32_t pixel_offset;     /* 1 reproduces camera.zig:100-101 (x = i%W + 1, y = i/W + 1) */
+} rtw_camera_params;
+
+typedef struct rtw_camera {
+    uint32_t image_width, image_height, size, samples_per_pixel, max_depth;
+    uint32_t background_mode, pixel_offset, _pad;
+    float center[3], pixel00_loc[3], pixel_delta_u[3], pixel_delta_v[3];
+    float u[3], v[3], w[3];
+    float defocus_disk_u[3], defocus_disk_v[3];
+    float defocus_angle;
+    float background[3];
+} rtw_camera;
+
+/* ---------------------------------------------------------------------------
+ * Entry points
+ * ------------------------------------------------------------------------- */
+typedef struct rtw_ctx rtw_ctx;
+
+/* Progress callback: samples (pixel x spp) finished so far in this call.
+ * Return non-zero to cancel (like RenderThread.stop, src/main.zig:58-60). */
+typedef int (*rtw_progress_fn)(uint64_t samples_done, uint64_t samples_total, void* user);
+
+typedef struct rtw_render_opts {
+    uint32_t spp_batch;        /* samples per kernel launch (cancel/progress granularity); 0 = auto */
+    uint32_t flags;            /* RTW_RENDER_* */
+    uint64_t* counters;        /* optional device-side stats out (RTW_STAT_COUNT u64) or NULL */
+} rtw_render_opts;
+
+enum { RTW_RENDER_NO_SYNC = 1u };  /* rtw_render_device: do not synchronise the stream */
+enum { RTW_STAT_RAYS = 0, RTW_STAT_NODES = 1, RTW_STAT_LEAVES = 2, RTW_STAT_SAMPLES = 3, RTW_STAT_NAN = 4,
+       RTW_STAT_COUNT = 8 };
+
+int rtw_version(void);
+const char* rtw_last_error(void);
+int rtw_device_count(int* out);
+
+/* Camera.init (src/camera.zig:118-154). Host-only arithmetic; shared by every caller. */
+int rtw_camera_init(const rtw_camera_params* params, rtw_camera* out);
+
+/* Builds the BVH (bvh_mode) on the host, flattens it to 32-byte depth-first
+ * nodes with skip links, and uploads nodes / materials / textures / images /
+ * perlin tables to `device`.  Replaces generateWorld's BVHTree.init
+ * (src/main.zig:309, src/bvh.zig:22-29). */
+int rtw_scene_create(const rtw_scene_desc* desc, int device, rtw_ctx** out);
+void rtw_scene_destroy(rtw_ctx* ctx);
+
+/* Camera.render for the pixel range [pix_begin, pix_end) (linear index
+ * i = y*W + x, the Task chunk of src/camera.zig:94-95) and the 0-based sample
+ * range [spp_begin, spp_end) (number_of_samples = s+1, camera.zig:98).
+ * accum: caller-owned HOST float4[W*H] (ColorAndSamples, camera.zig:21-39):
+ * rgb += sample radiance in sample order, w = spp_end (camera.zig:55-56).
+ * seed keys the counter-based RNG: identical (seed, pixel, sample) -> identical
+ * draws regardless of ranges, batching, devices.  cancel (may be NULL) is
+ * polled between sample batches (camera.zig:107).  Blocking. */
+int rtw_render(rtw_ctx* ctx, const rtw_camera* cam, uint32_t pix_begin, uint32_t pix_end,
+               uint32_t spp_begin, uint32_t spp_end, uint64_t seed, float* accum,
+               const volatile int32_t* cancel, rtw_progress_fn progress, void* user);
+
+/* Same, on a DEVICE buffer float4[W*H] already resident on ctx's device, on
+ * `stream` (a hipStream_t, or NULL for the ctx's own stream).  With
+ * RTW_RENDER_NO_SYNC the call only enqueues work. */
+int rtw_render_device(rtw_ctx* ctx, const rtw_camera* cam, uint32_t pix_begin, uint32_t pix_end,
+                      uint32_t spp_begin, uint32_t spp_end, uint64_t seed, float* d_accum,
+                      void* stream, const rtw_render_opts* opts);
+
+/* Row-interleaved shard of an image for multi-GPU:
+ * renders rows r with (r / rows_per_block) % n_shards == shard into a compact
+ * device buffer d_tile (float4[rows_in_shard * W], rows in increasing order). */
+int rtw_render_rows_device(rtw_ctx* ctx, const rtw_camera* cam, uint32_t rows_per_block, uint32_t n_shards,
+                           uint32_t shard, uint32_t spp_begin, uint32_t spp_end, uint64_t seed,
+                           float* d_tile, void* stream, const rtw_render_opts* opts);
+uint32_t rtw_shard_rows(uint32_t height, uint32_t rows_per_block, uint32_t n_shards, uint32_t shard);
+
+/* SharedStateImageWriter texel update: u8(256*clamp(sqrt(rgb/w),0,0.999)), alpha 255
+ * (src/camera.zig:58-65, src/color.zig:43-62). Host, n pixels. */
+int rtw_texture_from_accum(const float* accum, uint32_t n, uint8_t* rgba_out);
+
+/* Host-only: build + flatten the BVH exactly as rtw_scene_create does, without
+ * touching a device (nodes_out may be NULL to query the count). */
+int rtw_scene_flatten(const rtw_scene_desc* desc, void* nodes_out, uint32_t cap, uint32_t* n_out,
+                      uint32_t* depth_out);
+
+/* Introspection for tests / reports. */
+typedef struct rtw_scene_stats {
+    uint32_t n_nodes, n_leaves, n_inner, depth;
+    uint64_t device_bytes;
+    uint32_t axis_draws, _pad;
+} rtw_scene_stats;
+int rtw_scene_stats_get(rtw_ctx* ctx, rtw_scene_stats* out);
+/* Copies the flattened node array (32 B per node) to host. */
+int rtw_scene_nodes(rtw_ctx* ctx, void* out, uint32_t cap, uint32_t* n_out);
+
+/* Debug / known-answer hooks, executed ON THE DEVICE by the same device
+ * functions the render kernel uses. */
+int rtw_debug_rng(rtw_ctx* ctx, uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t n, float* out);
+int rtw_debug_sample(rtw_ctx* ctx, const rtw_camera* cam, uint64_t seed, uint32_t pixel, uint32_t sample,
+                     float out[3]);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RTW_GPU_H */

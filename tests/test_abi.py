@@ -1,0 +1,126 @@
+"""C-ABI boundary checks that need no GPU: the library loads, exports every
+symbol include/rtw_gpu.h declares, its records have the header's sizes, and its
+host-side halves (Camera.init, BVH build + flatten, toGamma2) agree bit-exactly
+with the oracle."""
+import ctypes as C
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import REPO
+
+HEADER = os.path.join(REPO, "include", "rtw_gpu.h")
+
+
+def header_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    names = re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\s*\*?\s*(rtw_[a-z_0-9]+)\s*\(", src, flags=re.M)
+    return sorted(set(names))
+
+
+def test_exports_every_header_symbol(rtw):
+    lib = rtw.lib()
+    names = header_functions()
+    assert len(names) >= 15
+    for n in names:
+        assert hasattr(lib, n), n
+    assert set(names) == set(rtw._abi.SIGNATURES), set(names) ^ set(rtw._abi.SIGNATURES)
+    assert lib.rtw_version() == 1
+
+
+def test_struct_sizes_match_header(rtw, tmp_path):
+    prog = tmp_path / "sizes.c"
+    structs = ["rtw_sphere", "rtw_material", "rtw_texture", "rtw_image", "rtw_perlin", "rtw_scene_desc",
+               "rtw_camera_params", "rtw_camera", "rtw_render_opts", "rtw_scene_stats"]
+    prog.write_text('#include <stdio.h>\n#include "rtw_gpu.h"\nint main(){' +
+                    "".join(f'printf("%zu\\n", sizeof({s}));' for s in structs) + "return 0;}\n")
+    exe = tmp_path / "sizes"
+    subprocess.check_call(["gcc", "-I", os.path.join(REPO, "include"), str(prog), "-o", str(exe)])
+    sizes = [int(x) for x in subprocess.check_output([str(exe)]).split()]
+    A = rtw._abi
+    mine = [A.SPHERE_DT.itemsize, A.MATERIAL_DT.itemsize, A.TEXTURE_DT.itemsize, C.sizeof(A.RtwImage),
+            A.PERLIN_DT.itemsize, C.sizeof(A.RtwSceneDesc), C.sizeof(A.RtwCameraParams), C.sizeof(A.RtwCamera),
+            C.sizeof(A.RtwRenderOpts), C.sizeof(A.RtwSceneStats)]
+    assert sizes == mine
+
+
+@pytest.mark.parametrize("kw", [dict(image_width=1200, aspect_ratio=1.5, spp=500),
+                                dict(image_width=400, aspect_ratio=16 / 9, spp=10),
+                                dict(image_width=3840, aspect_ratio=16 / 9, spp=1024)])
+def test_camera_init_matches_oracle(rtw, oracle, kw):
+    cam = rtw.book1_camera(max_depth=50, **kw).init()
+    o = oracle.camera(image_width=kw["image_width"], aspect_ratio=kw["aspect_ratio"],
+                      samples_per_pixel=kw["spp"], max_depth=50, background_mode=1)
+    assert bytes(cam.derived) == bytes(o)
+
+
+def test_camera_defaults_are_reference(rtw):
+    """camera.zig:70-91 defaults: 800 wide, 16:9 -> 450 high, spp 100, depth 16."""
+    cam = rtw.Camera().init()
+    assert (cam.derived.image_width, cam.derived.image_height) == (800, 450)
+    assert cam.samples_per_pixel == 100 and cam.max_depth == 16 and cam.pixel_offset == 1
+
+
+def test_texture_from_accum_matches_gamma2(rtw, oracle):
+    rng = np.random.default_rng(0)
+    acc = np.concatenate([rng.random((500, 3), np.float32) * 40, rng.integers(1, 50, (500, 1)).astype(np.float32)], 1)
+    acc[:5, :3] = 0
+    acc[5:10, :3] = 1e6
+    out = np.zeros((500, 4), np.uint8)
+    rtw.lib().rtw_texture_from_accum(acc.ctypes.data, 500, out.ctypes.data)
+    assert np.array_equal(out, oracle.gamma2(acc))
+
+
+@pytest.mark.parametrize("scene,seed", [("book1", 0), ("book1", 17), ("ref_head", 0)])
+def test_bvh_flatten_matches_oracle_tree(rtw, oracle, earth_rgba, scene, seed):
+    """Product BVH builder (C++, pre-order + skip links) == oracle pointer tree."""
+    imgs = [rtw.Image(earth_rgba)]
+    objs = rtw.worlds.generate_world(0, scene, imgs)
+    arr = rtw.flatten(objs, bvh_seed=seed)
+    nodes = rtw.scene.flatten_bvh(arr)
+    ow = oracle.World(arr.spheres, arr.materials, arr.textures, images=[earth_rgba], bvh_seed=seed)
+    d = ow.dump()
+    assert len(nodes) == len(d) == 2 * len(arr.spheres) - 1
+    a, b = nodes["a"], nodes["b"]
+    wbits = a[:, 3].view(np.uint32)
+    is_leaf = (wbits & 0x80000000) != 0
+    skip = wbits & 0x7FFFFFFF
+    assert np.array_equal(is_leaf, d[:, 6] >= 0)
+    assert np.array_equal(skip, np.arange(len(d)) + d[:, 7].astype(np.int64))
+    inner = ~is_leaf
+    assert np.array_equal(a[inner, :3], d[inner, 0:3]) and np.array_equal(b[inner, :3], d[inner, 3:6])
+    sid = b[is_leaf, 2].view(np.uint32)
+    assert np.array_equal(sid, d[is_leaf, 6].astype(np.uint32))
+    assert np.array_equal(a[is_leaf, :3], arr.spheres["center1"][sid])
+    assert np.array_equal(b[is_leaf, 0], arr.spheres["radius"][sid])
+    assert np.array_equal(b[is_leaf, 1].view(np.uint32), arr.spheres["material"][sid])
+
+
+def test_stress_scene_builds(rtw):
+    objs = rtw.worlds.stress_world(2000, 0)
+    arr = rtw.flatten(objs)
+    nodes = rtw.scene.flatten_bvh(arr)
+    assert len(nodes) == 2 * len(objs) - 1
+
+
+def test_shard_rows_partition(rtw):
+    L = rtw.lib()
+    for H in (1, 7, 800, 2160):
+        for rpb in (1, 8, 16):
+            for n in (1, 2, 3, 8):
+                assert sum(L.rtw_shard_rows(H, rpb, n, s) for s in range(n)) == H
+
+
+def test_invalid_scene_rejected(rtw):
+    objs = rtw.worlds.two_spheres_world()
+    arr = rtw.flatten(objs)
+    arr.materials["texture"][0] = 99
+    d = arr.desc()
+    h = C.c_void_p()
+    rc = rtw.lib().rtw_scene_create(C.byref(d), 0, C.byref(h))
+    assert rc in (rtw._abi.RTW_E_INVALID,)
+    assert b"texture" in rtw.lib().rtw_last_error()

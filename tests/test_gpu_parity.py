@@ -1,0 +1,268 @@
+"""GPU parity: the gfx950 kernels (through the C ABI) against the C oracle.
+
+Tolerance contract: every ray, hit, normal and scatter
+direction is computed with the same fp32 operations as the oracle
+(-ffp-contract=off, correctly rounded div/sqrt, restated Zig pow), so paths are
+identical; only the radiance product is re-associated (iterative L += T*e vs
+the reference's recursive e + a*(...)), bounded by max_depth * 2^-24 relative
+per sample.  Tests assert |gpu - oracle| <= 1e-5 * max(1, |oracle|) per
+channel for the untextured scenes.  The textured scene uses device
+acosf/atan2f/sinf (ocml) against glibc, so a texel index or noise value may
+differ by 1 ulp: there >= 99.5 % of pixels must meet 1e-4 and the image mean 1e-4.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+REL = 1e-5
+
+
+@pytest.fixture(scope="module")
+def book1(rtw):
+    arr = rtw.flatten(rtw.worlds.generate_world(0, "book1"))
+    return arr, rtw.World(arr)
+
+
+@pytest.fixture(scope="module")
+def oracle_book1(oracle):
+    sp, mt, tx = oracle.gen_book1(0, 0)
+    return oracle.World(sp, mt, tx)
+
+
+def close(gpu, ref, rel=REL):
+    return np.abs(gpu - ref) <= rel * np.maximum(1.0, np.abs(ref))
+
+
+def render_rows(rtw, world, cam, y0, y1, spp_begin, spp_end, seed, buf=None):
+    """rtw_render over full rows [y0, y1) (host buffer API)."""
+    W = cam.derived.image_width
+    if buf is None:
+        buf = np.zeros((cam.size, 4), np.float32)
+        buf[:, 3] = 1
+    rc = rtw.lib().rtw_render(world.handle, C.byref(cam.derived), y0 * W, y1 * W, spp_begin, spp_end, seed,
+                              buf.ctypes.data, None, rtw._abi.PROGRESS_FN(0), None)
+    rtw._abi.check(rc, "rtw_render")
+    return buf
+
+
+def test_device_count(rtw):
+    n = C.c_int()
+    rtw.lib().rtw_device_count(C.byref(n))
+    assert n.value >= 1
+
+
+def test_device_rng_bit_exact(rtw, oracle, book1):
+    _, world = book1
+    out = np.zeros(64, np.float32)
+    for seed, pix, s in ((0, 0, 0), (1, 959999, 499), (12345, 77, 3)):
+        rtw._abi.check(rtw.lib().rtw_debug_rng(world.handle, seed, pix, s, 64, out.ctypes.data), "rtw_debug_rng")
+        assert np.array_equal(out, oracle.rng_floats(seed, 0, pix, s, 64))
+
+
+def test_per_sample_radiance(rtw, oracle, book1, oracle_book1):
+    """One sample at a time: GPU device function vs oracle recursion."""
+    _, world = book1
+    cam = rtw.book1_camera().init()
+    ocam = oracle.camera(image_width=1200, aspect_ratio=1.5, samples_per_pixel=500, max_depth=50, background_mode=1)
+    rng = np.random.default_rng(3)
+    out = np.zeros(3, np.float32)
+    n_exact = 0
+    pairs = list(zip(rng.integers(0, cam.size, 300), rng.integers(0, 500, 300)))
+    for pix, s in pairs:
+        rtw._abi.check(rtw.lib().rtw_debug_sample(world.handle, C.byref(cam.derived), 0, int(pix), int(s),
+                                                  out.ctypes.data), "rtw_debug_sample")
+        ref = oracle_book1.sample(ocam, 0, int(pix), int(s))
+        assert close(out, ref).all(), (pix, s, out, ref)
+        n_exact += int(np.array_equal(out, ref))
+    assert n_exact >= len(pairs) // 2   # most paths have <= 2 bounces: bit-exact
+
+
+@pytest.mark.parametrize("name", ["book1_c2_center", "book1_c2_ground", "book1_c2_glass"])
+def test_golden_crops_book1(rtw, book1, name):
+    """Committed oracle float4 crops (tests/golden/crops.npz) vs rtw_render."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("make_golden", os.path.join(GOLDEN, "make_golden.py"))
+    mg = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mg)
+    crop = {c[0]: c for c in mg.CROPS}[name]
+    _, _, camkw, (x0, y0, w, h), spp, seed = crop
+    with np.load(os.path.join(GOLDEN, "crops.npz"), allow_pickle=False) as z:
+        ref, pix = z[name], z[name + "_pix"]
+    _, world = book1
+    cam = rtw.book1_camera(image_width=camkw["image_width"], aspect_ratio=camkw["aspect_ratio"],
+                           spp=camkw["samples_per_pixel"], max_depth=camkw["max_depth"]).init()
+    buf = np.zeros((cam.size, 4), np.float32)
+    render_rows(rtw, world, cam, y0, y0 + h, 0, spp, seed, buf)
+    got = buf[pix]
+    assert np.array_equal(got[:, 3], ref[:, 3])
+    ok = close(got[:, :3], ref[:, :3])
+    assert ok.all(), (np.argwhere(~ok)[:5], np.abs(got[:, :3] - ref[:, :3]).max())
+
+
+def test_golden_crop_ref_head_moving(rtw, earth_rgba):
+    """HEAD scene: moving spheres (initMoving), checker ground, earth texture."""
+    with np.load(os.path.join(GOLDEN, "crops.npz"), allow_pickle=False) as z:
+        ref = z["head_small"]
+    imgs = [rtw.Image(earth_rgba)]
+    world = rtw.World(rtw.flatten(rtw.worlds.generate_world(0, "ref_head", imgs)))
+    cam = rtw.book1_camera(image_width=320, aspect_ratio=16 / 9, spp=8, max_depth=50).init()
+    buf = render_rows(rtw, world, cam, 0, 180, 0, 8, 3)
+    ok = close(buf[:, :3], ref[:, :3], 1e-4)
+    assert ok.all(axis=1).mean() >= 0.995
+    assert abs(buf[:, :3].mean() - ref[:, :3].mean()) <= 1e-4 * abs(ref[:, :3].mean())
+
+
+def test_sky_rows_vs_reference_image2(rtw, book1):
+    """GPU reproduces the reference's own image2.ppm sky rows (+-1 LSB, round-256)."""
+    with np.load(os.path.join(GOLDEN, "sky_rows.npz"), allow_pickle=False) as z:
+        rows = z["image2_rows"].astype(np.int32)
+    _, world = book1
+    cam = rtw.book1_camera(image_width=400, aspect_ratio=16 / 9, spp=64, max_depth=50)
+    cam.pixel_offset = 0
+    cam.init()
+    buf = render_rows(rtw, world, cam, 0, 15, 0, 64, 0)[:15 * 400]
+    g = np.sqrt(buf[:, :3] / buf[:, 3:4])
+    got = np.round(256 * np.clip(g, 0, 0.999)).astype(np.int32).reshape(15, 400, 3)
+    assert np.abs(got - rows).max() <= 1
+
+
+def test_c2_full_size_properties(rtw, oracle, book1, oracle_book1):
+    """BASELINE config 2 geometry (1200x800) at 8 spp: batch invariance, shard
+    invariance, determinism, no NaN, and oracle agreement on 3000 random pixels."""
+    _, world = book1
+    cam = rtw.book1_camera().init()
+    a = render_rows(rtw, world, cam, 0, 800, 0, 8, 0)
+    b = render_rows(rtw, world, cam, 0, 800, 0, 3, 0)
+    b = render_rows(rtw, world, cam, 0, 800, 3, 8, 0, b)
+    assert np.array_equal(a, b)                        # progressive batches == one pass
+    c = render_rows(rtw, world, cam, 0, 800, 0, 8, 0)
+    assert np.array_equal(a, c)                        # deterministic
+    assert np.isfinite(a).all() and (a[:, 3] == 8).all()
+    pix = np.random.default_rng(0).choice(cam.size, 3000, replace=False).astype(np.uint32)
+    ocam = oracle.camera(image_width=1200, aspect_ratio=1.5, samples_per_pixel=500, max_depth=50, background_mode=1)
+    ref = oracle_book1.render_pixels(ocam, 0, pix, 0, 8, threads=os.cpu_count() or 1)
+    assert close(a[pix, :3], ref[:, :3]).all()
+
+
+def test_shard_rows_reassemble(rtw, book1):
+    """rtw_render_rows_device (the multi-GPU unit) reassembles to the 1-GPU image."""
+    import torch
+    _, world = book1
+    cam = rtw.book1_camera(image_width=600, aspect_ratio=1.5, spp=4).init()
+    H, W = cam.derived.image_height, cam.derived.image_width
+    full = render_rows(rtw, world, cam, 0, H, 0, 4, 9)
+    for n_shards, rpb in ((3, 8), (8, 16), (2, 1)):
+        img = np.zeros((H, W, 4), np.float32)
+        for s in range(n_shards):
+            rows = rtw.lib().rtw_shard_rows(H, rpb, n_shards, s)
+            nblk_owned = (((H + rpb - 1) // rpb) - s + n_shards - 1) // n_shards
+            tile = torch.zeros((max(1, nblk_owned * rpb) * W, 4), dtype=torch.float32, device="cuda")
+            rc = rtw.lib().rtw_render_rows_device(world.handle, C.byref(cam.derived), rpb, n_shards, s, 0, 4, 9,
+                                                  tile.data_ptr(), None, None)
+            rtw._abi.check(rc, "rtw_render_rows_device")
+            t = tile.cpu().numpy().reshape(-1, W, 4)
+            ys = [((r // rpb) * n_shards + s) * rpb + r % rpb for r in range(nblk_owned * rpb)]
+            k = 0
+            for r, y in enumerate(ys):
+                if y < H:
+                    img[y] = t[r]
+                    k += 1
+            assert k == rows
+        assert np.array_equal(img.reshape(-1, 4)[:, :3], full[:, :3])
+
+
+def test_reference_task_chunks(rtw, oracle, book1, oracle_book1):
+    """start_render: 8 Tasks of size/8 (main.zig:314-326) == oracle threads render;
+    trailing size % 8 pixels untouched; texture = toGamma2 of the buffer."""
+    arr, world = book1
+    cam = rtw.book1_camera(image_width=203, aspect_ratio=16 / 9, spp=4, max_depth=50)
+    cam.init()
+    writer = rtw.SharedStateImageWriter(cam.image_width, cam.image_height)
+    state = rtw.RayTraceState(cam, writer, world, seed=11)
+    rtw.start_render(state, 8)
+    ocam = oracle.camera(image_width=203, aspect_ratio=16 / 9, samples_per_pixel=4, max_depth=50, background_mode=1)
+    obuf, otex = oracle_book1.render_threads(ocam, 11, 8)
+    chunk = cam.size // 8
+    assert close(writer.buffer[:, :3], obuf[:, :3]).all()
+    assert np.array_equal(writer.buffer[:, 3], obuf[:, 3])
+    assert (writer.buffer[chunk * 8:] == np.array([0, 0, 0, 1], np.float32)).all()
+    same = (writer.buffer == obuf).all(axis=1)
+    assert np.array_equal(writer.texture_buffer[same][:chunk * 8], otex[same][:chunk * 8])
+
+
+def test_cancel_between_batches(rtw, book1):
+    _, world = book1
+    cam = rtw.book1_camera(image_width=300, aspect_ratio=1.5, spp=64).init()
+    writer = rtw.SharedStateImageWriter(cam.image_width, cam.image_height)
+    state = rtw.RayTraceState(cam, writer, world)
+    state.stop()
+    with pytest.raises(rtw.RtwError) as e:
+        cam.render(state, rtw.Task(0, cam.size))
+    assert e.value.code == rtw._abi.RTW_E_CANCELLED
+
+
+def test_textured_c5_crop(rtw, oracle, earth_rgba):
+    """Config 5 (earthmap image texture + Perlin noise) on a 1920x1080 crop."""
+    imgs = [rtw.Image(earth_rgba)]
+    arr = rtw.flatten(rtw.worlds.earth_perlin_world(0, imgs))
+    world = rtw.World(arr)
+    cam = rtw.earth_perlin_camera(image_width=1920, spp=4).init()
+    y0, y1 = 400, 464
+    buf = render_rows(rtw, world, cam, y0, y1, 0, 4, 1)
+    ow = oracle.World(arr.spheres, arr.materials, arr.textures, arr.perlins, [earth_rgba])
+    ocam = oracle.camera(aspect_ratio=16 / 9, image_width=1920, samples_per_pixel=4, max_depth=50,
+                         background=(0.7, 0.8, 1.0), background_mode=0, vfov=30.0, lookat=(0.0, 1.0, 0.0),
+                         defocus_angle=0.0)
+    pix = np.arange(y0 * 1920, y1 * 1920, dtype=np.uint32)
+    ref = ow.render_pixels(ocam, 1, pix, 0, 4, threads=os.cpu_count() or 1)
+    got = buf[pix]
+    ok = close(got[:, :3], ref[:, :3], 1e-4).all(axis=1)
+    assert ok.mean() >= 0.995, ok.mean()
+    assert abs(got[:, :3].mean() - ref[:, :3].mean()) <= 1e-4 * abs(ref[:, :3].mean())
+
+
+def test_stress_100k_crop(rtw, oracle):
+    """Config 4 (100k spheres): deep reference-topology BVH, GPU vs oracle on a strip."""
+    arr = rtw.flatten(rtw.worlds.stress_world(100_000, 0))
+    world = rtw.World(arr)
+    st = world.stats()
+    assert st["n_nodes"] == 2 * len(arr.spheres) - 1
+    cam = rtw.book1_camera(image_width=1920, aspect_ratio=16 / 9, spp=2).init()
+    y0, y1 = 500, 516
+    buf = render_rows(rtw, world, cam, y0, y1, 0, 2, 0)
+    ow = oracle.World(arr.spheres, arr.materials, arr.textures)
+    ocam = oracle.camera(image_width=1920, aspect_ratio=16 / 9, samples_per_pixel=256, max_depth=50,
+                         background_mode=1)
+    pix = np.arange(y0 * 1920, y1 * 1920, dtype=np.uint32)
+    ref = ow.render_pixels(ocam, 0, pix, 0, 2, threads=os.cpu_count() or 1)
+    assert close(buf[pix, :3], ref[:, :3]).all()
+
+
+def test_device_counters_equal_reference_traversal(rtw, oracle, book1, oracle_book1):
+    """The stackless walk visits exactly the reference's nodes: device ray/node/leaf
+    counters == oracle's instrumented recursion on the same pixels."""
+    import torch
+    _, world = book1
+    cam = rtw.book1_camera(image_width=1200, aspect_ratio=1.5, spp=2).init()
+    y0, y1 = 300, 332
+    acc = torch.zeros((cam.size, 4), dtype=torch.float32, device="cuda")
+    cnt = torch.zeros(8, dtype=torch.int64, device="cuda")
+    opts = rtw._abi.RtwRenderOpts(0, 0, cnt.data_ptr())
+    rc = rtw.lib().rtw_render_device(world.handle, C.byref(cam.derived), y0 * 1200, y1 * 1200, 0, 2, 0,
+                                     acc.data_ptr(), None, C.byref(opts))
+    rtw._abi.check(rc, "rtw_render_device")
+    g = cnt.cpu().numpy()
+    ocam = oracle.camera(image_width=1200, aspect_ratio=1.5, samples_per_pixel=500, max_depth=50, background_mode=1)
+    pix = np.arange(y0 * 1200, y1 * 1200, dtype=np.uint32)
+    with oracle.counters() as oc:
+        oracle_book1.render_pixels(ocam, 0, pix, 0, 2, threads=1)
+    assert g[rtw._abi.RTW_STAT_SAMPLES] == oc.samples
+    assert g[rtw._abi.RTW_STAT_RAYS] == oc.rays
+    assert g[rtw._abi.RTW_STAT_NODES] == oc.nodes
+    assert g[rtw._abi.RTW_STAT_LEAVES] == oc.leaves

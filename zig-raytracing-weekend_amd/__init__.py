@@ -1,0 +1,20 @@
+"""zig-raytracing-weekend_amd -- MI355X-native drop-in for the per-pixel sample
+loop of dariooddenino/zig-raytracing-weekend (src/camera.zig:93-208).
+
+Host API (mirrors the reference's Zig API names):
+  scene:   SolidColor, CheckerTexture, ImageTexture, NoiseTexture, Perlin,
+           Lambertian, Metal, Dielectric, DiffuseLight, Isotropic,
+           Sphere.init / Sphere.initMoving, BVHTree.init -> World
+  camera:  Camera (+ init, render(state, task)), SharedStateImageWriter, Task,
+           RayTraceState, start_render
+  worlds:  generate_world, earth_world, two_spheres_world, two_perlin_world,
+           stress_world, earth_perlin_world
+The hot path runs in librtw_gpu.so (include/rtw_gpu.h) on gfx950.
+"""
+from . import _abi, configs, rng, worlds  # noqa: F401
+from ._abi import RtwError, lib  # noqa: F401
+from .camera import (Camera, RayTraceState, SharedStateImageWriter, Task, book1_camera,  # noqa: F401
+                     earth_perlin_camera, start_render)
+from .scene import (BVHTree, CheckerTexture, Dielectric, DiffuseLight, Image, ImageTexture,  # noqa: F401
+                    Isotropic, Lambertian, Metal, NoiseTexture, Perlin, SceneArrays, SolidColor, Sphere, World,
+                    flatten)

@@ -1,0 +1,146 @@
+"""ctypes binding of include/rtw_gpu.h (librtw_gpu.so, built in-tree by build()).
+
+This is the Python stand-in for the FFI a Zig host would get from
+``@cImport(@cInclude("rtw_gpu.h"))``.  Loading fails loudly if
+the HIP library has not been built: there is no CPU fallback in the product.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "librtw_gpu.so")
+
+RTW_OK, RTW_E_INVALID, RTW_E_HIP, RTW_E_OOM, RTW_E_CANCELLED, RTW_E_NODEVICE = 0, -1, -2, -3, -4, -5
+RTW_MAT_LAMBERTIAN, RTW_MAT_METAL, RTW_MAT_DIELECTRIC, RTW_MAT_DIFFUSE_LIGHT, RTW_MAT_ISOTROPIC = range(5)
+RTW_TEX_SOLID, RTW_TEX_CHECKER, RTW_TEX_IMAGE, RTW_TEX_NOISE = range(4)
+RTW_BG_CONSTANT, RTW_BG_GRADIENT = 0, 1
+RTW_BVH_REFERENCE = 0
+RTW_RENDER_NO_SYNC = 1
+RTW_STAT_RAYS, RTW_STAT_NODES, RTW_STAT_LEAVES, RTW_STAT_SAMPLES, RTW_STAT_NAN, RTW_STAT_COUNT = 0, 1, 2, 3, 4, 8
+
+# numpy record layouts == the C structs (asserted against sizeof in tests)
+SPHERE_DT = np.dtype([("center1", "<f4", 3), ("radius", "<f4"), ("center2", "<f4", 3), ("is_moving", "<u4"),
+                      ("material", "<u4"), ("_pad", "<u4", 3)])
+MATERIAL_DT = np.dtype([("kind", "<u4"), ("texture", "<u4"), ("fuzz", "<f4"), ("ir", "<f4"),
+                        ("albedo", "<f4", 3), ("_pad", "<f4")])
+TEXTURE_DT = np.dtype([("kind", "<u4"), ("image", "<u4"), ("perlin", "<u4"), ("scale", "<f4"),
+                       ("even", "<f4", 3), ("_p0", "<f4"), ("odd", "<f4", 3), ("_p1", "<f4")])
+PERLIN_DT = np.dtype([("ranvec", "<f4", (256, 3)), ("perm_x", "<u2", 256), ("perm_y", "<u2", 256),
+                      ("perm_z", "<u2", 256)])
+NODE_DT = np.dtype([("a", "<f4", 4), ("b", "<f4", 4)])
+assert SPHERE_DT.itemsize == 48 and MATERIAL_DT.itemsize == 32 and TEXTURE_DT.itemsize == 48
+assert PERLIN_DT.itemsize == 4608 and NODE_DT.itemsize == 32
+
+
+class RtwImage(C.Structure):
+    _fields_ = [("data", C.c_void_p), ("width", C.c_uint32), ("height", C.c_uint32),
+                ("bytes_per_row", C.c_uint32), ("_pad", C.c_uint32)]
+
+
+class RtwSceneDesc(C.Structure):
+    _fields_ = [("spheres", C.c_void_p), ("n_spheres", C.c_uint32),
+                ("materials", C.c_void_p), ("n_materials", C.c_uint32),
+                ("textures", C.c_void_p), ("n_textures", C.c_uint32),
+                ("images", C.c_void_p), ("n_images", C.c_uint32),
+                ("perlins", C.c_void_p), ("n_perlins", C.c_uint32),
+                ("bvh_seed", C.c_uint64), ("bvh_mode", C.c_uint32), ("_pad", C.c_uint32)]
+
+
+F3 = C.c_float * 3
+
+
+class RtwCameraParams(C.Structure):
+    _fields_ = [("aspect_ratio", C.c_float), ("image_width", C.c_uint32), ("image_height", C.c_uint32),
+                ("samples_per_pixel", C.c_uint32), ("max_depth", C.c_uint32), ("background_mode", C.c_uint32),
+                ("background", F3), ("vfov", C.c_float), ("lookfrom", F3), ("lookat", F3), ("vup", F3),
+                ("defocus_angle", C.c_float), ("focus_dist", C.c_float), ("pixel_offset", C.c_uint32)]
+
+
+class RtwCamera(C.Structure):
+    _fields_ = [("image_width", C.c_uint32), ("image_height", C.c_uint32), ("size", C.c_uint32),
+                ("samples_per_pixel", C.c_uint32), ("max_depth", C.c_uint32), ("background_mode", C.c_uint32),
+                ("pixel_offset", C.c_uint32), ("_pad", C.c_uint32),
+                ("center", F3), ("pixel00_loc", F3), ("pixel_delta_u", F3), ("pixel_delta_v", F3),
+                ("u", F3), ("v", F3), ("w", F3), ("defocus_disk_u", F3), ("defocus_disk_v", F3),
+                ("defocus_angle", C.c_float), ("background", F3)]
+
+
+class RtwRenderOpts(C.Structure):
+    _fields_ = [("spp_batch", C.c_uint32), ("flags", C.c_uint32), ("counters", C.c_void_p)]
+
+
+class RtwSceneStats(C.Structure):
+    _fields_ = [("n_nodes", C.c_uint32), ("n_leaves", C.c_uint32), ("n_inner", C.c_uint32), ("depth", C.c_uint32),
+                ("device_bytes", C.c_uint64), ("axis_draws", C.c_uint32), ("_pad", C.c_uint32)]
+
+
+PROGRESS_FN = C.CFUNCTYPE(C.c_int, C.c_uint64, C.c_uint64, C.c_void_p)
+
+# every symbol include/rtw_gpu.h declares: name -> (restype, argtypes)
+SIGNATURES = {
+    "rtw_version": (C.c_int, []),
+    "rtw_last_error": (C.c_char_p, []),
+    "rtw_device_count": (C.c_int, [C.POINTER(C.c_int)]),
+    "rtw_camera_init": (C.c_int, [C.POINTER(RtwCameraParams), C.POINTER(RtwCamera)]),
+    "rtw_scene_create": (C.c_int, [C.POINTER(RtwSceneDesc), C.c_int, C.POINTER(C.c_void_p)]),
+    "rtw_scene_destroy": (None, [C.c_void_p]),
+    "rtw_render": (C.c_int, [C.c_void_p, C.POINTER(RtwCamera), C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
+                             C.c_uint64, C.c_void_p, C.c_void_p, PROGRESS_FN, C.c_void_p]),
+    "rtw_render_device": (C.c_int, [C.c_void_p, C.POINTER(RtwCamera), C.c_uint32, C.c_uint32, C.c_uint32,
+                                    C.c_uint32, C.c_uint64, C.c_void_p, C.c_void_p, C.POINTER(RtwRenderOpts)]),
+    "rtw_render_rows_device": (C.c_int, [C.c_void_p, C.POINTER(RtwCamera), C.c_uint32, C.c_uint32, C.c_uint32,
+                                         C.c_uint32, C.c_uint32, C.c_uint64, C.c_void_p, C.c_void_p,
+                                         C.POINTER(RtwRenderOpts)]),
+    "rtw_shard_rows": (C.c_uint32, [C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32]),
+    "rtw_texture_from_accum": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p]),
+    "rtw_scene_flatten": (C.c_int, [C.POINTER(RtwSceneDesc), C.c_void_p, C.c_uint32, C.POINTER(C.c_uint32),
+                                    C.POINTER(C.c_uint32)]),
+    "rtw_scene_stats_get": (C.c_int, [C.c_void_p, C.POINTER(RtwSceneStats)]),
+    "rtw_scene_nodes": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.POINTER(C.c_uint32)]),
+    "rtw_debug_rng": (C.c_int, [C.c_void_p, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_void_p]),
+    "rtw_debug_sample": (C.c_int, [C.c_void_p, C.POINTER(RtwCamera), C.c_uint64, C.c_uint32, C.c_uint32,
+                                   C.c_void_p]),
+}
+
+_lib = None
+
+
+class RtwError(RuntimeError):
+    def __init__(self, code: int, where: str, msg: str):
+        super().__init__(f"{where} failed ({code}): {msg}")
+        self.code = code
+
+
+def lib() -> C.CDLL:
+    """Load librtw_gpu.so (raises if the HIP extension was not built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"librtw_gpu.so not built at {LIB_PATH}: run __graft_entry__.build() "
+                              "(the product has no CPU fallback)")
+        # torch (if present) must own the HIP runtime first: load it before us so the
+        # soname libamdhip64.so.7 resolves to one runtime per process.
+        try:
+            import torch  # noqa: F401
+        except Exception:
+            pass
+        L = C.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(code: int, where: str) -> None:
+    if code != RTW_OK:
+        raise RtwError(code, where, lib().rtw_last_error().decode(errors="replace"))
+
+
+def ptr(a: np.ndarray) -> int:
+    return a.ctypes.data if a is not None and a.size else 0

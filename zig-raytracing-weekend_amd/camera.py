@@ -1,0 +1,174 @@
+"""Camera / SharedStateImageWriter / Task mirror of src/camera.zig, with
+``Camera.render`` routed through the C ABI to the gfx950 kernels.
+
+Reference call stack being replaced (src/main.zig:49-69, 314-326)::
+
+    startRender -> 8 x RenderThread.start(Task{thread_idx, chunk_size = size/8})
+        -> renderFn -> Camera.render(raytrace, task)        (src/camera.zig:93-116)
+
+Here ``Camera.render(state, task)`` issues ONE ``rtw_render`` for the task's
+pixel chunk and the whole sample range; the per-sample loop runs on the GPU.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass, field
+from typing import Callable, Optional
+
+import numpy as np
+
+from . import _abi
+from .scene import World
+
+
+@dataclass
+class Task:
+    """camera.zig:19"""
+    thread_idx: int
+    chunk_size: int
+
+
+class SharedStateImageWriter:
+    """camera.zig:22-67: float4 ColorAndSamples buffer + u8 RGBA texture."""
+
+    def __init__(self, image_width: int, image_height: int):
+        self.width, self.height = int(image_width), int(image_height)
+        n = self.width * self.height
+        self.buffer = np.zeros((n, 4), np.float32)
+        self.buffer[:, 3] = 1.0                      # init / scrub: {0,0,0,1} (camera.zig:34-45)
+        self.texture_buffer = np.zeros((n, 4), np.uint8)
+
+    def scrub(self):
+        self.buffer[:] = 0.0
+        self.buffer[:, 3] = 1.0
+
+    def update_texture(self, begin: int = 0, end: Optional[int] = None):
+        """toGamma2 texel update of writeColor (camera.zig:58-65) for [begin, end)."""
+        end = self.buffer.shape[0] if end is None else end
+        if end <= begin:
+            return
+        src = np.ascontiguousarray(self.buffer[begin:end])
+        dst = np.zeros((end - begin, 4), np.uint8)
+        _abi.check(_abi.lib().rtw_texture_from_accum(src.ctypes.data, end - begin, dst.ctypes.data),
+                   "rtw_texture_from_accum")
+        self.texture_buffer[begin:end] = dst
+
+    def image(self) -> np.ndarray:
+        return self.texture_buffer.reshape(self.height, self.width, 4)
+
+
+@dataclass
+class Camera:
+    """camera.zig:69-91 (defaults are the reference's), plus the two knobs the
+    reference hard-codes: background_mode (gradient = the commented Book-1 sky,
+    camera.zig:204-206) and pixel_offset (the +1 of camera.zig:100-101)."""
+    aspect_ratio: float = 16.0 / 9.0
+    image_width: int = 800
+    image_height: int = 0
+    samples_per_pixel: int = 100
+    max_depth: int = 16
+    background: tuple = (0.0, 0.0, 0.0)
+    background_mode: int = _abi.RTW_BG_CONSTANT
+    vfov: float = 20.0
+    lookfrom: tuple = (13.0, 2.0, 3.0)
+    lookat: tuple = (0.0, 0.0, 0.0)
+    vup: tuple = (0.0, 1.0, 0.0)
+    defocus_angle: float = 0.6
+    focus_dist: float = 10.0
+    pixel_offset: int = 1
+    derived: Optional[_abi.RtwCamera] = field(default=None, repr=False)
+
+    def params(self) -> _abi.RtwCameraParams:
+        p = _abi.RtwCameraParams()
+        p.aspect_ratio = self.aspect_ratio
+        p.image_width = self.image_width
+        p.image_height = self.image_height
+        p.samples_per_pixel = self.samples_per_pixel
+        p.max_depth = self.max_depth
+        p.background_mode = self.background_mode
+        p.background[:] = list(self.background)
+        p.vfov = self.vfov
+        p.lookfrom[:] = list(self.lookfrom)
+        p.lookat[:] = list(self.lookat)
+        p.vup[:] = list(self.vup)
+        p.defocus_angle = self.defocus_angle
+        p.focus_dist = self.focus_dist
+        p.pixel_offset = self.pixel_offset
+        return p
+
+    def init(self) -> "Camera":
+        """Camera.init (camera.zig:118-154) via rtw_camera_init."""
+        c = _abi.RtwCamera()
+        _abi.check(_abi.lib().rtw_camera_init(C.byref(self.params()), C.byref(c)), "rtw_camera_init")
+        self.derived = c
+        if self.image_height == 0:
+            self.image_height = c.image_height
+        return self
+
+    @property
+    def size(self) -> int:
+        return int(self.derived.size)
+
+    def render(self, state: "RayTraceState", task: Task) -> None:
+        """Camera.render (camera.zig:93-116) for one Task, all samples."""
+        if self.derived is None:
+            self.init()
+        start = task.thread_idx * task.chunk_size
+        end = start + task.chunk_size
+        self.render_range(state, start, end, 0, self.samples_per_pixel)
+
+    def render_range(self, state: "RayTraceState", pix_begin: int, pix_end: int, spp_begin: int, spp_end: int,
+                     progress: Optional[Callable[[int, int], bool]] = None) -> None:
+        w = state.writer
+        buf = w.buffer
+        assert buf.flags["C_CONTIGUOUS"] and buf.dtype == np.float32 and buf.shape == (self.size, 4)
+        cb = _abi.PROGRESS_FN(0)
+        if progress is not None:
+            cb = _abi.PROGRESS_FN(lambda done, total, user: 1 if progress(done, total) else 0)
+        rc = _abi.lib().rtw_render(state.world.handle, C.byref(self.derived), pix_begin, pix_end, spp_begin,
+                                   spp_end, state.seed, buf.ctypes.data, C.addressof(state.cancel), cb, None)
+        _abi.check(rc, "rtw_render")
+        w.update_texture(pix_begin, pix_end)
+
+
+@dataclass
+class RayTraceState:
+    """The parts of RayTraceState (src/main.zig:71-86) the render path reads."""
+    camera: Camera
+    writer: SharedStateImageWriter
+    world: World
+    seed: int = 0
+    cancel: C.c_int32 = field(default_factory=lambda: C.c_int32(0))
+
+    def stop(self):
+        """RenderThread.stop (src/main.zig:58-60): polled between sample batches."""
+        self.cancel.value = 1
+
+
+def start_render(state: RayTraceState, number_of_threads: int = 8) -> None:
+    """startRender (src/main.zig:314-326): scrub, Camera.init, 8 Tasks of size/8.
+
+    The Tasks are issued back to back on the GPU (each one is a whole-chunk,
+    all-samples launch sequence); the trailing size % 8 pixels are left
+    unrendered exactly like the reference."""
+    state.writer.scrub()
+    state.camera.init()
+    chunk = state.camera.size // number_of_threads
+    for t in range(number_of_threads):
+        state.camera.render(state, Task(t, chunk))
+
+
+# ------------------------------------------------------------------ presets
+def book1_camera(image_width: int = 1200, aspect_ratio: float = 1.5, spp: int = 500, max_depth: int = 50,
+                 image_height: int = 0) -> Camera:
+    """Book-1 cover camera (camera.zig defaults + gradient sky), BASELINE config 2 by default."""
+    return Camera(aspect_ratio=aspect_ratio, image_width=image_width, image_height=image_height,
+                  samples_per_pixel=spp, max_depth=max_depth, background_mode=_abi.RTW_BG_GRADIENT,
+                  vfov=20.0, lookfrom=(13.0, 2.0, 3.0), lookat=(0.0, 0.0, 0.0), defocus_angle=0.6, focus_dist=10.0)
+
+
+def earth_perlin_camera(image_width: int = 1920, spp: int = 512, max_depth: int = 50) -> Camera:
+    """BASELINE config 5: constant (0.7,0.8,1.0) sky as RTNW, no defocus."""
+    return Camera(aspect_ratio=16.0 / 9.0, image_width=image_width, samples_per_pixel=spp, max_depth=max_depth,
+                  background=(0.7, 0.8, 1.0), background_mode=_abi.RTW_BG_CONSTANT, vfov=30.0,
+                  lookfrom=(13.0, 2.0, 3.0), lookat=(0.0, 1.0, 0.0), defocus_angle=0.0, focus_dist=10.0)

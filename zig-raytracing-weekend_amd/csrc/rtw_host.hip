@@ -1,0 +1,515 @@
+// rtw_host.hip -- C ABI implementation (include/rtw_gpu.h): scene upload,
+// Camera.init, batched launches with cancel/progress, sharded row rendering.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/rtw_gpu.h"
+#include "rtw_internal.h"
+#include "rtw_layout.h"
+#include "rtw_rng.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* msg) {
+    g_err = msg;
+    return code;
+}
+
+int hip_fail(hipError_t e, const char* where) {
+    g_err = std::string(where) + ": " + hipGetErrorString(e);
+    return e == hipErrorOutOfMemory ? RTW_E_OOM : RTW_E_HIP;
+}
+
+#define HIP_TRY(expr)                                   \
+    do {                                                \
+        hipError_t _e = (expr);                         \
+        if (_e != hipSuccess) return hip_fail(_e, #expr); \
+    } while (0)
+
+}  // namespace
+
+struct rtw_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    void* d_blob = nullptr;       // single allocation holding every scene array
+    size_t blob_bytes = 0;
+    rtw_launch base{};
+    rtw_scene_stats stats{};
+    std::vector<rtw_node> nodes_host;
+    float* d_scratch = nullptr;    // host-API accum staging
+    size_t scratch_bytes = 0;
+    float* d_dbg = nullptr;        // debug kernels output
+};
+
+extern "C" {
+
+int rtw_version(void) { return RTW_ABI_VERSION; }
+
+const char* rtw_last_error(void) { return g_err.c_str(); }
+
+int rtw_device_count(int* out) {
+    if (!out) return fail(RTW_E_INVALID, "null out");
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) n = 0;
+    *out = n;
+    return RTW_OK;
+}
+
+// Camera.init (src/camera.zig:118-154).  Plain fp32 host arithmetic in the
+// Zig expression order; tan is the host libm (the Zig std tan is a musl port).
+int rtw_camera_init(const rtw_camera_params* p, rtw_camera* c) {
+#pragma STDC FP_CONTRACT OFF
+    if (!p || !c) return fail(RTW_E_INVALID, "null camera params");
+    if (p->image_width == 0) return fail(RTW_E_INVALID, "image_width == 0");
+    std::memset(c, 0, sizeof *c);
+    uint32_t H = p->image_height;
+    if (H == 0) H = (uint32_t)std::round((float)p->image_width / p->aspect_ratio);
+    if (H < 1) H = 1;
+    const uint32_t W = p->image_width;
+    c->image_width = W;
+    c->image_height = H;
+    c->size = W * H;
+    c->samples_per_pixel = p->samples_per_pixel;
+    c->max_depth = p->max_depth;
+    c->background_mode = p->background_mode;
+    c->pixel_offset = p->pixel_offset;
+    for (int k = 0; k < 3; k++) c->background[k] = p->background[k];
+    const float pi = 3.1415926535897932385f;
+    const float theta = p->vfov * pi / 180.0f;
+    const float h = std::tan(theta / 2.0f);
+    const float vh = 2 * h * p->focus_dist;
+    const float vw = vh * ((float)W / (float)H);
+    float w[3], u[3], v[3], tmp[3];
+    for (int k = 0; k < 3; k++) tmp[k] = p->lookfrom[k] - p->lookat[k];
+    auto unit = [](const float* a, float* o) {
+        float l = std::sqrt(a[0] * a[0] + a[1] * a[1] + a[2] * a[2]);
+        for (int k = 0; k < 3; k++) o[k] = a[k] / l;
+    };
+    auto cross = [](const float* a, const float* b, float* o) {
+        o[0] = a[1] * b[2] - a[2] * b[1];
+        o[1] = a[2] * b[0] - a[0] * b[2];
+        o[2] = a[0] * b[1] - a[1] * b[0];
+    };
+    unit(tmp, w);
+    cross(p->vup, w, tmp);
+    unit(tmp, u);
+    cross(w, u, v);
+    float vu[3], vv[3];
+    for (int k = 0; k < 3; k++) {
+        vu[k] = vw * u[k];
+        vv[k] = vh * -v[k];
+        c->pixel_delta_u[k] = vu[k] / (float)W;
+        c->pixel_delta_v[k] = vv[k] / (float)H;
+        const float upper_left = ((p->lookfrom[k] - p->focus_dist * w[k]) - vu[k] / 2.0f) - vv[k] / 2.0f;
+        c->pixel00_loc[k] = upper_left + 0.5f * (c->pixel_delta_u[k] + c->pixel_delta_v[k]);
+        c->center[k] = p->lookfrom[k];
+        c->u[k] = u[k];
+        c->v[k] = v[k];
+        c->w[k] = w[k];
+    }
+    const float defocus_radius = p->focus_dist * std::tan((p->defocus_angle / 2.0f) * pi / 180.0f);
+    for (int k = 0; k < 3; k++) {
+        c->defocus_disk_u[k] = u[k] * defocus_radius;
+        c->defocus_disk_v[k] = v[k] * defocus_radius;
+    }
+    c->defocus_angle = p->defocus_angle;
+    return RTW_OK;
+}
+
+int rtw_scene_create(const rtw_scene_desc* d, int device, rtw_ctx** out) {
+    if (!d || !out) return fail(RTW_E_INVALID, "null scene desc");
+    *out = nullptr;
+    if (d->n_spheres == 0 || !d->spheres) return fail(RTW_E_INVALID, "scene has no spheres");
+    if (d->n_materials == 0 || !d->materials) return fail(RTW_E_INVALID, "scene has no materials");
+    for (uint32_t i = 0; i < d->n_spheres; i++)
+        if (d->spheres[i].material >= d->n_materials) return fail(RTW_E_INVALID, "sphere material index out of range");
+    for (uint32_t i = 0; i < d->n_materials; i++) {
+        const rtw_material& m = d->materials[i];
+        if (m.kind > RTW_MAT_ISOTROPIC) return fail(RTW_E_INVALID, "unknown material kind");
+        const bool textured = m.kind == RTW_MAT_LAMBERTIAN || m.kind == RTW_MAT_DIFFUSE_LIGHT || m.kind == RTW_MAT_ISOTROPIC;
+        if (textured && m.texture >= d->n_textures) return fail(RTW_E_INVALID, "material texture index out of range");
+    }
+    for (uint32_t i = 0; i < d->n_textures; i++) {
+        const rtw_texture& t = d->textures[i];
+        if (t.kind > RTW_TEX_NOISE) return fail(RTW_E_INVALID, "unknown texture kind");
+        if (t.kind == RTW_TEX_IMAGE && t.image >= d->n_images) return fail(RTW_E_INVALID, "texture image index out of range");
+        if (t.kind == RTW_TEX_NOISE && t.perlin >= d->n_perlins) return fail(RTW_E_INVALID, "texture perlin index out of range");
+    }
+    for (uint32_t i = 0; i < d->n_images; i++) {
+        const rtw_image& im = d->images[i];
+        if (im.width && im.height && (!im.data || im.bytes_per_row < 4 * im.width))
+            return fail(RTW_E_INVALID, "bad image");
+    }
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(RTW_E_NODEVICE, "no HIP device visible");
+    if (device < 0 || device >= ndev) return fail(RTW_E_INVALID, "device index out of range");
+
+    rtw_ctx* ctx = new rtw_ctx();
+    ctx->device = device;
+    std::vector<float> cvec;
+    uint32_t depth = 0, draws = 0;
+    int rc = rtw_build_bvh(*d, ctx->nodes_host, cvec, &depth, &draws);
+    if (rc != RTW_OK) {
+        delete ctx;
+        return fail(rc, "BVH build failed (unknown bvh_mode?)");
+    }
+
+    // Blob layout (each section 256-B aligned): nodes | cvec | materials | textures | images-info | perlin | image bytes
+    auto align = [](size_t x) { return (x + 255) & ~size_t(255); };
+    const size_t n_nodes = ctx->nodes_host.size();
+    size_t off = 0;
+    const size_t o_nodes = off; off = align(off + n_nodes * sizeof(rtw_node));
+    const size_t o_cvec = off; off = align(off + cvec.size() * sizeof(float) + 16);
+    const size_t o_mats = off; off = align(off + d->n_materials * sizeof(rtw_dev_material));
+    const size_t o_texs = off; off = align(off + (d->n_textures + 1) * sizeof(rtw_dev_texture));
+    const size_t o_imgi = off; off = align(off + (d->n_images + 1) * sizeof(rtw_dev_image));
+    const size_t o_perl = off; off = align(off + (size_t)(d->n_perlins + 1) * RTW_PERLIN_BYTES);
+    const size_t o_imgs = off;
+    std::vector<rtw_dev_image> img_info(d->n_images + 1);
+    size_t img_bytes = 0;
+    for (uint32_t i = 0; i < d->n_images; i++) {
+        img_info[i].offset = img_bytes;
+        img_info[i].width = d->images[i].width;
+        img_info[i].height = d->images[i].height;
+        img_info[i].bytes_per_row = d->images[i].bytes_per_row;
+        img_bytes += align((size_t)d->images[i].bytes_per_row * d->images[i].height);
+    }
+    off = align(off + img_bytes + 16);
+
+    std::vector<uint8_t> blob(off, 0);
+    std::memcpy(blob.data() + o_nodes, ctx->nodes_host.data(), n_nodes * sizeof(rtw_node));
+    if (!cvec.empty()) std::memcpy(blob.data() + o_cvec, cvec.data(), cvec.size() * sizeof(float));
+    for (uint32_t i = 0; i < d->n_materials; i++) {
+        rtw_dev_material m{};
+        m.kind = d->materials[i].kind;
+        m.texture = d->materials[i].texture;
+        m.fuzz = d->materials[i].fuzz;
+        m.ir = d->materials[i].ir;
+        for (int k = 0; k < 3; k++) m.albedo[k] = d->materials[i].albedo[k];
+        std::memcpy(blob.data() + o_mats + i * sizeof m, &m, sizeof m);
+    }
+    for (uint32_t i = 0; i < d->n_textures; i++) {
+        rtw_dev_texture t{};
+        const rtw_texture& s = d->textures[i];
+        t.kind = s.kind; t.image = s.image; t.perlin = s.perlin; t.scale = s.scale;
+        for (int k = 0; k < 3; k++) { t.even[k] = s.even[k]; t.odd[k] = s.odd[k]; }
+        std::memcpy(blob.data() + o_texs + i * sizeof t, &t, sizeof t);
+    }
+    std::memcpy(blob.data() + o_imgi, img_info.data(), img_info.size() * sizeof(rtw_dev_image));
+    for (uint32_t i = 0; i < d->n_perlins; i++) {
+        uint8_t* base = blob.data() + o_perl + (size_t)i * RTW_PERLIN_BYTES;
+        float* vec = reinterpret_cast<float*>(base);
+        for (int k = 0; k < 256; k++) {
+            vec[4 * k + 0] = d->perlins[i].ranvec[k][0];
+            vec[4 * k + 1] = d->perlins[i].ranvec[k][1];
+            vec[4 * k + 2] = d->perlins[i].ranvec[k][2];
+            vec[4 * k + 3] = 0.0f;
+        }
+        uint32_t* perm = reinterpret_cast<uint32_t*>(base + 256 * 16);
+        for (int k = 0; k < 256; k++) {
+            perm[k] = d->perlins[i].perm_x[k];
+            perm[256 + k] = d->perlins[i].perm_y[k];
+            perm[512 + k] = d->perlins[i].perm_z[k];
+        }
+    }
+    for (uint32_t i = 0; i < d->n_images; i++) {
+        const size_t nb = (size_t)d->images[i].bytes_per_row * d->images[i].height;
+        if (nb) std::memcpy(blob.data() + o_imgs + img_info[i].offset, d->images[i].data, nb);
+    }
+
+    hipError_t e = hipSetDevice(device);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipMalloc(&ctx->d_blob, off);
+    if (e == hipSuccess) e = hipMemcpy(ctx->d_blob, blob.data(), off, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMalloc(&ctx->d_dbg, 64 * sizeof(float));
+    if (e != hipSuccess) {
+        int code = hip_fail(e, "rtw_scene_create upload");
+        rtw_scene_destroy(ctx);
+        return code;
+    }
+    ctx->blob_bytes = off;
+    uint8_t* dev = static_cast<uint8_t*>(ctx->d_blob);
+    rtw_launch& L = ctx->base;
+    L.nodes = reinterpret_cast<const float4*>(dev + o_nodes);
+    L.cvec = reinterpret_cast<const float4*>(dev + o_cvec);
+    L.mats = reinterpret_cast<const rtw_dev_material*>(dev + o_mats);
+    L.texs = reinterpret_cast<const rtw_dev_texture*>(dev + o_texs);
+    L.img_info = reinterpret_cast<const rtw_dev_image*>(dev + o_imgi);
+    L.perlin = reinterpret_cast<const float4*>(dev + o_perl);
+    L.images = dev + o_imgs;
+    L.n_nodes = (uint32_t)n_nodes;
+    L.n_perlin = d->n_perlins;
+
+    ctx->stats.n_nodes = (uint32_t)n_nodes;
+    ctx->stats.n_leaves = d->n_spheres;
+    ctx->stats.n_inner = (uint32_t)n_nodes - d->n_spheres;
+    ctx->stats.depth = depth;
+    ctx->stats.device_bytes = off;
+    ctx->stats.axis_draws = draws;
+    *out = ctx;
+    return RTW_OK;
+}
+
+void rtw_scene_destroy(rtw_ctx* ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->d_blob) (void)hipFree(ctx->d_blob);
+    if (ctx->d_scratch) (void)hipFree(ctx->d_scratch);
+    if (ctx->d_dbg) (void)hipFree(ctx->d_dbg);
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+int rtw_scene_flatten(const rtw_scene_desc* d, void* out, uint32_t cap, uint32_t* n_out, uint32_t* depth_out) {
+    if (!d || d->n_spheres == 0 || !d->spheres) return fail(RTW_E_INVALID, "scene has no spheres");
+    std::vector<rtw_node> nodes;
+    std::vector<float> cvec;
+    uint32_t depth = 0, draws = 0;
+    int rc = rtw_build_bvh(*d, nodes, cvec, &depth, &draws);
+    if (rc != RTW_OK) return fail(rc, "BVH build failed");
+    const uint32_t n = (uint32_t)nodes.size();
+    if (n_out) *n_out = n;
+    if (depth_out) *depth_out = depth;
+    if (out) std::memcpy(out, nodes.data(), sizeof(rtw_node) * (cap < n ? cap : n));
+    return RTW_OK;
+}
+
+int rtw_scene_stats_get(rtw_ctx* ctx, rtw_scene_stats* out) {
+    if (!ctx || !out) return fail(RTW_E_INVALID, "null ctx");
+    *out = ctx->stats;
+    return RTW_OK;
+}
+
+int rtw_scene_nodes(rtw_ctx* ctx, void* out, uint32_t cap, uint32_t* n_out) {
+    if (!ctx) return fail(RTW_E_INVALID, "null ctx");
+    const uint32_t n = (uint32_t)ctx->nodes_host.size();
+    if (n_out) *n_out = n;
+    if (out) std::memcpy(out, ctx->nodes_host.data(), sizeof(rtw_node) * (cap < n ? cap : n));
+    return RTW_OK;
+}
+
+}  // extern "C"
+
+namespace {
+
+rtw_launch make_launch(const rtw_ctx* ctx, const rtw_camera* c, uint64_t seed) {
+    rtw_launch L = ctx->base;
+    for (int k = 0; k < 3; k++) {
+        L.center[k] = c->center[k];
+        L.pixel00[k] = c->pixel00_loc[k];
+        L.du[k] = c->pixel_delta_u[k];
+        L.dv[k] = c->pixel_delta_v[k];
+        L.disk_u[k] = c->defocus_disk_u[k];
+        L.disk_v[k] = c->defocus_disk_v[k];
+        L.background[k] = c->background[k];
+    }
+    L.defocus_angle = c->defocus_angle;
+    L.W = c->image_width;
+    L.H = c->image_height;
+    L.max_depth = c->max_depth;
+    L.bg_mode = c->background_mode;
+    L.pixel_offset = c->pixel_offset;
+    L.key0 = rtw_mix64(seed);
+    return L;
+}
+
+uint32_t auto_batch(uint64_t pixels, uint32_t spp) {
+    // ~64M samples per launch: long enough to amortise the launch, short enough to poll cancel
+    uint64_t b = pixels ? (64ull << 20) / pixels : spp;
+    if (b < 1) b = 1;
+    if (b > spp) b = spp;
+    return (uint32_t)b;
+}
+
+int validate_cam(const rtw_camera* cam) {
+    if (!cam) return fail(RTW_E_INVALID, "null camera");
+    if (cam->image_width == 0 || cam->image_height == 0) return fail(RTW_E_INVALID, "camera not initialised");
+    if ((uint64_t)cam->image_width * cam->image_height > 0xFFFFFFFFull) return fail(RTW_E_INVALID, "image too large");
+    return RTW_OK;
+}
+
+// Enqueue [s0, s1) in batches on `stream`, polling cancel/progress between
+// batches when `sync_each` (host API).  Returns status.
+int run_batches(rtw_ctx* ctx, rtw_launch L, uint32_t s0, uint32_t s1, uint32_t batch, hipStream_t stream,
+                bool sync_each, const volatile int32_t* cancel, rtw_progress_fn progress, void* user,
+                uint64_t pixels) {
+    const uint64_t total = pixels * (uint64_t)(s1 - s0);
+    for (uint32_t s = s0; s < s1; s += batch) {
+        if (cancel && *cancel) return fail(RTW_E_CANCELLED, "cancelled");
+        L.s0 = s;
+        L.s1 = (s1 - s < batch) ? s1 : s + batch;
+        rtw_launch_render(L, stream, 0);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return hip_fail(e, "render launch");
+        if (sync_each) {
+            HIP_TRY(hipStreamSynchronize(stream));
+            if (progress && progress(pixels * (uint64_t)(L.s1 - s0), total, user)) return fail(RTW_E_CANCELLED, "cancelled by progress callback");
+        }
+    }
+    (void)ctx;
+    return RTW_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int rtw_render(rtw_ctx* ctx, const rtw_camera* cam, uint32_t pix_begin, uint32_t pix_end, uint32_t spp_begin,
+               uint32_t spp_end, uint64_t seed, float* accum, const volatile int32_t* cancel,
+               rtw_progress_fn progress, void* user) {
+    if (!ctx || !accum) return fail(RTW_E_INVALID, "null ctx/accum");
+    if (int rc = validate_cam(cam)) return rc;
+    if (pix_end > cam->size || pix_begin > pix_end) return fail(RTW_E_INVALID, "pixel range out of image");
+    if (spp_begin > spp_end) return fail(RTW_E_INVALID, "bad sample range");
+    if (pix_begin == pix_end || spp_begin == spp_end) return RTW_OK;
+    HIP_TRY(hipSetDevice(ctx->device));
+    const size_t bytes = (size_t)cam->size * 16;
+    if (ctx->scratch_bytes < bytes) {
+        if (ctx->d_scratch) (void)hipFree(ctx->d_scratch);
+        ctx->d_scratch = nullptr;
+        ctx->scratch_bytes = 0;
+        HIP_TRY(hipMalloc(&ctx->d_scratch, bytes));
+        ctx->scratch_bytes = bytes;
+    }
+    const size_t o = (size_t)pix_begin * 16, nb = (size_t)(pix_end - pix_begin) * 16;
+    HIP_TRY(hipMemcpyAsync((char*)ctx->d_scratch + o, (char*)accum + o, nb, hipMemcpyHostToDevice, ctx->stream));
+    rtw_launch L = make_launch(ctx, cam, seed);
+    L.accum = reinterpret_cast<float4*>(ctx->d_scratch);
+    L.pix_begin = pix_begin;
+    L.pix_end = pix_end;
+    L.row0 = pix_begin / cam->image_width;
+    L.n_rows = (pix_end - 1) / cam->image_width - L.row0 + 1;
+    L.n_shards = 0;
+    L.counters = nullptr;
+    const uint32_t batch = auto_batch(pix_end - pix_begin, spp_end - spp_begin);
+    int rc = run_batches(ctx, L, spp_begin, spp_end, batch, ctx->stream, true, cancel, progress, user,
+                         pix_end - pix_begin);
+    // copy back whatever was rendered (also on cancel: completed batches are valid)
+    hipError_t e = hipMemcpyAsync((char*)accum + o, (char*)ctx->d_scratch + o, nb, hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    if (e != hipSuccess) return hip_fail(e, "rtw_render copy back");
+    return rc;
+}
+
+int rtw_render_device(rtw_ctx* ctx, const rtw_camera* cam, uint32_t pix_begin, uint32_t pix_end, uint32_t spp_begin,
+                      uint32_t spp_end, uint64_t seed, float* d_accum, void* stream, const rtw_render_opts* opts) {
+    if (!ctx || !d_accum) return fail(RTW_E_INVALID, "null ctx/accum");
+    if (int rc = validate_cam(cam)) return rc;
+    if (pix_end > cam->size || pix_begin > pix_end) return fail(RTW_E_INVALID, "pixel range out of image");
+    if (spp_begin > spp_end) return fail(RTW_E_INVALID, "bad sample range");
+    if (pix_begin == pix_end || spp_begin == spp_end) return RTW_OK;
+    HIP_TRY(hipSetDevice(ctx->device));
+    hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+    rtw_launch L = make_launch(ctx, cam, seed);
+    L.accum = reinterpret_cast<float4*>(d_accum);
+    L.pix_begin = pix_begin;
+    L.pix_end = pix_end;
+    L.row0 = pix_begin / cam->image_width;
+    L.n_rows = (pix_end - 1) / cam->image_width - L.row0 + 1;
+    L.n_shards = 0;
+    L.counters = opts ? reinterpret_cast<unsigned long long*>(opts->counters) : nullptr;
+    uint32_t batch = opts && opts->spp_batch ? opts->spp_batch : auto_batch(pix_end - pix_begin, spp_end - spp_begin);
+    int rc = run_batches(ctx, L, spp_begin, spp_end, batch, s, false, nullptr, nullptr, nullptr, pix_end - pix_begin);
+    if (rc) return rc;
+    if (!(opts && (opts->flags & RTW_RENDER_NO_SYNC))) HIP_TRY(hipStreamSynchronize(s));
+    return RTW_OK;
+}
+
+uint32_t rtw_shard_rows(uint32_t H, uint32_t rpb, uint32_t n_shards, uint32_t shard) {
+    if (!rpb || !n_shards || shard >= n_shards) return 0;
+    uint32_t rows = 0;
+    const uint32_t nblk = (H + rpb - 1) / rpb;
+    for (uint32_t b = shard; b < nblk; b += n_shards) {
+        const uint32_t y0 = b * rpb;
+        rows += (H - y0 < rpb) ? H - y0 : rpb;
+    }
+    return rows;
+}
+
+int rtw_render_rows_device(rtw_ctx* ctx, const rtw_camera* cam, uint32_t rpb, uint32_t n_shards, uint32_t shard,
+                           uint32_t spp_begin, uint32_t spp_end, uint64_t seed, float* d_tile, void* stream,
+                           const rtw_render_opts* opts) {
+    if (!ctx || !d_tile) return fail(RTW_E_INVALID, "null ctx/tile");
+    if (int rc = validate_cam(cam)) return rc;
+    if (!rpb || !n_shards || shard >= n_shards) return fail(RTW_E_INVALID, "bad shard spec");
+    if (spp_begin > spp_end) return fail(RTW_E_INVALID, "bad sample range");
+    const uint32_t rows = rtw_shard_rows(cam->image_height, rpb, n_shards, shard);
+    if (rows == 0 || spp_begin == spp_end) return RTW_OK;
+    HIP_TRY(hipSetDevice(ctx->device));
+    hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+    rtw_launch L = make_launch(ctx, cam, seed);
+    L.accum = reinterpret_cast<float4*>(d_tile);
+    L.row0 = 0;
+    // logical rows 0 .. (#blocks owned * rpb); rows past H are masked in-kernel
+    const uint32_t nblk = (cam->image_height + rpb - 1) / rpb;
+    const uint32_t owned = nblk > shard ? (nblk - shard + n_shards - 1) / n_shards : 0;
+    L.n_rows = owned * rpb;
+    L.rpb = rpb;
+    L.n_shards = n_shards;
+    L.shard = shard;
+    L.pix_begin = 0;
+    L.pix_end = cam->size;
+    L.counters = opts ? reinterpret_cast<unsigned long long*>(opts->counters) : nullptr;
+    uint32_t batch = opts && opts->spp_batch ? opts->spp_batch : auto_batch((uint64_t)rows * cam->image_width, spp_end - spp_begin);
+    int rc = run_batches(ctx, L, spp_begin, spp_end, batch, s, false, nullptr, nullptr, nullptr,
+                         (uint64_t)rows * cam->image_width);
+    if (rc) return rc;
+    if (!(opts && (opts->flags & RTW_RENDER_NO_SYNC))) HIP_TRY(hipStreamSynchronize(s));
+    return RTW_OK;
+}
+
+int rtw_texture_from_accum(const float* accum, uint32_t n, uint8_t* out) {
+#pragma STDC FP_CONTRACT OFF
+    if (!accum || !out) return fail(RTW_E_INVALID, "null buffer");
+    for (uint32_t i = 0; i < n; i++) {
+        const float* px = accum + 4 * (size_t)i;
+        const float scale = 1.0f / px[3];
+        for (int k = 0; k < 3; k++) {
+            float x = std::sqrt(px[k] * scale);
+            if (x < 0.0f) x = 0.0f;
+            if (x > 0.999f) x = 0.999f;
+            out[4 * (size_t)i + k] = (uint8_t)(256 * x);
+        }
+        out[4 * (size_t)i + 3] = 255;
+    }
+    return RTW_OK;
+}
+
+int rtw_debug_rng(rtw_ctx* ctx, uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t n, float* out) {
+    if (!ctx || !out || n > 64) return fail(RTW_E_INVALID, "bad debug_rng args (n <= 64)");
+    HIP_TRY(hipSetDevice(ctx->device));
+    rtw_launch_debug_rng(seed, pixel, sample, n, ctx->d_dbg, ctx->stream);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(out, ctx->d_dbg, n * sizeof(float), hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    return RTW_OK;
+}
+
+int rtw_debug_sample(rtw_ctx* ctx, const rtw_camera* cam, uint64_t seed, uint32_t pixel, uint32_t sample,
+                     float out[3]) {
+    if (!ctx || !out) return fail(RTW_E_INVALID, "null args");
+    if (int rc = validate_cam(cam)) return rc;
+    if (pixel >= cam->size) return fail(RTW_E_INVALID, "pixel out of range");
+    HIP_TRY(hipSetDevice(ctx->device));
+    rtw_launch L = make_launch(ctx, cam, seed);
+    rtw_launch_debug_sample(L, pixel, sample, ctx->d_dbg, ctx->stream);
+    HIP_TRY(hipGetLastError());
+    float tmp[6];
+    HIP_TRY(hipMemcpyAsync(tmp, ctx->d_dbg, sizeof tmp, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    out[0] = tmp[0];
+    out[1] = tmp[1];
+    out[2] = tmp[2];
+    return RTW_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,51 @@
+// rtw_internal.h -- private declarations shared by the host runtime
+// (rtw_host.hip), the BVH builder (rtw_bvh.hip) and the kernels (rtw_kernels.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <vector>
+
+#include "rtw_layout.h"
+
+struct rtw_scene_desc;
+
+// Everything one launch of the path-tracing kernel reads (passed by value as
+// kernel arguments; scalars live in SGPRs).
+struct rtw_launch {
+    // scene (device pointers)
+    const float4* nodes;
+    const float4* cvec;          // per-sphere center_vec (moving spheres)
+    const rtw_dev_material* mats;
+    const rtw_dev_texture* texs;
+    const uint8_t* images;
+    const rtw_dev_image* img_info;
+    const float4* perlin;        // RTW_PERLIN_BYTES per table
+    uint32_t n_nodes;
+    uint32_t n_perlin;
+
+    // camera (Camera.init outputs, src/camera.zig:118-154)
+    float center[3], pixel00[3], du[3], dv[3], disk_u[3], disk_v[3], background[3];
+    float defocus_angle;
+    uint32_t W, H, max_depth, bg_mode, pixel_offset;
+
+    // work: rows [row0, row0 + n_rows) of the logical row space, pixels
+    // restricted to linear range [pix_begin, pix_end); samples [s0, s1)
+    uint32_t row0, n_rows;
+    uint32_t pix_begin, pix_end;
+    uint32_t s0, s1;
+    // row mapping: logical row r -> image row
+    //   shard mode (n_shards > 0): y = ((r / rpb) * n_shards + shard) * rpb + r % rpb, out idx = r*W + x
+    //   plain mode: y = r, out idx = y*W + x
+    uint32_t rpb, n_shards, shard;
+    uint64_t key0;               // mix64(seed + 0*G): render-domain key
+    float4* accum;
+    unsigned long long* counters;  // RTW_STAT_COUNT or nullptr
+};
+
+void rtw_launch_render(const rtw_launch& L, void* stream, int variant);
+void rtw_launch_debug_rng(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t n, float* d_out, void* stream);
+void rtw_launch_debug_sample(const rtw_launch& L, uint32_t pixel, uint32_t sample, float* d_out, void* stream);
+
+int rtw_build_bvh(const rtw_scene_desc& desc, std::vector<rtw_node>& nodes, std::vector<float>& cvec,
+                  uint32_t* depth, uint32_t* axis_draws);

@@ -1,0 +1,471 @@
+// rtw_kernels.hip -- gfx950 path-tracing kernels: the device side of the
+// per-pixel sample loop Camera.render -> rayColor -> BVHNode.hit / Aabb.hit ->
+// Sphere.hit -> Material.scatter -> Texture.value (src/camera.zig:93-208).
+//
+// Arithmetic contract: compiled with -ffp-contract=off (Zig's strict float
+// mode never fuses), correctly rounded fp32 div/sqrt (hipcc default), fp32
+// denormals kept.  Every geometric quantity (ray, t, p, normal, scatter
+// direction) is evaluated with the same IEEE-754 operations in the same order
+// as the Zig source, so paths are bit-identical to the CPU restatement under
+// the same RNG key.  The radiance of a path is accumulated iteratively
+// (L += T*e; T *= a) instead of the reference's recursive e0 + a0*(e1 + ...),
+// a re-association bounded by max_depth * 2^-24 relative.
+#include <hip/hip_runtime.h>
+
+#include "../../include/rtw_gpu.h"
+#include "rtw_internal.h"
+#include "rtw_layout.h"
+#include "rtw_rng.h"
+
+#pragma clang fp contract(off)
+
+namespace {
+
+constexpr float kPi = 3.1415926535897932385f;  // rtweekend.zig:4
+constexpr float kInf = __builtin_inff();
+
+struct f3 {
+    float x, y, z;
+};
+__device__ __forceinline__ f3 mk(float x, float y, float z) { return f3{x, y, z}; }
+__device__ __forceinline__ f3 operator+(f3 a, f3 b) { return f3{a.x + b.x, a.y + b.y, a.z + b.z}; }
+__device__ __forceinline__ f3 operator-(f3 a, f3 b) { return f3{a.x - b.x, a.y - b.y, a.z - b.z}; }
+__device__ __forceinline__ f3 operator*(f3 a, f3 b) { return f3{a.x * b.x, a.y * b.y, a.z * b.z}; }
+__device__ __forceinline__ f3 operator-(f3 a) { return f3{-a.x, -a.y, -a.z}; }
+__device__ __forceinline__ f3 splat(float s) { return f3{s, s, s}; }
+__device__ __forceinline__ f3 divs(f3 a, float s) { return f3{a.x / s, a.y / s, a.z / s}; }
+__device__ __forceinline__ float dot(f3 u, f3 v) { return u.x * v.x + u.y * v.y + u.z * v.z; }
+__device__ __forceinline__ float length_squared(f3 u) { return u.x * u.x + u.y * u.y + u.z * u.z; }
+__device__ __forceinline__ f3 unit_vector(f3 v) { return divs(v, __builtin_sqrtf(length_squared(v))); }
+__device__ __forceinline__ f3 ld3(const float* p) { return f3{p[0], p[1], p[2]}; }
+__device__ __forceinline__ bool near_zero(f3 u) {  // vec3.zig:19-22
+    const float s = 1e-8f;
+    return __builtin_fabsf(u.x) < s && __builtin_fabsf(u.y) < s && __builtin_fabsf(u.z) < s;
+}
+__device__ __forceinline__ f3 reflect(f3 v, f3 n) { return v - n * splat(dot(v, n) * 2); }  // vec3.zig:77-79
+__device__ __forceinline__ f3 refract(f3 uv, f3 n, float e) {                             // vec3.zig:81-86
+    float c = dot(-uv, n);
+    float cos_theta = c < 1.0f ? c : 1.0f;
+    f3 perp = splat(e) * (uv + n * splat(cos_theta));
+    f3 par = n * splat(-__builtin_sqrtf(__builtin_fabsf(1.0f - length_squared(perp))));
+    return perp + par;
+}
+__device__ __forceinline__ uint32_t fbits(float f) { return __float_as_uint(f); }
+
+// ---- RNG helpers (rtweekend.zig / vec3.zig samplers) ----
+__device__ __forceinline__ float rnd(rtw_rng& r) { return rtw_rng_float(r); }
+__device__ __forceinline__ f3 random_unit_vector(rtw_rng& r) {  // vec3.zig:59-68
+    for (;;) {
+        float x = rtw_rng_range(r, -1, 1);
+        float y = rtw_rng_range(r, -1, 1);
+        float z = rtw_rng_range(r, -1, 1);
+        f3 p = mk(x, y, z);
+        if (length_squared(p) < 1) return unit_vector(p);
+    }
+}
+
+// Zig std.math.pow(f32, x, 5) via frexp-significand square-and-multiply +
+// scalbn (restated; identical fp32 operations to the CPU restatement).
+__device__ __forceinline__ float scalbn_f(float x, int n) {
+    float y = x;
+    if (n > 127) {
+        y *= 1.7014118346046923e38f; n -= 127;
+        if (n > 127) { y *= 1.7014118346046923e38f; n -= 127; if (n > 127) n = 127; }
+    } else if (n < -126) {
+        y *= 1.1754943508222875e-38f * 16777216.0f; n += 126 - 24;
+        if (n < -126) { y *= 1.1754943508222875e-38f * 16777216.0f; n += 126 - 24; if (n < -126) n = -126; }
+    }
+    return y * __uint_as_float((uint32_t)(0x7f + n) << 23);
+}
+__device__ __forceinline__ float frexp_sig(float x, int* e) {
+    uint32_t u = fbits(x);
+    int ee = (int)((u >> 23) & 0xFF);
+    int extra = 0;
+    if (ee == 0) {
+        if (x == 0) { *e = 0; return x; }
+        x = x * 18446744073709551616.0f;
+        u = fbits(x);
+        ee = (int)((u >> 23) & 0xFF);
+        extra = -64;
+    }
+    *e = ee - 126 + extra;
+    return __uint_as_float((u & 0x807FFFFFu) | 0x3F000000u);
+}
+__device__ __forceinline__ float pow5(float x) {
+    if (x == 1) return 1;
+    if (x == 0) return x;  // pow(+-0, odd int > 0) = +-0
+    if (!(x == x)) return x;
+    int xe;
+    float x1 = frexp_sig(x, &xe);
+    float a1 = 1.0f;
+    int ae = 0;
+    // i = 5 = 0b101
+    a1 *= x1; ae += xe;
+    x1 *= x1; xe <<= 1; if (x1 < 0.5f) { x1 += x1; xe -= 1; }
+    x1 *= x1; xe <<= 1; if (x1 < 0.5f) { x1 += x1; xe -= 1; }
+    a1 *= x1; ae += xe;
+    return scalbn_f(a1, ae);
+}
+__device__ __forceinline__ float reflectance(float cosine, float ref_idx) {  // material.zig:101-106
+    float r0 = (1 - ref_idx) / (1 + ref_idx);
+    r0 = r0 * r0;
+    return r0 + (1 - r0) * pow5(1 - cosine);
+}
+
+struct Ray {
+    f3 o, d;
+    float time;
+};
+
+// Camera.getRay (camera.zig:156-180)
+__device__ __forceinline__ Ray get_ray(const rtw_launch& L, uint32_t i, uint32_t j, rtw_rng& rng) {
+    const f3 du = ld3(L.du), dv = ld3(L.dv);
+    f3 pixel_center = (ld3(L.pixel00) + du * splat((float)i)) + dv * splat((float)j);
+    float px = -0.5f + rnd(rng);
+    float py = -0.5f + rnd(rng);
+    f3 pixel_sample = pixel_center + (splat(px) * du + splat(py) * dv);
+    f3 origin;
+    if (L.defocus_angle <= 0) {
+        origin = ld3(L.center);
+    } else {
+        float dx, dy;
+        for (;;) {  // vec3.randomInUnitDisk (vec3.zig:40-45)
+            dx = rtw_rng_range(rng, -1, 1);
+            dy = rtw_rng_range(rng, -1, 1);
+            if (dx * dx + dy * dy + 0.0f * 0.0f < 1) break;
+        }
+        origin = (ld3(L.center) + ld3(L.disk_u) * splat(dx)) + ld3(L.disk_v) * splat(dy);
+    }
+    Ray r;
+    r.o = origin;
+    r.d = pixel_sample - origin;
+    r.time = rnd(rng);
+    return r;
+}
+
+// Texture.value (textures.zig:22-123)
+__device__ float perlin_noise(const float4* tab, f3 p) {  // perlin.zig:117-162 + perlin_interp 30-53
+    const uint32_t* perm = reinterpret_cast<const uint32_t*>(tab + 256);
+    float u = p.x - __builtin_floorf(p.x);
+    float v = p.y - __builtin_floorf(p.y);
+    float w = p.z - __builtin_floorf(p.z);
+    int i = (int)__builtin_floorf(p.x);
+    int j = (int)__builtin_floorf(p.y);
+    int k = (int)__builtin_floorf(p.z);
+    float uu = u * u * (3 - 2 * u);
+    float vv = v * v * (3 - 2 * v);
+    float ww = w * w * (3 - 2 * w);
+    float accum = 0;
+#pragma unroll
+    for (int di = 0; di < 2; di++)
+#pragma unroll
+        for (int dj = 0; dj < 2; dj++)
+#pragma unroll
+            for (int dk = 0; dk < 2; dk++) {
+                uint32_t idx = perm[(i + di) & 255] ^ perm[256 + ((j + dj) & 255)] ^ perm[512 + ((k + dk) & 255)];
+                float4 c = tab[idx & 255];
+                const float i_f = (float)di, j_f = (float)dj, k_f = (float)dk;
+                f3 wv = mk(u - i_f, v - j_f, w - k_f);
+                accum += (i_f * uu + (1 - i_f) * (1 - uu)) * (j_f * vv + (1 - j_f) * (1 - vv)) *
+                         (k_f * ww + (1 - k_f) * (1 - ww)) * dot(mk(c.x, c.y, c.z), wv);
+            }
+    return accum;
+}
+
+__device__ __forceinline__ void sphere_uv(f3 p, float& u, float& v) {  // objects.zig:101-114
+    float theta = acosf(-p.y);
+    float phi = atan2f(-p.z, p.x) + kPi;
+    u = phi / (2 * kPi);
+    v = theta / kPi;
+}
+
+__device__ f3 texture_value(const rtw_launch& L, uint32_t ti, f3 outward, f3 p) {
+    const rtw_dev_texture& t = L.texs[ti];
+    switch (t.kind) {
+    case RTW_TEX_SOLID:
+        return ld3(t.even);
+    case RTW_TEX_CHECKER: {  // textures.zig:60-72
+        int xi = (int)__builtin_floorf(t.scale * p.x);
+        int yi = (int)__builtin_floorf(t.scale * p.y);
+        int zi = (int)__builtin_floorf(t.scale * p.z);
+        return ((xi + yi + zi) % 2 == 0) ? ld3(t.even) : ld3(t.odd);
+    }
+    case RTW_TEX_IMAGE: {  // textures.zig:85-104, rtw_image.zig:37-62
+        const rtw_dev_image im = L.img_info[t.image];
+        if (im.height <= 0) return mk(0, 1, 1);
+        float u, v;
+        sphere_uv(outward, u, v);
+        float nu = u < 0 ? 0 : (u > 1 ? 1 : u);
+        float nv = 1.0f - (v < 0 ? 0 : (v > 1 ? 1 : v));
+        uint32_t i = (uint32_t)__builtin_floorf(nu * (float)im.width);
+        uint32_t j = (uint32_t)__builtin_floorf(nv * (float)im.height);
+        uint32_t x = i < im.width ? i : im.width - 1;
+        uint32_t y = j < im.height ? j : im.height - 1;
+        const uchar4 px = *reinterpret_cast<const uchar4*>(L.images + im.offset + (uint64_t)y * im.bytes_per_row + 4ull * x);
+        const float cs = 1.0f / 255.0f;
+        return mk(cs * (float)px.x, cs * (float)px.y, cs * (float)px.z);
+    }
+    case RTW_TEX_NOISE: {  // textures.zig:118-123, perlin.zig:103-115
+        const float4* tab = L.perlin + (size_t)t.perlin * (RTW_PERLIN_BYTES / 16);
+        f3 s = splat(t.scale) * p;
+        float accum = 0, weight = 1.0f;
+        f3 tp = s;
+        for (int k = 0; k < 7; k++) {
+            accum += weight * perlin_noise(tab, tp);
+            weight *= 0.5f;
+            tp = tp * splat(2);
+        }
+        float turb = __builtin_fabsf(accum);
+        return splat(0.5f * (1 + sinf(s.z + 10 * turb)));
+    }
+    }
+    return mk(0, 0, 0);
+}
+
+struct Counters {
+    uint32_t rays = 0, nodes = 0, leaves = 0, nans = 0;
+};
+
+// World hit: stackless pre-order walk of the reference BVH (bvh.zig:122-136,
+// aabb.zig:82-114, objects.zig:116-136).  Returns leaf node index or -1.
+__device__ __forceinline__ int traverse(const rtw_launch& L, const Ray& r, float& t_out, Counters& cnt) {
+    const f3 inv = mk(1 / r.d.x, 1 / r.d.y, 1 / r.d.z);
+    const float a = length_squared(r.d);
+    const float tmin = 0.001f;
+    float closest = kInf;
+    int hit = -1;
+    uint32_t i = 0;
+    const uint32_t n = L.n_nodes;
+    while (i < n) {
+        const float4 A = L.nodes[2 * i];
+        const uint32_t w = fbits(A.w);
+        if (w & RTW_LEAF_BIT) {
+            cnt.leaves++;
+            const float4 B = L.nodes[2 * i + 1];
+            f3 center = mk(A.x, A.y, A.z);
+            if (fbits(B.w)) {
+                const float4 cv = L.cvec[fbits(B.z)];
+                center = center + splat(r.time) * mk(cv.x, cv.y, cv.z);
+            }
+            const f3 oc = r.o - center;
+            const float half_b = dot(oc, r.d);
+            const float c = length_squared(oc) - B.x * B.x;
+            const float disc = half_b * half_b - a * c;
+            if (disc >= 0) {
+                const float sq = __builtin_sqrtf(disc);
+                float root = (-half_b - sq) / a;
+                bool ok = tmin < root && root < closest;
+                if (!ok) {
+                    root = (-half_b + sq) / a;
+                    ok = tmin < root && root < closest;
+                }
+                if (ok) {
+                    closest = root;
+                    hit = (int)i;
+                }
+            }
+            i = w & RTW_SKIP_MASK;
+        } else {
+            cnt.nodes++;
+            const float4 B = L.nodes[2 * i + 1];
+            float lo = tmin, hi = closest;
+            {
+                float t0 = (A.x - r.o.x) * inv.x, t1 = (B.x - r.o.x) * inv.x;
+                if (inv.x < 0) { float tt = t1; t1 = t0; t0 = tt; }
+                if (t0 > lo) lo = t0;
+                if (t1 < hi) hi = t1;
+            }
+            {
+                float t0 = (A.y - r.o.y) * inv.y, t1 = (B.y - r.o.y) * inv.y;
+                if (inv.y < 0) { float tt = t1; t1 = t0; t0 = tt; }
+                if (t0 > lo) lo = t0;
+                if (t1 < hi) hi = t1;
+            }
+            {
+                float t0 = (A.z - r.o.z) * inv.z, t1 = (B.z - r.o.z) * inv.z;
+                if (inv.z < 0) { float tt = t1; t1 = t0; t0 = tt; }
+                if (t0 > lo) lo = t0;
+                if (t1 < hi) hi = t1;
+            }
+            // per-axis early exit of aabb.zig:111 is equivalent: lo only grows, hi only shrinks
+            i = (hi <= lo) ? w : i + 1;
+        }
+    }
+    t_out = closest;
+    return hit;
+}
+
+// One sample's radiance: getRay + iterative rayColor (camera.zig:169-208).
+__device__ f3 sample_radiance(const rtw_launch& L, uint32_t pixel, uint32_t x, uint32_t y, uint32_t s,
+                              Counters& cnt) {
+    rtw_rng rng;
+    rng.s = rtw_mix64(L.key0 ^ (((uint64_t)pixel << 32) | (uint64_t)s));
+    Ray r = get_ray(L, x, y, rng);
+    f3 acc = mk(0, 0, 0);
+    f3 thr = mk(1, 1, 1);
+    for (uint32_t depth = L.max_depth; depth > 0; depth--) {
+        cnt.rays++;
+        float t;
+        const int hit = traverse(L, r, t, cnt);
+        if (hit < 0) {
+            f3 bg;
+            if (L.bg_mode == RTW_BG_GRADIENT) {  // camera.zig:204-206
+                f3 ud = unit_vector(r.d);
+                float a = 0.5f * (ud.y + 1.0f);
+                bg = mk(1, 1, 1) * splat(1.0f - a) + mk(0.5f, 0.7f, 1.0f) * splat(a);
+            } else {
+                bg = ld3(L.background);
+            }
+            acc = acc + thr * bg;
+            break;
+        }
+        // HitRecord (objects.zig:139-145), recomputed once for the closest hit
+        const float4 A = L.nodes[2 * hit];
+        const float4 B = L.nodes[2 * hit + 1];
+        f3 center = mk(A.x, A.y, A.z);
+        if (fbits(B.w)) {
+            const float4 cv = L.cvec[fbits(B.z)];
+            center = center + splat(r.time) * mk(cv.x, cv.y, cv.z);
+        }
+        const f3 p = r.o + splat(t) * r.d;
+        const f3 outward = divs(p - center, B.x);
+        const bool front = dot(r.d, outward) < 0;
+        const f3 normal = front ? outward : -outward;
+        const rtw_dev_material m = L.mats[fbits(B.y)];
+
+        f3 att;
+        Ray sc;
+        sc.o = p;
+        sc.time = r.time;
+        bool scattered = true;
+        switch (m.kind) {
+        case RTW_MAT_LAMBERTIAN: {  // material.zig:43-54
+            f3 dir = normal + random_unit_vector(rng);
+            if (near_zero(dir)) dir = normal;
+            sc.d = dir;
+            att = texture_value(L, m.texture, outward, p);
+            break;
+        }
+        case RTW_MAT_METAL: {  // material.zig:65-70
+            f3 refl = reflect(unit_vector(r.d), normal);
+            sc.d = refl + splat(m.fuzz) * random_unit_vector(rng);
+            att = ld3(m.albedo);
+            scattered = dot(sc.d, normal) > 0;
+            break;
+        }
+        case RTW_MAT_DIELECTRIC: {  // material.zig:80-98
+            att = mk(1, 1, 1);
+            const float ratio = front ? (1.0f / m.ir) : m.ir;
+            const f3 ud = unit_vector(r.d);
+            const float dd = dot(-ud, normal);
+            const float cos_theta = dd < 1.0f ? dd : 1.0f;
+            const float sin_theta = __builtin_sqrtf(1.0f - cos_theta * cos_theta);
+            const bool cannot = ratio * sin_theta > 1.0f;
+            if (cannot || reflectance(cos_theta, ratio) > rnd(rng))
+                sc.d = reflect(ud, normal);
+            else
+                sc.d = refract(ud, normal, ratio);
+            break;
+        }
+        case RTW_MAT_DIFFUSE_LIGHT: {  // material.zig:119-125
+            acc = acc + thr * texture_value(L, m.texture, outward, p);
+            scattered = false;
+            break;
+        }
+        default: {  // RTW_MAT_ISOTROPIC (material.zig:139-143)
+            sc.d = random_unit_vector(rng);
+            att = texture_value(L, m.texture, outward, p);
+            break;
+        }
+        }
+        if (!scattered) break;
+        thr = thr * att;
+        r = sc;
+    }
+    return acc;
+}
+
+__device__ __forceinline__ bool map_row(const rtw_launch& L, uint32_t r, uint32_t& y, uint32_t& out_row) {
+    if (L.n_shards) {
+        const uint32_t blk = r / L.rpb;
+        y = (blk * L.n_shards + L.shard) * L.rpb + r % L.rpb;
+        out_row = r;
+    } else {
+        y = r;
+        out_row = r;
+    }
+    return y < L.H;
+}
+
+__device__ __forceinline__ void flush_counters(const rtw_launch& L, const Counters& c, uint32_t samples) {
+    if (!L.counters) return;
+    atomicAdd(&L.counters[RTW_STAT_RAYS], (unsigned long long)c.rays);
+    atomicAdd(&L.counters[RTW_STAT_NODES], (unsigned long long)c.nodes);
+    atomicAdd(&L.counters[RTW_STAT_LEAVES], (unsigned long long)c.leaves);
+    atomicAdd(&L.counters[RTW_STAT_SAMPLES], (unsigned long long)samples);
+    if (c.nans) atomicAdd(&L.counters[RTW_STAT_NAN], (unsigned long long)c.nans);
+}
+
+// v0: one thread per pixel, each wave an 8x8 pixel tile, block = 32x8 pixels;
+// samples [s0, s1) looped in order, accumulator read once / written once.
+__global__ __launch_bounds__(256) void render_pixels_v0(rtw_launch L) {
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t x = blockIdx.x * 32 + wave * 8 + (lane & 7);
+    const uint32_t r = L.row0 + blockIdx.y * 8 + (lane >> 3);
+    if (x >= L.W || r >= L.row0 + L.n_rows) return;
+    uint32_t y, out_row;
+    if (!map_row(L, r, y, out_row)) return;
+    const uint32_t pixel = y * L.W + x;
+    if (!L.n_shards && (pixel < L.pix_begin || pixel >= L.pix_end)) return;
+    float4* slot = L.accum + (size_t)out_row * L.W + x;
+    float4 acc = *slot;
+    Counters cnt;
+    const uint32_t px = x + L.pixel_offset, py = y + L.pixel_offset;  // camera.zig:100-101
+    for (uint32_t s = L.s0; s < L.s1; s++) {
+        f3 c = sample_radiance(L, pixel, px, py, s, cnt);
+        if (!(c.x == c.x) || !(c.y == c.y) || !(c.z == c.z)) cnt.nans++;
+        acc.x += c.x;
+        acc.y += c.y;
+        acc.z += c.z;
+    }
+    acc.w = (float)L.s1;  // writeColor: buffer[i][3] = number_of_samples (camera.zig:56)
+    *slot = acc;
+    flush_counters(L, cnt, L.s1 - L.s0);
+}
+
+__global__ void debug_rng_kernel(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t n, float* out) {
+    if (threadIdx.x | blockIdx.x) return;
+    rtw_rng r;
+    r.s = rtw_mix64(rtw_mix64(seed) ^ (((uint64_t)pixel << 32) | (uint64_t)sample));
+    for (uint32_t k = 0; k < n; k++) out[k] = rtw_rng_float(r);
+}
+
+__global__ void debug_sample_kernel(rtw_launch L, uint32_t pixel, uint32_t sample, float* out) {
+    if (threadIdx.x | blockIdx.x) return;
+    Counters cnt;
+    const uint32_t x = pixel % L.W, y = pixel / L.W;
+    f3 c = sample_radiance(L, pixel, x + L.pixel_offset, y + L.pixel_offset, sample, cnt);
+    out[0] = c.x;
+    out[1] = c.y;
+    out[2] = c.z;
+    out[3] = (float)cnt.rays;
+    out[4] = (float)cnt.nodes;
+    out[5] = (float)cnt.leaves;
+}
+
+}  // namespace
+
+void rtw_launch_render(const rtw_launch& L, void* stream, int variant) {
+    (void)variant;
+    dim3 block(256);
+    dim3 grid((L.W + 31) / 32, (L.n_rows + 7) / 8);
+    hipLaunchKernelGGL(render_pixels_v0, grid, block, 0, (hipStream_t)stream, L);
+}
+
+void rtw_launch_debug_rng(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t n, float* d_out, void* stream) {
+    hipLaunchKernelGGL(debug_rng_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, seed, pixel, sample, n, d_out);
+}
+
+void rtw_launch_debug_sample(const rtw_launch& L, uint32_t pixel, uint32_t sample, float* d_out, void* stream) {
+    hipLaunchKernelGGL(debug_sample_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, L, pixel, sample, d_out);
+}

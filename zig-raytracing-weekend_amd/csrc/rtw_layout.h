@@ -1,0 +1,56 @@
+// rtw_layout.h -- device-resident scene layout (HBM), shared by the host-side
+// builder (rtw_bvh.cpp / rtw_host.hip) and the gfx950 kernels (rtw_kernels.hip).
+//
+// Node (32 B = two 16-B loads).  Nodes are stored in
+// depth-first pre-order of the reference BVHTree (src/bvh.zig:43-89) with a
+// skip link = index of the first node after the subtree.  A stackless
+// traversal (hit -> i+1, miss -> skip) therefore visits nodes in exactly the
+// order of the reference's recursive BVHNode.hit (src/bvh.zig:122-136):
+// left subtree first, right subtree with the interval shrunk to the closest
+// hit so far, leaves tested without a box test.
+//
+//   inner: a = (bmin.x, bmin.y, bmin.z, bits(skip))            b = (bmax.x, bmax.y, bmax.z, 0)
+//   leaf : a = (c1.x,   c1.y,   c1.z,   bits(skip | LEAF_BIT)) b = (radius, bits(mat), bits(sphere), bits(moving))
+//
+// Moving spheres keep center_vec = center2 - center1 in a side array indexed by
+// sphere id (only read when the moving flag is set).
+#pragma once
+#include <stdint.h>
+
+#define RTW_LEAF_BIT 0x80000000u
+#define RTW_SKIP_MASK 0x7FFFFFFFu
+
+struct rtw_node {
+    float a[4];
+    float b[4];
+};
+static_assert(sizeof(rtw_node) == 32, "node must be 32 bytes");
+
+// 32 B: {kind, texture, fuzz, ir} {albedo.xyz, 0}
+struct rtw_dev_material {
+    uint32_t kind;
+    uint32_t texture;
+    float fuzz;
+    float ir;
+    float albedo[4];
+};
+static_assert(sizeof(rtw_dev_material) == 32, "material must be 32 bytes");
+
+// 48 B, same field order as rtw_texture (image/perlin are indices)
+struct rtw_dev_texture {
+    uint32_t kind;
+    uint32_t image;
+    uint32_t perlin;
+    float scale;
+    float even[4];
+    float odd[4];
+};
+static_assert(sizeof(rtw_dev_texture) == 48, "texture must be 48 bytes");
+
+struct rtw_dev_image {
+    uint64_t offset;          // byte offset into the image blob
+    uint32_t width, height, bytes_per_row, _pad;
+};
+
+// Per perlin table: ranvec as float4[256] (4 KiB) then perm_x|perm_y|perm_z as uint32[3][256]
+#define RTW_PERLIN_BYTES (256 * 16 + 3 * 256 * 4)

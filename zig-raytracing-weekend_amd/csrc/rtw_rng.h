@@ -1,0 +1,79 @@
+// rtw_rng.h -- counter-based RNG replacing std.crypto.random (src/rtweekend.zig:14-27).
+//
+// The reference draws every random number from Zig's thread-local, OS-seeded
+// CSPRNG; it cannot be seeded.  This product keys a SplitMix64 stream by
+// (seed, domain, a, b):
+//     key  = mix64(mix64(seed + domain * G) ^ (a << 32 | b))
+//     draw = mix64(state += G)                    G = 0x9E3779B97F4A7C15
+// domain 0 = render samples (a = pixel linear index, b = 0-based sample index),
+// 1 = scene generation, 2 = BVH build axes, 3 = Perlin tables (a = table id).
+// Every draw is mapped to f32 exactly like Zig's std.Random.float(f32).
+// Identical (seed, pixel, sample) -> identical draws on any device, batch or
+// shard.  Single-sourced for host (BVH build) and device (render kernel).
+#pragma once
+#include <stdint.h>
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#endif
+
+#if defined(__HIPCC__)
+#define RTW_HD __host__ __device__ __forceinline__
+#else
+#define RTW_HD static inline
+#endif
+
+#define RTW_GOLDEN 0x9E3779B97F4A7C15ull
+
+RTW_HD uint64_t rtw_mix64(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+    return z ^ (z >> 31);
+}
+
+struct rtw_rng {
+    uint64_t s;
+};
+
+RTW_HD rtw_rng rtw_rng_stream(uint64_t seed, uint64_t domain, uint32_t a, uint32_t b) {
+    rtw_rng r;
+    r.s = rtw_mix64(rtw_mix64(seed + domain * RTW_GOLDEN) ^ (((uint64_t)a << 32) | (uint64_t)b));
+    return r;
+}
+
+RTW_HD uint64_t rtw_rng_next(rtw_rng& r) {
+    r.s += RTW_GOLDEN;
+    return rtw_mix64(r.s);
+}
+
+RTW_HD int rtw_clz64(uint64_t x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return x ? __clzll((long long)x) : 64;
+#else
+    return x ? __builtin_clzll(x) : 64;
+#endif
+}
+
+RTW_HD int rtw_clz32(uint32_t x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return x ? __clz((int)x) : 32;
+#else
+    return x ? __builtin_clz(x) : 32;
+#endif
+}
+
+// Zig std.Random.float(f32): mantissa = low 23 bits, exponent 126 - clz(draw).
+RTW_HD float rtw_rng_float(rtw_rng& r) {
+    uint64_t x = rtw_rng_next(r);
+    int lz = rtw_clz64(x);
+    if (lz >= 41) {
+        lz = 41 + rtw_clz64(rtw_rng_next(r));
+        if (lz == 41 + 64) lz += rtw_clz32((uint32_t)rtw_rng_next(r) | 0x7FFu);
+    }
+    uint32_t bits = ((uint32_t)(126 - lz) << 23) | (uint32_t)(x & 0x7FFFFFu);
+    union { uint32_t u; float f; } cv;
+    cv.u = bits;
+    return cv.f;
+}
+
+// rtweekend.zig:18-20
+RTW_HD float rtw_rng_range(rtw_rng& r, float mn, float mx) { return mn + (mx - mn) * rtw_rng_float(r); }
