@@ -79,7 +79,8 @@ def main():
     max_blk = (n_blk + world_size - 1) // world_size
     tile = torch.zeros((max_blk * ROWS_PER_BLOCK * W, 4), dtype=torch.float32, device="cuda")
     my_rows = L.rtw_shard_rows(H, ROWS_PER_BLOCK, world_size, rank)
-    stream = torch.cuda.current_stream()
+    stream = torch.cuda.Stream()          # explicit stream: the kernels and the timing events share it
+    torch.cuda.set_stream(stream)
     opts = pkg._abi.RtwRenderOpts(spp, pkg._abi.RTW_RENDER_NO_SYNC, None)   # one launch per step
     gather_list = [torch.empty_like(tile) for _ in range(world_size)] if (distributed and rank == 0) else None
     image = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda") if rank == 0 else None

@@ -18,6 +18,7 @@ if [ "${SKIP_TESTS:-0}" != 1 ]; then
   step pytest_gpu 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider
   step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 fi
+if [ -n "${TUNE_ARGS:-}" ]; then step tune 600 python tools/tune.py ${TUNE_ARGS}; fi
 step bench 900 python bench.py ${BENCH_ARGS:-}
 if [ "${PROFILE:-1}" = 1 ]; then
   step rocprof 900 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python bench.py --no-cpu-baseline --steps 2 --warmup 0 ${BENCH_ARGS:-}

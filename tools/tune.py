@@ -1,0 +1,43 @@
+"""A/B timing of kernel variants / knobs on BASELINE config 2 geometry (reduced spp).
+Usage: python tools/tune.py [spp] ; knobs via env lists in the script."""
+import ctypes as C
+import importlib
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+pkg = importlib.import_module("zig-raytracing-weekend_amd")
+spp = int(sys.argv[1]) if len(sys.argv) > 1 else 100
+cfg_name = sys.argv[2] if len(sys.argv) > 2 else "c2"
+settings = json.loads(os.environ.get("TUNE", '[{"RTW_KERNEL":"v0"},{"RTW_KERNEL":"v1","RTW_SHADE_MIN":"8"},'
+                                     '{"RTW_KERNEL":"v1","RTW_SHADE_MIN":"16"},{"RTW_KERNEL":"v1","RTW_SHADE_MIN":"32"},'
+                                     '{"RTW_KERNEL":"v1","RTW_SHADE_MIN":"48"}]'))
+cfg = pkg.configs.CONFIGS[cfg_name]
+arr = pkg.flatten(cfg.objects())
+cam = cfg.camera()
+cam.samples_per_pixel = spp
+cam.init()
+acc = torch.zeros((cam.size, 4), dtype=torch.float32, device="cuda")
+stream = torch.cuda.Stream()
+for st in settings:
+    for k in ("RTW_KERNEL", "RTW_SHADE_MIN"):
+        os.environ.pop(k, None)
+    os.environ.update(st)
+    world = pkg.World(arr)
+    opts = pkg._abi.RtwRenderOpts(spp, 0, None)
+    best = 1e9
+    for it in range(3):
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        rc = pkg.lib().rtw_render_device(world.handle, C.byref(cam.derived), 0, cam.size, 0, spp, 0,
+                                         acc.data_ptr(), C.c_void_p(stream.cuda_stream), C.byref(opts))
+        pkg._abi.check(rc, "render")
+        torch.cuda.synchronize()
+        best = min(best, time.perf_counter() - t)
+    print(json.dumps({"setting": st, "config": cfg_name, "spp": spp, "s": round(best, 4),
+                      "Msamples_s": round(cam.size * spp / best / 1e6, 2)}), flush=True)
+    world.close()

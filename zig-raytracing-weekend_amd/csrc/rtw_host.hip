@@ -4,6 +4,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -46,7 +47,31 @@ struct rtw_ctx {
     float* d_scratch = nullptr;    // host-API accum staging
     size_t scratch_bytes = 0;
     float* d_dbg = nullptr;        // debug kernels output
+    uint32_t* d_work = nullptr;    // persistent-kernel work counter (zeroed before each launch)
+    uint32_t feat = 0;             // RTW_F_* scene features
+    int grid = 0;                  // resident blocks of the persistent kernel
+    int variant = 1;               // 1 = persistent v1 (default), 0 = simple v0 (RTW_KERNEL=v0)
+    uint32_t shade_min = 16;       // RTW_SHADE_MIN
 };
+
+namespace {
+uint32_t scene_features(const rtw_scene_desc* d) {
+    uint32_t f = 0;
+    for (uint32_t i = 0; i < d->n_spheres; i++)
+        if (d->spheres[i].is_moving) f |= RTW_F_MOVING;
+    for (uint32_t i = 0; i < d->n_materials; i++) {
+        const rtw_material& m = d->materials[i];
+        if (m.kind == RTW_MAT_DIFFUSE_LIGHT || m.kind == RTW_MAT_ISOTROPIC) f |= RTW_F_LIGHT;
+        const bool textured = m.kind == RTW_MAT_LAMBERTIAN || m.kind == RTW_MAT_DIFFUSE_LIGHT || m.kind == RTW_MAT_ISOTROPIC;
+        if (!textured) continue;
+        const uint32_t k = d->textures[m.texture].kind;
+        if (k == RTW_TEX_CHECKER) f |= RTW_F_CHECKER;
+        if (k == RTW_TEX_IMAGE) f |= RTW_F_IMAGE;
+        if (k == RTW_TEX_NOISE) f |= RTW_F_NOISE;
+    }
+    return f;
+}
+}  // namespace
 
 extern "C" {
 
@@ -226,10 +251,13 @@ int rtw_scene_create(const rtw_scene_desc* d, int device, rtw_ctx** out) {
     }
 
     hipError_t e = hipSetDevice(device);
-    if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
+    // blocking stream: orders with the legacy NULL stream (torch's default), so a caller passing
+    // device buffers and stream == NULL sees its prior NULL-stream work (e.g. zero fills) complete first
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->stream, hipStreamDefault);
     if (e == hipSuccess) e = hipMalloc(&ctx->d_blob, off);
     if (e == hipSuccess) e = hipMemcpy(ctx->d_blob, blob.data(), off, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMalloc(&ctx->d_dbg, 64 * sizeof(float));
+    if (e == hipSuccess) e = hipMalloc(&ctx->d_work, 256);
     if (e != hipSuccess) {
         int code = hip_fail(e, "rtw_scene_create upload");
         rtw_scene_destroy(ctx);
@@ -247,6 +275,16 @@ int rtw_scene_create(const rtw_scene_desc* d, int device, rtw_ctx** out) {
     L.images = dev + o_imgs;
     L.n_nodes = (uint32_t)n_nodes;
     L.n_perlin = d->n_perlins;
+    ctx->feat = scene_features(d);
+    L.feat = ctx->feat;
+    L.work_counter = ctx->d_work;
+    if (const char* kv = std::getenv("RTW_KERNEL")) ctx->variant = (std::strcmp(kv, "v0") == 0) ? 0 : 1;
+    if (const char* sm = std::getenv("RTW_SHADE_MIN")) {
+        int v = std::atoi(sm);
+        ctx->shade_min = (uint32_t)(v < 1 ? 1 : (v > 64 ? 64 : v));
+    }
+    L.shade_min = ctx->shade_min;
+    ctx->grid = rtw_persistent_grid(ctx->feat, n_nodes <= RTW_LDS_NODES, ctx->stream);
 
     ctx->stats.n_nodes = (uint32_t)n_nodes;
     ctx->stats.n_leaves = d->n_spheres;
@@ -265,6 +303,7 @@ void rtw_scene_destroy(rtw_ctx* ctx) {
     if (ctx->d_blob) (void)hipFree(ctx->d_blob);
     if (ctx->d_scratch) (void)hipFree(ctx->d_scratch);
     if (ctx->d_dbg) (void)hipFree(ctx->d_dbg);
+    if (ctx->d_work) (void)hipFree(ctx->d_work);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -347,7 +386,8 @@ int run_batches(rtw_ctx* ctx, rtw_launch L, uint32_t s0, uint32_t s1, uint32_t b
         if (cancel && *cancel) return fail(RTW_E_CANCELLED, "cancelled");
         L.s0 = s;
         L.s1 = (s1 - s < batch) ? s1 : s + batch;
-        rtw_launch_render(L, stream, 0);
+        if (ctx->variant == 1) HIP_TRY(hipMemsetAsync(ctx->d_work, 0, 256, stream));
+        rtw_launch_render(L, stream, ctx->variant, ctx->grid);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return hip_fail(e, "render launch");
         if (sync_each) {
@@ -355,8 +395,12 @@ int run_batches(rtw_ctx* ctx, rtw_launch L, uint32_t s0, uint32_t s1, uint32_t b
             if (progress && progress(pixels * (uint64_t)(L.s1 - s0), total, user)) return fail(RTW_E_CANCELLED, "cancelled by progress callback");
         }
     }
-    (void)ctx;
     return RTW_OK;
+}
+
+void set_tiles(rtw_launch& L) {
+    L.n_tiles_x = (L.W + RTW_TILE_W - 1) / RTW_TILE_W;
+    L.n_tiles = L.n_tiles_x * ((L.n_rows + RTW_TILE_H - 1) / RTW_TILE_H);
 }
 
 }  // namespace
@@ -390,6 +434,7 @@ int rtw_render(rtw_ctx* ctx, const rtw_camera* cam, uint32_t pix_begin, uint32_t
     L.n_rows = (pix_end - 1) / cam->image_width - L.row0 + 1;
     L.n_shards = 0;
     L.counters = nullptr;
+    set_tiles(L);
     const uint32_t batch = auto_batch(pix_end - pix_begin, spp_end - spp_begin);
     int rc = run_batches(ctx, L, spp_begin, spp_end, batch, ctx->stream, true, cancel, progress, user,
                          pix_end - pix_begin);
@@ -417,6 +462,7 @@ int rtw_render_device(rtw_ctx* ctx, const rtw_camera* cam, uint32_t pix_begin, u
     L.n_rows = (pix_end - 1) / cam->image_width - L.row0 + 1;
     L.n_shards = 0;
     L.counters = opts ? reinterpret_cast<unsigned long long*>(opts->counters) : nullptr;
+    set_tiles(L);
     uint32_t batch = opts && opts->spp_batch ? opts->spp_batch : auto_batch(pix_end - pix_begin, spp_end - spp_begin);
     int rc = run_batches(ctx, L, spp_begin, spp_end, batch, s, false, nullptr, nullptr, nullptr, pix_end - pix_begin);
     if (rc) return rc;
@@ -459,6 +505,7 @@ int rtw_render_rows_device(rtw_ctx* ctx, const rtw_camera* cam, uint32_t rpb, ui
     L.pix_begin = 0;
     L.pix_end = cam->size;
     L.counters = opts ? reinterpret_cast<unsigned long long*>(opts->counters) : nullptr;
+    set_tiles(L);
     uint32_t batch = opts && opts->spp_batch ? opts->spp_batch : auto_batch((uint64_t)rows * cam->image_width, spp_end - spp_begin);
     int rc = run_batches(ctx, L, spp_begin, spp_end, batch, s, false, nullptr, nullptr, nullptr,
                          (uint64_t)rows * cam->image_width);

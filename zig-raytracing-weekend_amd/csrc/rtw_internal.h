@@ -41,9 +41,37 @@ struct rtw_launch {
     uint64_t key0;               // mix64(seed + 0*G): render-domain key
     float4* accum;
     unsigned long long* counters;  // RTW_STAT_COUNT or nullptr
+
+    // persistent kernel (v1) work queue: tiles of RTW_TILE_W x RTW_TILE_H logical pixels
+    uint32_t* work_counter;      // zeroed before every launch
+    uint32_t n_tiles_x, n_tiles;
+    uint32_t shade_min;          // lanes that must be ready before a shading pass (<= 64)
+    uint32_t feat;               // RTW_F_* scene features (selects the kernel instantiation)
 };
 
-void rtw_launch_render(const rtw_launch& L, void* stream, int variant);
+#define RTW_TILE_W 16
+#define RTW_TILE_H 16
+#define RTW_TILE (RTW_TILE_W * RTW_TILE_H)
+
+// scene feature bits: kernels are instantiated per feature set so Book-1
+// (solid textures, static spheres, no lights) carries no texture/motion code
+#define RTW_F_CHECKER 1u
+#define RTW_F_IMAGE 2u
+#define RTW_F_NOISE 4u
+#define RTW_F_MOVING 8u
+#define RTW_F_LIGHT 16u
+#define RTW_F_ALL 31u
+
+// max nodes staged in LDS by the persistent kernel (48 KiB)
+#define RTW_LDS_NODES 1536
+
+struct rtw_kernel_info {
+    int blocks_per_cu;
+    int n_cu;
+};
+int rtw_persistent_grid(uint32_t feat, bool lds, void* stream);
+
+void rtw_launch_render(const rtw_launch& L, void* stream, int variant, int grid);
 void rtw_launch_debug_rng(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t n, float* d_out, void* stream);
 void rtw_launch_debug_sample(const rtw_launch& L, uint32_t pixel, uint32_t sample, float* d_out, void* stream);
 

@@ -179,125 +179,220 @@ __device__ __forceinline__ void sphere_uv(f3 p, float& u, float& v) {  // object
     v = theta / kPi;
 }
 
+template <uint32_t FEAT>
 __device__ f3 texture_value(const rtw_launch& L, uint32_t ti, f3 outward, f3 p) {
     const rtw_dev_texture& t = L.texs[ti];
-    switch (t.kind) {
-    case RTW_TEX_SOLID:
-        return ld3(t.even);
-    case RTW_TEX_CHECKER: {  // textures.zig:60-72
-        int xi = (int)__builtin_floorf(t.scale * p.x);
-        int yi = (int)__builtin_floorf(t.scale * p.y);
-        int zi = (int)__builtin_floorf(t.scale * p.z);
-        return ((xi + yi + zi) % 2 == 0) ? ld3(t.even) : ld3(t.odd);
-    }
-    case RTW_TEX_IMAGE: {  // textures.zig:85-104, rtw_image.zig:37-62
-        const rtw_dev_image im = L.img_info[t.image];
-        if (im.height <= 0) return mk(0, 1, 1);
-        float u, v;
-        sphere_uv(outward, u, v);
-        float nu = u < 0 ? 0 : (u > 1 ? 1 : u);
-        float nv = 1.0f - (v < 0 ? 0 : (v > 1 ? 1 : v));
-        uint32_t i = (uint32_t)__builtin_floorf(nu * (float)im.width);
-        uint32_t j = (uint32_t)__builtin_floorf(nv * (float)im.height);
-        uint32_t x = i < im.width ? i : im.width - 1;
-        uint32_t y = j < im.height ? j : im.height - 1;
-        const uchar4 px = *reinterpret_cast<const uchar4*>(L.images + im.offset + (uint64_t)y * im.bytes_per_row + 4ull * x);
-        const float cs = 1.0f / 255.0f;
-        return mk(cs * (float)px.x, cs * (float)px.y, cs * (float)px.z);
-    }
-    case RTW_TEX_NOISE: {  // textures.zig:118-123, perlin.zig:103-115
-        const float4* tab = L.perlin + (size_t)t.perlin * (RTW_PERLIN_BYTES / 16);
-        f3 s = splat(t.scale) * p;
-        float accum = 0, weight = 1.0f;
-        f3 tp = s;
-        for (int k = 0; k < 7; k++) {
-            accum += weight * perlin_noise(tab, tp);
-            weight *= 0.5f;
-            tp = tp * splat(2);
+    const uint32_t kind = t.kind;
+    if constexpr ((FEAT & RTW_F_CHECKER) != 0) {
+        if (kind == RTW_TEX_CHECKER) {  // textures.zig:60-72
+            int xi = (int)__builtin_floorf(t.scale * p.x);
+            int yi = (int)__builtin_floorf(t.scale * p.y);
+            int zi = (int)__builtin_floorf(t.scale * p.z);
+            return ((xi + yi + zi) % 2 == 0) ? ld3(t.even) : ld3(t.odd);
         }
-        float turb = __builtin_fabsf(accum);
-        return splat(0.5f * (1 + sinf(s.z + 10 * turb)));
     }
+    if constexpr ((FEAT & RTW_F_IMAGE) != 0) {
+        if (kind == RTW_TEX_IMAGE) {  // textures.zig:85-104, rtw_image.zig:37-62
+            const rtw_dev_image im = L.img_info[t.image];
+            if (im.height <= 0) return mk(0, 1, 1);
+            float u, v;
+            sphere_uv(outward, u, v);
+            float nu = u < 0 ? 0 : (u > 1 ? 1 : u);
+            float nv = 1.0f - (v < 0 ? 0 : (v > 1 ? 1 : v));
+            uint32_t i = (uint32_t)__builtin_floorf(nu * (float)im.width);
+            uint32_t j = (uint32_t)__builtin_floorf(nv * (float)im.height);
+            uint32_t x = i < im.width ? i : im.width - 1;
+            uint32_t y = j < im.height ? j : im.height - 1;
+            const uchar4 px =
+                *reinterpret_cast<const uchar4*>(L.images + im.offset + (uint64_t)y * im.bytes_per_row + 4ull * x);
+            const float cs = 1.0f / 255.0f;
+            return mk(cs * (float)px.x, cs * (float)px.y, cs * (float)px.z);
+        }
     }
-    return mk(0, 0, 0);
+    if constexpr ((FEAT & RTW_F_NOISE) != 0) {
+        if (kind == RTW_TEX_NOISE) {  // textures.zig:118-123, perlin.zig:103-115
+            const float4* tab = L.perlin + (size_t)t.perlin * (RTW_PERLIN_BYTES / 16);
+            f3 s = splat(t.scale) * p;
+            float accum = 0, weight = 1.0f;
+            f3 tp = s;
+            for (int k = 0; k < 7; k++) {
+                accum += weight * perlin_noise(tab, tp);
+                weight *= 0.5f;
+                tp = tp * splat(2);
+            }
+            float turb = __builtin_fabsf(accum);
+            return splat(0.5f * (1 + sinf(s.z + 10 * turb)));
+        }
+    }
+    return ld3(t.even);  // RTW_TEX_SOLID (textures.zig:43-45)
 }
 
 struct Counters {
     uint32_t rays = 0, nodes = 0, leaves = 0, nans = 0;
 };
 
-// World hit: stackless pre-order walk of the reference BVH (bvh.zig:122-136,
-// aabb.zig:82-114, objects.zig:116-136).  Returns leaf node index or -1.
-__device__ __forceinline__ int traverse(const rtw_launch& L, const Ray& r, float& t_out, Counters& cnt) {
-    const f3 inv = mk(1 / r.d.x, 1 / r.d.y, 1 / r.d.z);
-    const float a = length_squared(r.d);
-    const float tmin = 0.001f;
+// Per-ray constants of the traversal.
+struct RayTrav {
+    f3 inv;      // 1 / d per axis (aabb.zig:87)
+    float a;     // lengthSquared(d) (objects.zig:124)
+};
+__device__ __forceinline__ RayTrav ray_trav(const Ray& r) {
+    RayTrav t;
+    t.inv = mk(1 / r.d.x, 1 / r.d.y, 1 / r.d.z);
+    t.a = length_squared(r.d);
+    return t;
+}
+
+constexpr float kTmin = 0.001f;  // camera.zig:187
+
+// One node of the stackless pre-order walk of the reference BVH
+// (bvh.zig:122-136): a leaf is tested without a box test (Sphere.hit,
+// objects.zig:116-136, open interval (0.001, closest)); an inner node's box is
+// tested with [0.001, closest] (Aabb.hit, aabb.zig:82-114).  Returns the next
+// node index.  hi/lo use fmax/fmin: for the NaN slabs of a zero direction
+// component (0*inf) maxNum keeps the other operand exactly like the
+// reference's `if (t0 > min) min = t0`, and lo/hi only grow/shrink, so the
+// single final `hi <= lo` equals the per-axis early exit of aabb.zig:111.
+template <uint32_t FEAT>
+__device__ __forceinline__ uint32_t trav_step(const float4* __restrict__ nodes, const rtw_launch& L, const Ray& r,
+                                              const RayTrav& rt, uint32_t i, float& closest, int& hit,
+                                              Counters& cnt) {
+    const float4 A = nodes[2 * i];
+    const float4 B = nodes[2 * i + 1];
+    const uint32_t w = fbits(A.w);
+    if (w & RTW_LEAF_BIT) {
+        cnt.leaves++;
+        f3 center = mk(A.x, A.y, A.z);
+        if constexpr ((FEAT & RTW_F_MOVING) != 0) {
+            if (fbits(B.w)) {  // Sphere.getCenter (objects.zig:94-98)
+                const float4 cv = L.cvec[fbits(B.z)];
+                center = center + splat(r.time) * mk(cv.x, cv.y, cv.z);
+            }
+        }
+        const f3 oc = r.o - center;
+        const float half_b = dot(oc, r.d);
+        const float c = length_squared(oc) - B.x * B.x;
+        const float disc = half_b * half_b - rt.a * c;
+        if (disc >= 0) {
+            const float sq = __builtin_sqrtf(disc);
+            float root = (-half_b - sq) / rt.a;
+            bool ok = kTmin < root && root < closest;
+            if (!ok) {
+                root = (-half_b + sq) / rt.a;
+                ok = kTmin < root && root < closest;
+            }
+            if (ok) {
+                closest = root;
+                hit = (int)i;
+            }
+        }
+        return w & RTW_SKIP_MASK;
+    }
+    cnt.nodes++;
+    float t0x = (A.x - r.o.x) * rt.inv.x, t1x = (B.x - r.o.x) * rt.inv.x;
+    float t0y = (A.y - r.o.y) * rt.inv.y, t1y = (B.y - r.o.y) * rt.inv.y;
+    float t0z = (A.z - r.o.z) * rt.inv.z, t1z = (B.z - r.o.z) * rt.inv.z;
+    if (rt.inv.x < 0) { float tt = t1x; t1x = t0x; t0x = tt; }
+    if (rt.inv.y < 0) { float tt = t1y; t1y = t0y; t0y = tt; }
+    if (rt.inv.z < 0) { float tt = t1z; t1z = t0z; t0z = tt; }
+    const float lo = __builtin_fmaxf(__builtin_fmaxf(kTmin, t0x), __builtin_fmaxf(t0y, t0z));
+    const float hi = __builtin_fminf(__builtin_fminf(closest, t1x), __builtin_fminf(t1y, t1z));
+    return (hi <= lo) ? w : i + 1;
+}
+
+// World hit for one ray (whole walk).  Returns leaf node index or -1.
+template <uint32_t FEAT>
+__device__ __forceinline__ int traverse(const float4* __restrict__ nodes, const rtw_launch& L, const Ray& r,
+                                        float& t_out, Counters& cnt) {
+    const RayTrav rt = ray_trav(r);
     float closest = kInf;
     int hit = -1;
     uint32_t i = 0;
     const uint32_t n = L.n_nodes;
-    while (i < n) {
-        const float4 A = L.nodes[2 * i];
-        const uint32_t w = fbits(A.w);
-        if (w & RTW_LEAF_BIT) {
-            cnt.leaves++;
-            const float4 B = L.nodes[2 * i + 1];
-            f3 center = mk(A.x, A.y, A.z);
-            if (fbits(B.w)) {
-                const float4 cv = L.cvec[fbits(B.z)];
-                center = center + splat(r.time) * mk(cv.x, cv.y, cv.z);
-            }
-            const f3 oc = r.o - center;
-            const float half_b = dot(oc, r.d);
-            const float c = length_squared(oc) - B.x * B.x;
-            const float disc = half_b * half_b - a * c;
-            if (disc >= 0) {
-                const float sq = __builtin_sqrtf(disc);
-                float root = (-half_b - sq) / a;
-                bool ok = tmin < root && root < closest;
-                if (!ok) {
-                    root = (-half_b + sq) / a;
-                    ok = tmin < root && root < closest;
-                }
-                if (ok) {
-                    closest = root;
-                    hit = (int)i;
-                }
-            }
-            i = w & RTW_SKIP_MASK;
-        } else {
-            cnt.nodes++;
-            const float4 B = L.nodes[2 * i + 1];
-            float lo = tmin, hi = closest;
-            {
-                float t0 = (A.x - r.o.x) * inv.x, t1 = (B.x - r.o.x) * inv.x;
-                if (inv.x < 0) { float tt = t1; t1 = t0; t0 = tt; }
-                if (t0 > lo) lo = t0;
-                if (t1 < hi) hi = t1;
-            }
-            {
-                float t0 = (A.y - r.o.y) * inv.y, t1 = (B.y - r.o.y) * inv.y;
-                if (inv.y < 0) { float tt = t1; t1 = t0; t0 = tt; }
-                if (t0 > lo) lo = t0;
-                if (t1 < hi) hi = t1;
-            }
-            {
-                float t0 = (A.z - r.o.z) * inv.z, t1 = (B.z - r.o.z) * inv.z;
-                if (inv.z < 0) { float tt = t1; t1 = t0; t0 = tt; }
-                if (t0 > lo) lo = t0;
-                if (t1 < hi) hi = t1;
-            }
-            // per-axis early exit of aabb.zig:111 is equivalent: lo only grows, hi only shrinks
-            i = (hi <= lo) ? w : i + 1;
-        }
-    }
+    while (i < n) i = trav_step<FEAT>(nodes, L, r, rt, i, closest, hit, cnt);
     t_out = closest;
     return hit;
 }
 
+__device__ __forceinline__ f3 background(const rtw_launch& L, const Ray& r) {
+    if (L.bg_mode == RTW_BG_GRADIENT) {  // camera.zig:204-206
+        f3 ud = unit_vector(r.d);
+        float a = 0.5f * (ud.y + 1.0f);
+        return mk(1, 1, 1) * splat(1.0f - a) + mk(0.5f, 0.7f, 1.0f) * splat(a);
+    }
+    return ld3(L.background);  // camera.zig:207
+}
+
+// Hit record for the closest hit + Material.emitted/scatter
+// (objects.zig:139-145, material.zig:18-144).  Adds thr*emission to acc and
+// returns true with (att, sc) when the ray scatters.
+template <uint32_t FEAT>
+__device__ __forceinline__ bool shade(const float4* __restrict__ nodes, const rtw_launch& L, const Ray& r, int hit,
+                                      float t, rtw_rng& rng, f3 thr, f3& acc, f3& att, Ray& sc) {
+    const float4 A = nodes[2 * hit];
+    const float4 B = nodes[2 * hit + 1];
+    f3 center = mk(A.x, A.y, A.z);
+    if constexpr ((FEAT & RTW_F_MOVING) != 0) {
+        if (fbits(B.w)) {
+            const float4 cv = L.cvec[fbits(B.z)];
+            center = center + splat(r.time) * mk(cv.x, cv.y, cv.z);
+        }
+    }
+    const f3 p = r.o + splat(t) * r.d;
+    const f3 outward = divs(p - center, B.x);
+    const bool front = dot(r.d, outward) < 0;
+    const f3 normal = front ? outward : -outward;
+    const rtw_dev_material m = L.mats[fbits(B.y)];
+    sc.o = p;
+    sc.time = r.time;
+    switch (m.kind) {
+    case RTW_MAT_LAMBERTIAN: {  // material.zig:43-54
+        f3 dir = normal + random_unit_vector(rng);
+        if (near_zero(dir)) dir = normal;
+        sc.d = dir;
+        att = texture_value<FEAT>(L, m.texture, outward, p);
+        return true;
+    }
+    case RTW_MAT_METAL: {  // material.zig:65-70
+        f3 refl = reflect(unit_vector(r.d), normal);
+        sc.d = refl + splat(m.fuzz) * random_unit_vector(rng);
+        att = ld3(m.albedo);
+        return dot(sc.d, normal) > 0;
+    }
+    case RTW_MAT_DIELECTRIC: {  // material.zig:80-98
+        att = mk(1, 1, 1);
+        const float ratio = front ? (1.0f / m.ir) : m.ir;
+        const f3 ud = unit_vector(r.d);
+        const float dd = dot(-ud, normal);
+        const float cos_theta = dd < 1.0f ? dd : 1.0f;
+        const float sin_theta = __builtin_sqrtf(1.0f - cos_theta * cos_theta);
+        const bool cannot = ratio * sin_theta > 1.0f;
+        if (cannot || reflectance(cos_theta, ratio) > rnd(rng))
+            sc.d = reflect(ud, normal);
+        else
+            sc.d = refract(ud, normal, ratio);
+        return true;
+    }
+    default:
+        break;
+    }
+    if constexpr ((FEAT & RTW_F_LIGHT) != 0) {
+        if (m.kind == RTW_MAT_DIFFUSE_LIGHT) {  // material.zig:119-125
+            acc = acc + thr * texture_value<FEAT>(L, m.texture, outward, p);
+            return false;
+        }
+        // RTW_MAT_ISOTROPIC (material.zig:139-143)
+        sc.d = random_unit_vector(rng);
+        att = texture_value<FEAT>(L, m.texture, outward, p);
+        return true;
+    }
+    return false;
+}
+
 // One sample's radiance: getRay + iterative rayColor (camera.zig:169-208).
-__device__ f3 sample_radiance(const rtw_launch& L, uint32_t pixel, uint32_t x, uint32_t y, uint32_t s,
-                              Counters& cnt) {
+template <uint32_t FEAT>
+__device__ f3 sample_radiance(const float4* __restrict__ nodes, const rtw_launch& L, uint32_t pixel, uint32_t x,
+                              uint32_t y, uint32_t s, Counters& cnt) {
     rtw_rng rng;
     rng.s = rtw_mix64(L.key0 ^ (((uint64_t)pixel << 32) | (uint64_t)s));
     Ray r = get_ray(L, x, y, rng);
@@ -306,93 +401,26 @@ __device__ f3 sample_radiance(const rtw_launch& L, uint32_t pixel, uint32_t x, u
     for (uint32_t depth = L.max_depth; depth > 0; depth--) {
         cnt.rays++;
         float t;
-        const int hit = traverse(L, r, t, cnt);
+        const int hit = traverse<FEAT>(nodes, L, r, t, cnt);
         if (hit < 0) {
-            f3 bg;
-            if (L.bg_mode == RTW_BG_GRADIENT) {  // camera.zig:204-206
-                f3 ud = unit_vector(r.d);
-                float a = 0.5f * (ud.y + 1.0f);
-                bg = mk(1, 1, 1) * splat(1.0f - a) + mk(0.5f, 0.7f, 1.0f) * splat(a);
-            } else {
-                bg = ld3(L.background);
-            }
-            acc = acc + thr * bg;
+            acc = acc + thr * background(L, r);
             break;
         }
-        // HitRecord (objects.zig:139-145), recomputed once for the closest hit
-        const float4 A = L.nodes[2 * hit];
-        const float4 B = L.nodes[2 * hit + 1];
-        f3 center = mk(A.x, A.y, A.z);
-        if (fbits(B.w)) {
-            const float4 cv = L.cvec[fbits(B.z)];
-            center = center + splat(r.time) * mk(cv.x, cv.y, cv.z);
-        }
-        const f3 p = r.o + splat(t) * r.d;
-        const f3 outward = divs(p - center, B.x);
-        const bool front = dot(r.d, outward) < 0;
-        const f3 normal = front ? outward : -outward;
-        const rtw_dev_material m = L.mats[fbits(B.y)];
-
         f3 att;
         Ray sc;
-        sc.o = p;
-        sc.time = r.time;
-        bool scattered = true;
-        switch (m.kind) {
-        case RTW_MAT_LAMBERTIAN: {  // material.zig:43-54
-            f3 dir = normal + random_unit_vector(rng);
-            if (near_zero(dir)) dir = normal;
-            sc.d = dir;
-            att = texture_value(L, m.texture, outward, p);
-            break;
-        }
-        case RTW_MAT_METAL: {  // material.zig:65-70
-            f3 refl = reflect(unit_vector(r.d), normal);
-            sc.d = refl + splat(m.fuzz) * random_unit_vector(rng);
-            att = ld3(m.albedo);
-            scattered = dot(sc.d, normal) > 0;
-            break;
-        }
-        case RTW_MAT_DIELECTRIC: {  // material.zig:80-98
-            att = mk(1, 1, 1);
-            const float ratio = front ? (1.0f / m.ir) : m.ir;
-            const f3 ud = unit_vector(r.d);
-            const float dd = dot(-ud, normal);
-            const float cos_theta = dd < 1.0f ? dd : 1.0f;
-            const float sin_theta = __builtin_sqrtf(1.0f - cos_theta * cos_theta);
-            const bool cannot = ratio * sin_theta > 1.0f;
-            if (cannot || reflectance(cos_theta, ratio) > rnd(rng))
-                sc.d = reflect(ud, normal);
-            else
-                sc.d = refract(ud, normal, ratio);
-            break;
-        }
-        case RTW_MAT_DIFFUSE_LIGHT: {  // material.zig:119-125
-            acc = acc + thr * texture_value(L, m.texture, outward, p);
-            scattered = false;
-            break;
-        }
-        default: {  // RTW_MAT_ISOTROPIC (material.zig:139-143)
-            sc.d = random_unit_vector(rng);
-            att = texture_value(L, m.texture, outward, p);
-            break;
-        }
-        }
-        if (!scattered) break;
+        if (!shade<FEAT>(nodes, L, r, hit, t, rng, thr, acc, att, sc)) break;
         thr = thr * att;
         r = sc;
     }
     return acc;
 }
 
-__device__ __forceinline__ bool map_row(const rtw_launch& L, uint32_t r, uint32_t& y, uint32_t& out_row) {
+__device__ __forceinline__ bool map_row(const rtw_launch& L, uint32_t r, uint32_t& y) {
     if (L.n_shards) {
         const uint32_t blk = r / L.rpb;
         y = (blk * L.n_shards + L.shard) * L.rpb + r % L.rpb;
-        out_row = r;
     } else {
         y = r;
-        out_row = r;
     }
     return y < L.H;
 }
@@ -406,24 +434,29 @@ __device__ __forceinline__ void flush_counters(const rtw_launch& L, const Counte
     if (c.nans) atomicAdd(&L.counters[RTW_STAT_NAN], (unsigned long long)c.nans);
 }
 
+__device__ __forceinline__ bool is_nan3(f3 c) { return !(c.x == c.x) || !(c.y == c.y) || !(c.z == c.z); }
+
+// ---------------------------------------------------------------------------
 // v0: one thread per pixel, each wave an 8x8 pixel tile, block = 32x8 pixels;
 // samples [s0, s1) looped in order, accumulator read once / written once.
+// Kept as the simple reference kernel (and the A/B baseline for v1).
+// ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void render_pixels_v0(rtw_launch L) {
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint32_t x = blockIdx.x * 32 + wave * 8 + (lane & 7);
     const uint32_t r = L.row0 + blockIdx.y * 8 + (lane >> 3);
     if (x >= L.W || r >= L.row0 + L.n_rows) return;
-    uint32_t y, out_row;
-    if (!map_row(L, r, y, out_row)) return;
+    uint32_t y;
+    if (!map_row(L, r, y)) return;
     const uint32_t pixel = y * L.W + x;
     if (!L.n_shards && (pixel < L.pix_begin || pixel >= L.pix_end)) return;
-    float4* slot = L.accum + (size_t)out_row * L.W + x;
+    float4* slot = L.accum + (size_t)r * L.W + x;
     float4 acc = *slot;
     Counters cnt;
     const uint32_t px = x + L.pixel_offset, py = y + L.pixel_offset;  // camera.zig:100-101
     for (uint32_t s = L.s0; s < L.s1; s++) {
-        f3 c = sample_radiance(L, pixel, px, py, s, cnt);
-        if (!(c.x == c.x) || !(c.y == c.y) || !(c.z == c.z)) cnt.nans++;
+        f3 c = sample_radiance<RTW_F_ALL>(L.nodes, L, pixel, px, py, s, cnt);
+        if (is_nan3(c)) cnt.nans++;
         acc.x += c.x;
         acc.y += c.y;
         acc.z += c.z;
@@ -431,6 +464,183 @@ __global__ __launch_bounds__(256) void render_pixels_v0(rtw_launch L) {
     acc.w = (float)L.s1;  // writeColor: buffer[i][3] = number_of_samples (camera.zig:56)
     *slot = acc;
     flush_counters(L, cnt, L.s1 - L.s0);
+}
+
+// ---------------------------------------------------------------------------
+// v1: persistent megakernel.
+//  * grid = resident blocks only; each wave pulls 16x16 pixel tiles from a
+//    global atomic work counter and hands pixels to its lanes one at a time
+//    (ballot + mbcnt), so a lane that finishes its pixel immediately takes the
+//    next one -- no lane waits for the slowest pixel of a fixed tile;
+//  * a lane owns one pixel for all samples [s0, s1) and adds the sample
+//    radiances in sample order (bit-identical sums to the reference order);
+//  * per-lane path regeneration: when a lane's path ends it starts the next
+//    sample at once (ST_NEWSAMPLE) instead of waiting for the wave;
+//  * traversal runs node steps until >= shade_min lanes have finished their
+//    walk (ballot popcount), then shades only those lanes: the wave's shading
+//    pass is shared by many lanes instead of one;
+//  * the BVH (<= RTW_LDS_NODES nodes) is staged once per block in LDS.
+// ---------------------------------------------------------------------------
+enum : uint32_t { ST_TRAV = 0, ST_SHADE = 1, ST_NEWSAMPLE = 2, ST_NEWPIXEL = 3, ST_DONE = 4 };
+
+__device__ __forceinline__ uint32_t popc64(uint64_t m) { return (uint32_t)__popcll(m); }
+
+template <uint32_t FEAT, bool LDS>
+__global__ __launch_bounds__(256) void render_persistent_v1(rtw_launch L) {
+    extern __shared__ float4 lds_nodes[];
+    const float4* __restrict__ nodes;
+    if constexpr (LDS) {
+        const uint32_t n4 = 2 * L.n_nodes;
+        for (uint32_t k = threadIdx.x; k < n4; k += blockDim.x) lds_nodes[k] = L.nodes[k];
+        __syncthreads();
+        nodes = lds_nodes;
+    } else {
+        nodes = L.nodes;
+    }
+    const uint32_t lane = __lane_id();
+    const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    const uint32_t n_nodes = L.n_nodes;
+
+    // wave-uniform queue state
+    uint32_t q_cur = 0, q_end = 0;
+    bool q_empty = false;
+
+    uint32_t st = ST_NEWPIXEL;
+    uint32_t pixel = 0, out_idx = 0, px = 0, py = 0, s = 0;
+    f3 acc = mk(0, 0, 0), Ls = mk(0, 0, 0), thr = mk(1, 1, 1);
+    rtw_rng rng;
+    rng.s = 0;
+    Ray ray;
+    ray.o = ray.d = mk(0, 0, 0);
+    ray.time = 0;
+    RayTrav rt;
+    rt.inv = mk(0, 0, 0);
+    rt.a = 0;
+    uint32_t depth = 0, ti = 0;
+    float closest = kInf;
+    int hit = -1;
+    Counters cnt;
+    uint32_t samples_done = 0;
+
+    for (;;) {
+        // ---- 1. hand pixels to lanes that need one
+        uint64_t need = __ballot(st == ST_NEWPIXEL);
+        while (need) {
+            if (q_cur >= q_end) {
+                if (q_empty) {
+                    if (st == ST_NEWPIXEL) st = ST_DONE;
+                    break;
+                }
+                uint32_t t = 0;
+                if (lane == 0) t = atomicAdd(L.work_counter, 1u);
+                t = __builtin_amdgcn_readfirstlane(t);
+                if (t >= L.n_tiles) {
+                    q_empty = true;
+                    continue;
+                }
+                q_cur = t * RTW_TILE;
+                q_end = q_cur + RTW_TILE;
+            }
+            const uint32_t avail = q_end - q_cur;
+            const uint32_t rank = popc64(need & lt_mask);
+            if (st == ST_NEWPIXEL && rank < avail) {
+                const uint32_t seq = q_cur + rank;
+                const uint32_t tile = seq / RTW_TILE, k = seq % RTW_TILE;
+                const uint32_t x = (tile % L.n_tiles_x) * RTW_TILE_W + k % RTW_TILE_W;
+                const uint32_t r = L.row0 + (tile / L.n_tiles_x) * RTW_TILE_H + k / RTW_TILE_W;
+                uint32_t y;
+                if (x < L.W && r < L.row0 + L.n_rows && map_row(L, r, y)) {
+                    const uint32_t pix = y * L.W + x;
+                    if (L.n_shards || (pix >= L.pix_begin && pix < L.pix_end)) {
+                        pixel = pix;
+                        out_idx = r * L.W + x;
+                        px = x + L.pixel_offset;  // camera.zig:100-101
+                        py = y + L.pixel_offset;
+                        s = L.s0;
+                        const float4 a0 = L.accum[out_idx];
+                        acc = mk(a0.x, a0.y, a0.z);
+                        st = (s < L.s1) ? ST_NEWSAMPLE : ST_NEWPIXEL;
+                    }
+                }
+            }
+            const uint32_t cnt_need = popc64(need);
+            q_cur += cnt_need < avail ? cnt_need : avail;
+            need = __ballot(st == ST_NEWPIXEL);
+        }
+        const uint64_t live = __ballot(st != ST_DONE);
+        if (!live) break;
+
+        // ---- 2. start a new sample: getRay (camera.zig:169-180)
+        if (st == ST_NEWSAMPLE) {
+            rng.s = rtw_mix64(L.key0 ^ (((uint64_t)pixel << 32) | (uint64_t)s));
+            ray = get_ray(L, px, py, rng);
+            thr = mk(1, 1, 1);
+            Ls = mk(0, 0, 0);
+            depth = L.max_depth;
+            if (depth == 0) {
+                st = ST_SHADE;  // rayColor(r, 0) = 0: finishes below without tracing
+                hit = -2;
+            } else {
+                rt = ray_trav(ray);
+                ti = 0;
+                closest = kInf;
+                hit = -1;
+                st = ST_TRAV;
+                cnt.rays++;
+            }
+        }
+
+        // ---- 3. traversal until enough lanes are ready to shade
+        {
+            const uint32_t n_live = popc64(live);
+            const uint32_t want = L.shade_min < n_live ? L.shade_min : n_live;
+            for (;;) {
+                const uint64_t trav = __ballot(st == ST_TRAV);
+                if (!trav) break;
+                if (popc64(__ballot(st == ST_SHADE)) >= want) break;
+                if (st == ST_TRAV) {
+                    ti = trav_step<FEAT>(nodes, L, ray, rt, ti, closest, hit, cnt);
+                    if (ti >= n_nodes) st = ST_SHADE;
+                }
+            }
+        }
+
+        // ---- 4. shade lanes whose walk is complete
+        if (st == ST_SHADE) {
+            bool cont = false;
+            if (hit == -1) {
+                Ls = Ls + thr * background(L, ray);
+            } else if (hit >= 0) {
+                f3 att;
+                Ray sc;
+                if (shade<FEAT>(nodes, L, ray, hit, closest, rng, thr, Ls, att, sc) && depth > 1) {
+                    thr = thr * att;
+                    ray = sc;
+                    depth--;
+                    rt = ray_trav(ray);
+                    ti = 0;
+                    closest = kInf;
+                    hit = -1;
+                    st = ST_TRAV;
+                    cnt.rays++;
+                    cont = true;
+                }
+            }
+            if (!cont) {
+                if (is_nan3(Ls)) cnt.nans++;
+                acc = acc + Ls;
+                samples_done++;
+                s++;
+                if (s < L.s1) {
+                    st = ST_NEWSAMPLE;
+                } else {
+                    L.accum[out_idx] = make_float4(acc.x, acc.y, acc.z, (float)L.s1);  // camera.zig:55-56
+                    st = ST_NEWPIXEL;
+                }
+            }
+        }
+    }
+    flush_counters(L, cnt, samples_done);
 }
 
 __global__ void debug_rng_kernel(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t n, float* out) {
@@ -444,7 +654,7 @@ __global__ void debug_sample_kernel(rtw_launch L, uint32_t pixel, uint32_t sampl
     if (threadIdx.x | blockIdx.x) return;
     Counters cnt;
     const uint32_t x = pixel % L.W, y = pixel / L.W;
-    f3 c = sample_radiance(L, pixel, x + L.pixel_offset, y + L.pixel_offset, sample, cnt);
+    f3 c = sample_radiance<RTW_F_ALL>(L.nodes, L, pixel, x + L.pixel_offset, y + L.pixel_offset, sample, cnt);
     out[0] = c.x;
     out[1] = c.y;
     out[2] = c.z;
@@ -453,13 +663,63 @@ __global__ void debug_sample_kernel(rtw_launch L, uint32_t pixel, uint32_t sampl
     out[5] = (float)cnt.leaves;
 }
 
+template <uint32_t FEAT, bool LDS>
+void launch_v1(const rtw_launch& L, hipStream_t stream, int grid) {
+    const size_t lds = LDS ? (size_t)L.n_nodes * 32 : 0;
+    hipLaunchKernelGGL((render_persistent_v1<FEAT, LDS>), dim3(grid), dim3(256), lds, stream, L);
+}
+
+template <uint32_t FEAT, bool LDS>
+int occupancy_v1() {
+    int b = 0;
+    const size_t lds = LDS ? (size_t)RTW_LDS_NODES * 32 : 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, render_persistent_v1<FEAT, LDS>, 256, lds) != hipSuccess)
+        b = 1;
+    return b < 1 ? 1 : b;
+}
+
+uint32_t pick_feat(uint32_t f) {
+    if ((f & ~RTW_F_CHECKER) == 0) return f ? RTW_F_CHECKER : 0u;
+    return RTW_F_ALL;
+}
+
 }  // namespace
 
-void rtw_launch_render(const rtw_launch& L, void* stream, int variant) {
-    (void)variant;
-    dim3 block(256);
-    dim3 grid((L.W + 31) / 32, (L.n_rows + 7) / 8);
-    hipLaunchKernelGGL(render_pixels_v0, grid, block, 0, (hipStream_t)stream, L);
+void rtw_launch_render(const rtw_launch& L, void* stream, int variant, int grid) {
+    hipStream_t st = (hipStream_t)stream;
+    if (variant == 0) {
+        dim3 block(256);
+        dim3 g((L.W + 31) / 32, (L.n_rows + 7) / 8);
+        hipLaunchKernelGGL(render_pixels_v0, g, block, 0, st, L);
+        return;
+    }
+    const bool lds = L.n_nodes <= RTW_LDS_NODES;
+    switch (pick_feat(L.feat)) {
+    case 0u:
+        lds ? launch_v1<0u, true>(L, st, grid) : launch_v1<0u, false>(L, st, grid);
+        break;
+    case RTW_F_CHECKER:
+        lds ? launch_v1<RTW_F_CHECKER, true>(L, st, grid) : launch_v1<RTW_F_CHECKER, false>(L, st, grid);
+        break;
+    default:
+        lds ? launch_v1<RTW_F_ALL, true>(L, st, grid) : launch_v1<RTW_F_ALL, false>(L, st, grid);
+        break;
+    }
+}
+
+int rtw_persistent_grid(uint32_t feat, bool lds, void* stream) {
+    (void)stream;
+    int dev = 0, n_cu = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
+    if (n_cu <= 0) n_cu = 256;
+    int b;
+    switch (pick_feat(feat)) {
+    case 0u: b = lds ? occupancy_v1<0u, true>() : occupancy_v1<0u, false>(); break;
+    case RTW_F_CHECKER: b = lds ? occupancy_v1<RTW_F_CHECKER, true>() : occupancy_v1<RTW_F_CHECKER, false>(); break;
+    default: b = lds ? occupancy_v1<RTW_F_ALL, true>() : occupancy_v1<RTW_F_ALL, false>(); break;
+    }
+    return n_cu * b;
 }
 
 void rtw_launch_debug_rng(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t n, float* d_out, void* stream) {
