@@ -37,6 +37,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="c2", choices=["c2", "c3", "c4", "c5"])
     ap.add_argument("--spp", type=int, default=0, help="override spp (0 = config's)")
+    ap.add_argument("--bvh", default="sah", choices=["sah", "reference"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline duration")
     ap.add_argument("--cpu-threads", type=int, default=8, help="reference uses 8 render threads (main.zig:41)")
@@ -64,10 +65,13 @@ def main():
     L = pkg.lib()
     cfg = pkg.configs.CONFIGS[args.config]
     objs = cfg.objects()
-    arr = pkg.flatten(objs)
+    bvh_mode = {"sah": pkg._abi.RTW_BVH_SAH, "reference": pkg._abi.RTW_BVH_REFERENCE}[args.bvh]
+    arr = pkg.flatten(objs, bvh_mode=bvh_mode)
     t0 = time.time()
     world = pkg.World(arr, device=local_rank)
     build_s = time.time() - t0
+    # the reference topology (bvh.zig) defines the algorithmic bytes
+    world_ref = pkg.World(pkg.flatten(objs, bvh_mode=pkg._abi.RTW_BVH_REFERENCE), device=local_rank)
     cam = cfg.camera()
     if args.spp:
         cam.samples_per_pixel = args.spp
@@ -95,11 +99,11 @@ def main():
     src_idx = torch.tensor(src_idx, device="cuda")
     dst_idx = torch.tensor(dst_idx, device="cuda")
 
-    def render_step(counters=None):
+    def render_step(counters=None, w=None):
         tile.zero_()
         o = opts if counters is None else pkg._abi.RtwRenderOpts(spp, pkg._abi.RTW_RENDER_NO_SYNC, counters)
-        rc = L.rtw_render_rows_device(world.handle, C.byref(cam.derived), ROWS_PER_BLOCK, world_size, rank, 0, spp,
-                                      0, tile.data_ptr(), C.c_void_p(stream.cuda_stream), C.byref(o))
+        rc = L.rtw_render_rows_device((w or world).handle, C.byref(cam.derived), ROWS_PER_BLOCK, world_size, rank, 0,
+                                      spp, 0, tile.data_ptr(), C.c_void_p(stream.cuda_stream), C.byref(o))
         pkg._abi.check(rc, "rtw_render_rows_device")
 
     def gather_step():
@@ -111,14 +115,20 @@ def main():
         else:
             image.view(-1, W, 4).index_copy_(0, dst_idx, tile.view(-1, W, 4).index_select(0, src_idx))
 
-    # ---- algorithmic bytes of one step: counted pass (reference traversal == device traversal)
-    cnt = torch.zeros(8, dtype=torch.int64, device="cuda")
-    render_step(cnt.data_ptr())
-    torch.cuda.synchronize()
-    c = cnt.cpu().numpy()
-    nodes, leaves, rays, samples = (int(c[pkg._abi.RTW_STAT_NODES]), int(c[pkg._abi.RTW_STAT_LEAVES]),
-                                    int(c[pkg._abi.RTW_STAT_RAYS]), int(c[pkg._abi.RTW_STAT_SAMPLES]))
-    nan_count = int(c[pkg._abi.RTW_STAT_NAN])
+    # ---- algorithmic bytes of one step: counted pass on the reference topology (the device
+    # walk of a reference-topology tree visits exactly the nodes bvh.zig's recursion visits)
+    def counted(w):
+        cnt = torch.zeros(8, dtype=torch.int64, device="cuda")
+        render_step(cnt.data_ptr(), w)
+        torch.cuda.synchronize()
+        c = cnt.cpu().numpy()
+        return {k: int(c[getattr(pkg._abi, "RTW_STAT_" + k.upper())]) for k in ("nodes", "leaves", "rays", "samples",
+                                                                                 "nan")}
+    cref = counted(world_ref)
+    cdev = counted(world)
+    world_ref.close()
+    nodes, leaves, rays, samples = cref["nodes"], cref["leaves"], cref["rays"], cref["samples"]
+    nan_count = cdev["nan"]
     pixels = my_rows * W
     alg_bytes = NODE_BYTES * (nodes + leaves) + 32 * pixels
 
@@ -177,11 +187,13 @@ def main():
                        + (" + RCCL gather" if distributed else ""), "rows_per_block": ROWS_PER_BLOCK},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                         "kernel": "render_pixels_v0", "avg_launch_ms": round(avg_kernel_s * 1e3, 3),
+                         "kernel": "render_persistent_v1", "avg_launch_ms": round(avg_kernel_s * 1e3, 3),
                          "alg_bytes_per_launch": alg_bytes,
                          "alg_bytes_per_sample": round(alg_bytes / max(1, samples), 2),
                          "rays_per_sample": round(rays / max(1, samples), 4),
-                         "nodes_per_ray": round((nodes + leaves) / max(1, rays), 3)},
+                         "nodes_per_ray_reference": round((nodes + leaves) / max(1, rays), 3),
+                         "nodes_per_ray_device": round((cdev["nodes"] + cdev["leaves"]) / max(1, cdev["rays"]), 3),
+                         "bvh": args.bvh},
             "cpu_baseline": cpu,
             "nan_samples": nan_count,
             "scene_build_s": round(build_s, 4),

@@ -105,8 +105,10 @@ typedef struct rtw_perlin {
 } rtw_perlin;
 
 enum rtw_bvh_mode {
-    RTW_BVH_REFERENCE = 0      /* BVHTree.constructTree (src/bvh.zig:43-71): random axis from the
+    RTW_BVH_REFERENCE = 0,     /* BVHTree.constructTree (src/bvh.zig:43-71): random axis from the
                                   seeded build stream, std.sort.heap by box min, median split */
+    RTW_BVH_SAH = 1            /* binned SAH, single-sphere leaves, children ordered front-to-back
+                                  along order_dir.  Same closest hit (topology-independent). */
 };
 
 typedef struct rtw_scene_desc {
@@ -117,7 +119,7 @@ typedef struct rtw_scene_desc {
     const rtw_perlin* perlins;     uint32_t n_perlins;
     uint64_t bvh_seed;
     uint32_t bvh_mode;
-    uint32_t _pad;
+    float order_dir[3];        /* RTW_BVH_SAH child order hint (e.g. camera forward); 0 = (0,-1,0) */
 } rtw_scene_desc;
 
 /* ---------------------------------------------------------------------------

@@ -80,7 +80,7 @@ def test_bvh_flatten_matches_oracle_tree(rtw, oracle, earth_rgba, scene, seed):
     """Product BVH builder (C++, pre-order + skip links) == oracle pointer tree."""
     imgs = [rtw.Image(earth_rgba)]
     objs = rtw.worlds.generate_world(0, scene, imgs)
-    arr = rtw.flatten(objs, bvh_seed=seed)
+    arr = rtw.flatten(objs, bvh_seed=seed, bvh_mode=rtw._abi.RTW_BVH_REFERENCE)
     nodes = rtw.scene.flatten_bvh(arr)
     ow = oracle.World(arr.spheres, arr.materials, arr.textures, images=[earth_rgba], bvh_seed=seed)
     d = ow.dump()
@@ -100,11 +100,34 @@ def test_bvh_flatten_matches_oracle_tree(rtw, oracle, earth_rgba, scene, seed):
     assert np.array_equal(b[is_leaf, 1].view(np.uint32), arr.spheres["material"][sid])
 
 
-def test_stress_scene_builds(rtw):
+@pytest.mark.parametrize("mode", [0, 1])
+def test_stress_scene_builds(rtw, mode):
     objs = rtw.worlds.stress_world(2000, 0)
-    arr = rtw.flatten(objs)
+    arr = rtw.flatten(objs, bvh_mode=mode)
     nodes = rtw.scene.flatten_bvh(arr)
     assert len(nodes) == 2 * len(objs) - 1
+
+
+def test_sah_tree_is_valid_bvh(rtw):
+    """SAH mode: every sphere appears in exactly one leaf, skip links are proper
+    pre-order subtree ends, and every inner box encloses its subtree."""
+    arr = rtw.flatten(rtw.worlds.generate_world(0, "book1"), bvh_mode=rtw._abi.RTW_BVH_SAH)
+    nodes = rtw.scene.flatten_bvh(arr)
+    n = len(nodes)
+    a, b = nodes["a"], nodes["b"]
+    w = a[:, 3].view(np.uint32)
+    leaf = (w & 0x80000000) != 0
+    skip = (w & 0x7FFFFFFF).astype(np.int64)
+    sid = b[leaf, 2].view(np.uint32)
+    assert sorted(sid.tolist()) == list(range(len(arr.spheres)))
+    assert (skip[leaf] == np.nonzero(leaf)[0] + 1).all()
+    r = arr.spheres["radius"]
+    c = arr.spheres["center1"]
+    for i in np.nonzero(~leaf)[0]:
+        assert i + 1 < skip[i] <= n
+        sub = np.arange(i + 1, skip[i])
+        ls = b[sub[leaf[sub]], 2].view(np.uint32)
+        assert (c[ls] - r[ls, None] >= a[i, :3]).all() and (c[ls] + r[ls, None] <= b[i, :3]).all()
 
 
 def test_shard_rows_partition(rtw):

@@ -23,9 +23,12 @@ pytestmark = pytest.mark.gpu
 REL = 1e-5
 
 
-@pytest.fixture(scope="module")
-def book1(rtw):
-    arr = rtw.flatten(rtw.worlds.generate_world(0, "book1"))
+@pytest.fixture(scope="module", params=["sah", "reference"])
+def book1(rtw, request):
+    """Book-1 world in both BVH modes: the SAH tree (product default) and the
+    reference's random-axis median topology (exact traversal replay)."""
+    mode = {"sah": rtw._abi.RTW_BVH_SAH, "reference": rtw._abi.RTW_BVH_REFERENCE}[request.param]
+    arr = rtw.flatten(rtw.worlds.generate_world(0, "book1"), bvh_mode=mode)
     return arr, rtw.World(arr)
 
 
@@ -229,8 +232,10 @@ def test_textured_c5_crop(rtw, oracle, earth_rgba):
 
 def test_stress_100k_crop(rtw, oracle):
     """Config 4 (100k spheres): deep reference-topology BVH, GPU vs oracle on a strip."""
-    arr = rtw.flatten(rtw.worlds.stress_world(100_000, 0))
+    arr = rtw.flatten(rtw.worlds.stress_world(100_000, 0), bvh_mode=rtw._abi.RTW_BVH_REFERENCE)
     world = rtw.World(arr)
+    arr_sah = rtw.flatten(rtw.worlds.stress_world(100_000, 0))
+    world_sah = rtw.World(arr_sah)
     st = world.stats()
     assert st["n_nodes"] == 2 * len(arr.spheres) - 1
     cam = rtw.book1_camera(image_width=1920, aspect_ratio=16 / 9, spp=2).init()
@@ -242,13 +247,17 @@ def test_stress_100k_crop(rtw, oracle):
     pix = np.arange(y0 * 1920, y1 * 1920, dtype=np.uint32)
     ref = ow.render_pixels(ocam, 0, pix, 0, 2, threads=os.cpu_count() or 1)
     assert close(buf[pix, :3], ref[:, :3]).all()
+    buf2 = render_rows(rtw, world_sah, cam, y0, y1, 0, 2, 0)
+    assert close(buf2[pix, :3], ref[:, :3]).all()
 
 
 def test_device_counters_equal_reference_traversal(rtw, oracle, book1, oracle_book1):
     """The stackless walk visits exactly the reference's nodes: device ray/node/leaf
     counters == oracle's instrumented recursion on the same pixels."""
     import torch
-    _, world = book1
+    arr, world = book1
+    if arr.bvh_mode != rtw._abi.RTW_BVH_REFERENCE:
+        pytest.skip("traversal-count identity holds for the reference topology")
     cam = rtw.book1_camera(image_width=1200, aspect_ratio=1.5, spp=2).init()
     y0, y1 = 300, 332
     acc = torch.zeros((cam.size, 4), dtype=torch.float32, device="cuda")

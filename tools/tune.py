@@ -24,10 +24,20 @@ cam.init()
 acc = torch.zeros((cam.size, 4), dtype=torch.float32, device="cuda")
 stream = torch.cuda.Stream()
 for st in settings:
-    for k in ("RTW_KERNEL", "RTW_SHADE_MIN"):
+    st = dict(st)
+    for k in ("RTW_KERNEL", "RTW_SHADE_MIN", "RTW_WAVES"):
         os.environ.pop(k, None)
+    arr.bvh_mode = {"ref": 0, "sah": 1}[st.pop("bvh", "ref")]
+    arr.order_dir = tuple(st.pop("order", (0.0, 0.0, 0.0)))
     os.environ.update(st)
     world = pkg.World(arr)
+    cnt = torch.zeros(8, dtype=torch.int64, device="cuda")
+    copts = pkg._abi.RtwRenderOpts(spp, 0, cnt.data_ptr())
+    pkg._abi.check(pkg.lib().rtw_render_device(world.handle, C.byref(cam.derived), 0, cam.size, 0, 2, 0,
+                                               acc.data_ptr(), C.c_void_p(stream.cuda_stream), C.byref(copts)), "count")
+    c = cnt.cpu().tolist()
+    st["nodes_per_ray"] = round((c[1] + c[2]) / max(1, c[0]), 2)
+    st["inner_per_ray"] = round(c[1] / max(1, c[0]), 2)
     opts = pkg._abi.RtwRenderOpts(spp, 0, None)
     best = 1e9
     for it in range(3):

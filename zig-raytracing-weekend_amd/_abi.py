@@ -12,13 +12,13 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "librtw_gpu.so")
+LIB_PATH = os.environ.get("RTW_LIB") or os.path.join(_HERE, "librtw_gpu.so")  # RTW_LIB: A/B builds only
 
 RTW_OK, RTW_E_INVALID, RTW_E_HIP, RTW_E_OOM, RTW_E_CANCELLED, RTW_E_NODEVICE = 0, -1, -2, -3, -4, -5
 RTW_MAT_LAMBERTIAN, RTW_MAT_METAL, RTW_MAT_DIELECTRIC, RTW_MAT_DIFFUSE_LIGHT, RTW_MAT_ISOTROPIC = range(5)
 RTW_TEX_SOLID, RTW_TEX_CHECKER, RTW_TEX_IMAGE, RTW_TEX_NOISE = range(4)
 RTW_BG_CONSTANT, RTW_BG_GRADIENT = 0, 1
-RTW_BVH_REFERENCE = 0
+RTW_BVH_REFERENCE, RTW_BVH_SAH = 0, 1
 RTW_RENDER_NO_SYNC = 1
 RTW_STAT_RAYS, RTW_STAT_NODES, RTW_STAT_LEAVES, RTW_STAT_SAMPLES, RTW_STAT_NAN, RTW_STAT_COUNT = 0, 1, 2, 3, 4, 8
 
@@ -47,7 +47,7 @@ class RtwSceneDesc(C.Structure):
                 ("textures", C.c_void_p), ("n_textures", C.c_uint32),
                 ("images", C.c_void_p), ("n_images", C.c_uint32),
                 ("perlins", C.c_void_p), ("n_perlins", C.c_uint32),
-                ("bvh_seed", C.c_uint64), ("bvh_mode", C.c_uint32), ("_pad", C.c_uint32)]
+                ("bvh_seed", C.c_uint64), ("bvh_mode", C.c_uint32), ("order_dir", C.c_float * 3)]
 
 
 F3 = C.c_float * 3

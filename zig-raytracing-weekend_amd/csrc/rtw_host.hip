@@ -51,7 +51,7 @@ struct rtw_ctx {
     uint32_t feat = 0;             // RTW_F_* scene features
     int grid = 0;                  // resident blocks of the persistent kernel
     int variant = 1;               // 1 = persistent v1 (default), 0 = simple v0 (RTW_KERNEL=v0)
-    uint32_t shade_min = 16;       // RTW_SHADE_MIN
+    uint32_t shade_min = 48;       // RTW_SHADE_MIN (tuned on C2: 8..64 -> 48 best)
 };
 
 namespace {
@@ -284,7 +284,9 @@ int rtw_scene_create(const rtw_scene_desc* d, int device, rtw_ctx** out) {
         ctx->shade_min = (uint32_t)(v < 1 ? 1 : (v > 64 ? 64 : v));
     }
     L.shade_min = ctx->shade_min;
-    ctx->grid = rtw_persistent_grid(ctx->feat, n_nodes <= RTW_LDS_NODES, ctx->stream);
+    L.waves = 1;
+    if (const char* wv = std::getenv("RTW_WAVES")) L.waves = (uint32_t)std::atoi(wv);
+    ctx->grid = rtw_persistent_grid(ctx->feat, (uint32_t)n_nodes, (int)L.waves);
 
     ctx->stats.n_nodes = (uint32_t)n_nodes;
     ctx->stats.n_leaves = d->n_spheres;

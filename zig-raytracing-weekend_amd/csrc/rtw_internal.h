@@ -47,6 +47,7 @@ struct rtw_launch {
     uint32_t n_tiles_x, n_tiles;
     uint32_t shade_min;          // lanes that must be ready before a shading pass (<= 64)
     uint32_t feat;               // RTW_F_* scene features (selects the kernel instantiation)
+    uint32_t waves;              // launch-bound variant (min waves per SIMD): 1, 6 or 8
 };
 
 #define RTW_TILE_W 16
@@ -69,7 +70,7 @@ struct rtw_kernel_info {
     int blocks_per_cu;
     int n_cu;
 };
-int rtw_persistent_grid(uint32_t feat, bool lds, void* stream);
+int rtw_persistent_grid(uint32_t feat, uint32_t n_nodes, int waves);
 
 void rtw_launch_render(const rtw_launch& L, void* stream, int variant, int grid);
 void rtw_launch_debug_rng(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t n, float* d_out, void* stream);

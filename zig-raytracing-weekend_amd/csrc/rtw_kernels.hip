@@ -19,6 +19,14 @@
 
 #pragma clang fp contract(off)
 
+#if defined(RTW_ABLATE_MATH)
+// timing ablation only (not IEEE): hardware sqrt / reciprocal
+#define __builtin_sqrtf(x) __builtin_amdgcn_sqrtf(x)
+#define RTW_DIV(a, b) ((a) * __builtin_amdgcn_rcpf(b))
+#else
+#define RTW_DIV(a, b) ((a) / (b))
+#endif
+
 namespace {
 
 constexpr float kPi = 3.1415926535897932385f;  // rtweekend.zig:4
@@ -33,7 +41,7 @@ __device__ __forceinline__ f3 operator-(f3 a, f3 b) { return f3{a.x - b.x, a.y -
 __device__ __forceinline__ f3 operator*(f3 a, f3 b) { return f3{a.x * b.x, a.y * b.y, a.z * b.z}; }
 __device__ __forceinline__ f3 operator-(f3 a) { return f3{-a.x, -a.y, -a.z}; }
 __device__ __forceinline__ f3 splat(float s) { return f3{s, s, s}; }
-__device__ __forceinline__ f3 divs(f3 a, float s) { return f3{a.x / s, a.y / s, a.z / s}; }
+__device__ __forceinline__ f3 divs(f3 a, float s) { return f3{RTW_DIV(a.x, s), RTW_DIV(a.y, s), RTW_DIV(a.z, s)}; }
 __device__ __forceinline__ float dot(f3 u, f3 v) { return u.x * v.x + u.y * v.y + u.z * v.z; }
 __device__ __forceinline__ float length_squared(f3 u) { return u.x * u.x + u.y * u.y + u.z * u.z; }
 __device__ __forceinline__ f3 unit_vector(f3 v) { return divs(v, __builtin_sqrtf(length_squared(v))); }
@@ -238,7 +246,7 @@ struct RayTrav {
 };
 __device__ __forceinline__ RayTrav ray_trav(const Ray& r) {
     RayTrav t;
-    t.inv = mk(1 / r.d.x, 1 / r.d.y, 1 / r.d.z);
+    t.inv = mk(RTW_DIV(1.0f, r.d.x), RTW_DIV(1.0f, r.d.y), RTW_DIV(1.0f, r.d.z));
     t.a = length_squared(r.d);
     return t;
 }
@@ -275,10 +283,10 @@ __device__ __forceinline__ uint32_t trav_step(const float4* __restrict__ nodes, 
         const float disc = half_b * half_b - rt.a * c;
         if (disc >= 0) {
             const float sq = __builtin_sqrtf(disc);
-            float root = (-half_b - sq) / rt.a;
+            float root = RTW_DIV(-half_b - sq, rt.a);
             bool ok = kTmin < root && root < closest;
             if (!ok) {
-                root = (-half_b + sq) / rt.a;
+                root = RTW_DIV(-half_b + sq, rt.a);
                 ok = kTmin < root && root < closest;
             }
             if (ok) {
@@ -485,8 +493,8 @@ enum : uint32_t { ST_TRAV = 0, ST_SHADE = 1, ST_NEWSAMPLE = 2, ST_NEWPIXEL = 3, 
 
 __device__ __forceinline__ uint32_t popc64(uint64_t m) { return (uint32_t)__popcll(m); }
 
-template <uint32_t FEAT, bool LDS>
-__global__ __launch_bounds__(256) void render_persistent_v1(rtw_launch L) {
+template <uint32_t FEAT, bool LDS, int WAVES>
+__global__ __launch_bounds__(256, WAVES) void render_persistent_v1(rtw_launch L) {
     extern __shared__ float4 lds_nodes[];
     const float4* __restrict__ nodes;
     if constexpr (LDS) {
@@ -663,24 +671,39 @@ __global__ void debug_sample_kernel(rtw_launch L, uint32_t pixel, uint32_t sampl
     out[5] = (float)cnt.leaves;
 }
 
-template <uint32_t FEAT, bool LDS>
+template <uint32_t FEAT, bool LDS, int WAVES>
 void launch_v1(const rtw_launch& L, hipStream_t stream, int grid) {
     const size_t lds = LDS ? (size_t)L.n_nodes * 32 : 0;
-    hipLaunchKernelGGL((render_persistent_v1<FEAT, LDS>), dim3(grid), dim3(256), lds, stream, L);
+    hipLaunchKernelGGL((render_persistent_v1<FEAT, LDS, WAVES>), dim3(grid), dim3(256), lds, stream, L);
 }
 
-template <uint32_t FEAT, bool LDS>
-int occupancy_v1() {
+template <uint32_t FEAT, bool LDS, int WAVES>
+int occupancy_v1(size_t lds_bytes) {
     int b = 0;
-    const size_t lds = LDS ? (size_t)RTW_LDS_NODES * 32 : 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, render_persistent_v1<FEAT, LDS>, 256, lds) != hipSuccess)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, render_persistent_v1<FEAT, LDS, WAVES>, 256,
+                                                     LDS ? lds_bytes : 0) != hipSuccess)
         b = 1;
     return b < 1 ? 1 : b;
 }
 
+// waves-per-SIMD launch-bound variants (RTW_WAVES): 1 = compiler's choice, 6, 8
 uint32_t pick_feat(uint32_t f) {
     if ((f & ~RTW_F_CHECKER) == 0) return f ? RTW_F_CHECKER : 0u;
     return RTW_F_ALL;
+}
+
+
+template <uint32_t FEAT, bool LDS>
+void launch_waves(const rtw_launch& L, hipStream_t st, int grid, int waves) {
+    if (waves >= 8) launch_v1<FEAT, LDS, 8>(L, st, grid);
+    else if (waves >= 6) launch_v1<FEAT, LDS, 6>(L, st, grid);
+    else launch_v1<FEAT, LDS, 1>(L, st, grid);
+}
+template <uint32_t FEAT, bool LDS>
+int occ_waves(size_t lds, int waves) {
+    if (waves >= 8) return occupancy_v1<FEAT, LDS, 8>(lds);
+    if (waves >= 6) return occupancy_v1<FEAT, LDS, 6>(lds);
+    return occupancy_v1<FEAT, LDS, 1>(lds);
 }
 
 }  // namespace
@@ -694,30 +717,34 @@ void rtw_launch_render(const rtw_launch& L, void* stream, int variant, int grid)
         return;
     }
     const bool lds = L.n_nodes <= RTW_LDS_NODES;
+    const int w = (int)L.waves;
     switch (pick_feat(L.feat)) {
     case 0u:
-        lds ? launch_v1<0u, true>(L, st, grid) : launch_v1<0u, false>(L, st, grid);
+        lds ? launch_waves<0u, true>(L, st, grid, w) : launch_waves<0u, false>(L, st, grid, w);
         break;
     case RTW_F_CHECKER:
-        lds ? launch_v1<RTW_F_CHECKER, true>(L, st, grid) : launch_v1<RTW_F_CHECKER, false>(L, st, grid);
+        lds ? launch_waves<RTW_F_CHECKER, true>(L, st, grid, w) : launch_waves<RTW_F_CHECKER, false>(L, st, grid, w);
         break;
     default:
-        lds ? launch_v1<RTW_F_ALL, true>(L, st, grid) : launch_v1<RTW_F_ALL, false>(L, st, grid);
+        lds ? launch_waves<RTW_F_ALL, true>(L, st, grid, w) : launch_waves<RTW_F_ALL, false>(L, st, grid, w);
         break;
     }
 }
 
-int rtw_persistent_grid(uint32_t feat, bool lds, void* stream) {
-    (void)stream;
+int rtw_persistent_grid(uint32_t feat, uint32_t n_nodes, int waves) {
     int dev = 0, n_cu = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
     if (n_cu <= 0) n_cu = 256;
+    const bool lds = n_nodes <= RTW_LDS_NODES;
+    const size_t bytes = (size_t)n_nodes * 32;
     int b;
     switch (pick_feat(feat)) {
-    case 0u: b = lds ? occupancy_v1<0u, true>() : occupancy_v1<0u, false>(); break;
-    case RTW_F_CHECKER: b = lds ? occupancy_v1<RTW_F_CHECKER, true>() : occupancy_v1<RTW_F_CHECKER, false>(); break;
-    default: b = lds ? occupancy_v1<RTW_F_ALL, true>() : occupancy_v1<RTW_F_ALL, false>(); break;
+    case 0u: b = lds ? occ_waves<0u, true>(bytes, waves) : occ_waves<0u, false>(bytes, waves); break;
+    case RTW_F_CHECKER:
+        b = lds ? occ_waves<RTW_F_CHECKER, true>(bytes, waves) : occ_waves<RTW_F_CHECKER, false>(bytes, waves);
+        break;
+    default: b = lds ? occ_waves<RTW_F_ALL, true>(bytes, waves) : occ_waves<RTW_F_ALL, false>(bytes, waves); break;
     }
     return n_cu * b;
 }

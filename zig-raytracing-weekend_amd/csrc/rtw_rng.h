@@ -42,7 +42,14 @@ RTW_HD rtw_rng rtw_rng_stream(uint64_t seed, uint64_t domain, uint32_t a, uint32
 
 RTW_HD uint64_t rtw_rng_next(rtw_rng& r) {
     r.s += RTW_GOLDEN;
+#if defined(RTW_ABLATE_RNG) && defined(__HIP_DEVICE_COMPILE__)
+    // timing ablation only (wrong numbers): 32-bit multiply-free hash
+    uint32_t lo = (uint32_t)r.s, hi = (uint32_t)(r.s >> 32);
+    lo ^= lo << 13; lo ^= lo >> 17; lo ^= lo << 5; hi ^= lo; hi ^= hi << 7; hi ^= hi >> 9;
+    return ((uint64_t)hi << 32) | lo;
+#else
     return rtw_mix64(r.s);
+#endif
 }
 
 RTW_HD int rtw_clz64(uint64_t x) {

@@ -208,6 +208,8 @@ class SceneArrays:
     perlins: np.ndarray
     images: List[Image]
     bvh_seed: int = 0
+    bvh_mode: int = _abi.RTW_BVH_SAH   # or _abi.RTW_BVH_REFERENCE (bvh.zig topology, same closest hits)
+    order_dir: tuple = (0.0, 0.0, 0.0)
 
     def desc(self):
         """Build an RtwSceneDesc (keeps the ctypes image array alive on self)."""
@@ -225,11 +227,14 @@ class SceneArrays:
         d.images, d.n_images = (C.addressof(imgs) if self.images else 0), len(self.images)
         d.perlins, d.n_perlins = _abi.ptr(self.perlins), len(self.perlins)
         d.bvh_seed = self.bvh_seed
-        d.bvh_mode = _abi.RTW_BVH_REFERENCE
+        d.bvh_mode = self.bvh_mode
+        d.order_dir[:] = list(self.order_dir)
         return d
 
 
-def flatten(objects: Sequence[Sphere], bvh_seed: int = 0) -> SceneArrays:
+def flatten(objects: Sequence[Sphere], bvh_seed: int = 0, bvh_mode: Optional[int] = None) -> SceneArrays:
+    """Objects -> C-ABI records.  bvh_mode: RTW_BVH_SAH (default, fastest) or
+    RTW_BVH_REFERENCE (the reference's random-axis median tree, seeded by bvh_seed)."""
     sp = np.zeros(len(objects), _abi.SPHERE_DT)
     mats, texs, perlins, images = [], [], [], []
 
@@ -279,7 +284,8 @@ def flatten(objects: Sequence[Sphere], bvh_seed: int = 0) -> SceneArrays:
         pl[i]["ranvec"] = p.ranvec
         pl[i]["perm_x"], pl[i]["perm_y"], pl[i]["perm_z"] = p.perm_x, p.perm_y, p.perm_z
     return SceneArrays(sp, np.array(mats, _abi.MATERIAL_DT).reshape(-1),
-                       np.array(texs, _abi.TEXTURE_DT).reshape(-1), pl, images, bvh_seed)
+                       np.array(texs, _abi.TEXTURE_DT).reshape(-1), pl, images, bvh_seed,
+                       _abi.RTW_BVH_SAH if bvh_mode is None else bvh_mode)
 
 
 def flatten_bvh(arrays: SceneArrays) -> np.ndarray:
@@ -338,6 +344,6 @@ class BVHTree:
 
     @staticmethod
     def init(objects: Sequence[Sphere], start: int = 0, end: Optional[int] = None, seed: int = 0,
-             device: int = 0) -> World:
+             device: int = 0, bvh_mode: Optional[int] = None) -> World:
         end = len(objects) if end is None else end
-        return World(flatten(list(objects[start:end]), bvh_seed=seed), device)
+        return World(flatten(list(objects[start:end]), bvh_seed=seed, bvh_mode=bvh_mode), device)
