@@ -79,41 +79,21 @@ def main():
     W, H, spp = cam.derived.image_width, cam.derived.image_height, cam.samples_per_pixel
     stats = world.stats()
 
-    n_blk = (H + ROWS_PER_BLOCK - 1) // ROWS_PER_BLOCK
-    max_blk = (n_blk + world_size - 1) // world_size
-    tile = torch.zeros((max_blk * ROWS_PER_BLOCK * W, 4), dtype=torch.float32, device="cuda")
-    my_rows = L.rtw_shard_rows(H, ROWS_PER_BLOCK, world_size, rank)
     stream = torch.cuda.Stream()          # explicit stream: the kernels and the timing events share it
     torch.cuda.set_stream(stream)
-    opts = pkg._abi.RtwRenderOpts(spp, pkg._abi.RTW_RENDER_NO_SYNC, None)   # one launch per step
-    gather_list = [torch.empty_like(tile) for _ in range(world_size)] if (distributed and rank == 0) else None
-    image = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda") if rank == 0 else None
-    # image row of every (shard, tile row) -- reassembly index for rank 0
-    src_idx, dst_idx = [], []
-    for s in range(world_size):
-        for r in range(max_blk * ROWS_PER_BLOCK):
-            y = ((r // ROWS_PER_BLOCK) * world_size + s) * ROWS_PER_BLOCK + r % ROWS_PER_BLOCK
-            if y < H:
-                src_idx.append(s * max_blk * ROWS_PER_BLOCK + r)
-                dst_idx.append(y)
-    src_idx = torch.tensor(src_idx, device="cuda")
-    dst_idx = torch.tensor(dst_idx, device="cuda")
+    shard = pkg.distributed.ShardedRender(world, cam, rank, world_size, ROWS_PER_BLOCK)
+    my_rows = shard.rows
+    assert my_rows == L.rtw_shard_rows(H, ROWS_PER_BLOCK, world_size, rank)
 
     def render_step(counters=None, w=None):
-        tile.zero_()
-        o = opts if counters is None else pkg._abi.RtwRenderOpts(spp, pkg._abi.RTW_RENDER_NO_SYNC, counters)
-        rc = L.rtw_render_rows_device((w or world).handle, C.byref(cam.derived), ROWS_PER_BLOCK, world_size, rank, 0,
-                                      spp, 0, tile.data_ptr(), C.c_void_p(stream.cuda_stream), C.byref(o))
-        pkg._abi.check(rc, "rtw_render_rows_device")
+        if w is not None:
+            saved, shard.world = shard.world, w
+        shard.render(0, spp, seed=0, stream=stream, counters=counters)
+        if w is not None:
+            shard.world = saved
 
     def gather_step():
-        if distributed:
-            dist.gather(tile, gather_list=gather_list, dst=0)
-            if rank == 0:
-                allt = torch.stack(gather_list).view(-1, W, 4)
-                image.index_copy_(0, dst_idx, allt.index_select(0, src_idx))
-        else:
-            image.view(-1, W, 4).index_copy_(0, dst_idx, tile.view(-1, W, 4).index_select(0, src_idx))
+        shard.gather()
 
     # ---- algorithmic bytes of one step: counted pass on the reference topology (the device
     # walk of a reference-topology tree visits exactly the nodes bvh.zig's recursion visits)

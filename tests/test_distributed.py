@@ -1,0 +1,77 @@
+"""Multi-GPU path on CPU: row sharding covers the image exactly once, and the
+gather + reassembly of bench.py/distributed.py rebuilds the image over a real
+world_size-2 gloo process group (synthetic tiles stand in for the GPU render)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from conftest import load_pkg
+
+
+def test_shard_rows_match_library(rtw):
+    L = rtw.lib()
+    d = rtw.distributed
+    for H in (1, 15, 16, 17, 800, 2160):
+        for rpb in (1, 8, 16):
+            for n in (1, 2, 3, 4, 8):
+                allrows = []
+                for s in range(n):
+                    rows = d.shard_rows(H, rpb, n, s)
+                    assert len(rows) == L.rtw_shard_rows(H, rpb, n, s)
+                    assert len(rows) <= d.tile_rows_capacity(H, rpb, n)
+                    allrows += rows
+                assert sorted(allrows) == list(range(H))
+                src, dst = d.reassembly_index(H, rpb, n)
+                assert sorted(dst) == list(range(H))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world_size, port, H, W, rpb, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world_size)
+    pkg = load_pkg()
+    d = pkg.distributed
+    cap = d.tile_rows_capacity(H, rpb, world_size)
+    rows = d.shard_rows(H, rpb, world_size, rank)
+    tile = torch.zeros((cap * W, 4), dtype=torch.float32)
+    t = tile.view(cap, W, 4)
+    for r, y in enumerate(rows):          # "render": pixel value encodes (y, x)
+        t[r, :, 0] = y
+        t[r, :, 1] = torch.arange(W, dtype=torch.float32)
+        t[r, :, 3] = 7
+    src, dst = d.reassembly_index(H, rpb, world_size)
+    image = torch.zeros((H, W, 4)) if rank == 0 else None
+    glist = [torch.empty_like(tile) for _ in range(world_size)] if rank == 0 else None
+    d.gather_tiles(tile, image, glist, torch.tensor(src), torch.tensor(dst), W, world_size, rank)
+    if rank == 0:
+        q.put(image.numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world_size,H,rpb", [(2, 45, 16), (2, 37, 8), (3, 20, 4)])
+def test_gather_reassembles_image_gloo(world_size, H, rpb):
+    W = 11
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world_size, port, H, W, rpb, q)) for r in range(world_size)]
+    for p in procs:
+        p.start()
+    img = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert np.array_equal(img[:, :, 0], np.repeat(np.arange(H, dtype=np.float32)[:, None], W, 1))
+    assert np.array_equal(img[:, :, 1], np.repeat(np.arange(W, dtype=np.float32)[None, :], H, 0))
+    assert (img[:, :, 3] == 7).all()

@@ -285,6 +285,8 @@ int rtw_scene_create(const rtw_scene_desc* d, int device, rtw_ctx** out) {
     }
     L.shade_min = ctx->shade_min;
     L.waves = 1;
+    L.tile_order = 1;
+    if (const char* to = std::getenv("RTW_TILE_ORDER")) L.tile_order = (uint32_t)std::atoi(to);
     if (const char* wv = std::getenv("RTW_WAVES")) L.waves = (uint32_t)std::atoi(wv);
     ctx->grid = rtw_persistent_grid(ctx->feat, (uint32_t)n_nodes, (int)L.waves);
 

@@ -48,6 +48,7 @@ struct rtw_launch {
     uint32_t shade_min;          // lanes that must be ready before a shading pass (<= 64)
     uint32_t feat;               // RTW_F_* scene features (selects the kernel instantiation)
     uint32_t waves;              // launch-bound variant (min waves per SIMD): 1, 6 or 8
+    uint32_t tile_order;         // 1 = last tile row first (default), 0 = first row first
 };
 
 #define RTW_TILE_W 16

@@ -491,6 +491,18 @@ __global__ __launch_bounds__(256) void render_pixels_v0(rtw_launch L) {
 // ---------------------------------------------------------------------------
 enum : uint32_t { ST_TRAV = 0, ST_SHADE = 1, ST_NEWSAMPLE = 2, ST_NEWPIXEL = 3, ST_DONE = 4 };
 
+#if defined(RTW_STAMPS)
+// diagnostic build only: per-wave cycle split of the persistent loop
+#define STAMP(var)                                  \
+    __builtin_amdgcn_sched_barrier(0);              \
+    var = __builtin_amdgcn_s_memtime();             \
+    __builtin_amdgcn_sched_barrier(0);
+#define STAMP_ADD(acc, t0, t1) acc += (t1) - (t0);
+#else
+#define STAMP(var)
+#define STAMP_ADD(acc, t0, t1)
+#endif
+
 __device__ __forceinline__ uint32_t popc64(uint64_t m) { return (uint32_t)__popcll(m); }
 
 template <uint32_t FEAT, bool LDS, int WAVES>
@@ -529,8 +541,12 @@ __global__ __launch_bounds__(256, WAVES) void render_persistent_v1(rtw_launch L)
     int hit = -1;
     Counters cnt;
     uint32_t samples_done = 0;
+#if defined(RTW_STAMPS)
+    uint64_t c_assign = 0, c_gen = 0, c_trav = 0, c_shade = 0, c_steps = 0, c_passes = 0, t0, t1;
+#endif
 
     for (;;) {
+        STAMP(t0)
         // ---- 1. hand pixels to lanes that need one
         uint64_t need = __ballot(st == ST_NEWPIXEL);
         while (need) {
@@ -546,6 +562,11 @@ __global__ __launch_bounds__(256, WAVES) void render_persistent_v1(rtw_launch L)
                     q_empty = true;
                     continue;
                 }
+                // tiles are handed out last-row-first: the bottom of a frame (ground,
+                // many bounces) is the expensive part, the top (sky) the cheap one, so
+                // the end-of-launch tail is made of cheap pixels (order never changes
+                // arithmetic: a pixel is always one lane's, samples in order)
+                if (L.tile_order) t = L.n_tiles - 1 - t;
                 q_cur = t * RTW_TILE;
                 q_end = q_cur + RTW_TILE;
             }
@@ -577,6 +598,7 @@ __global__ __launch_bounds__(256, WAVES) void render_persistent_v1(rtw_launch L)
         }
         const uint64_t live = __ballot(st != ST_DONE);
         if (!live) break;
+        STAMP(t1) STAMP_ADD(c_assign, t0, t1)
 
         // ---- 2. start a new sample: getRay (camera.zig:169-180)
         if (st == ST_NEWSAMPLE) {
@@ -598,6 +620,7 @@ __global__ __launch_bounds__(256, WAVES) void render_persistent_v1(rtw_launch L)
             }
         }
 
+        STAMP(t0) STAMP_ADD(c_gen, t1, t0)
         // ---- 3. traversal until enough lanes are ready to shade
         {
             const uint32_t n_live = popc64(live);
@@ -610,8 +633,15 @@ __global__ __launch_bounds__(256, WAVES) void render_persistent_v1(rtw_launch L)
                     ti = trav_step<FEAT>(nodes, L, ray, rt, ti, closest, hit, cnt);
                     if (ti >= n_nodes) st = ST_SHADE;
                 }
+#if defined(RTW_STAMPS)
+                c_steps++;
+#endif
             }
         }
+        STAMP(t1) STAMP_ADD(c_trav, t0, t1)
+#if defined(RTW_STAMPS)
+        c_passes++;
+#endif
 
         // ---- 4. shade lanes whose walk is complete
         if (st == ST_SHADE) {
@@ -647,8 +677,19 @@ __global__ __launch_bounds__(256, WAVES) void render_persistent_v1(rtw_launch L)
                 }
             }
         }
+        STAMP(t0) STAMP_ADD(c_shade, t1, t0)
     }
     flush_counters(L, cnt, samples_done);
+#if defined(RTW_STAMPS)
+    if (L.counters && lane == 0) {
+        atomicAdd(&L.counters[8], (unsigned long long)c_assign);
+        atomicAdd(&L.counters[9], (unsigned long long)c_gen);
+        atomicAdd(&L.counters[10], (unsigned long long)c_trav);
+        atomicAdd(&L.counters[11], (unsigned long long)c_shade);
+        atomicAdd(&L.counters[12], (unsigned long long)c_steps);
+        atomicAdd(&L.counters[13], (unsigned long long)c_passes);
+    }
+#endif
 }
 
 __global__ void debug_rng_kernel(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t n, float* out) {

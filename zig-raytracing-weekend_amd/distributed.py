@@ -1,0 +1,101 @@
+"""Multi-GPU image sharding (one process per GPU, torch.distributed over RCCL).
+
+The reference splits one image over 8 CPU threads in contiguous chunks
+(src/main.zig:314-326), which is load-imbalanced (sky rows are cheap, ground
+rows expensive).  Here rank r of N renders the row blocks b (of
+``rows_per_block`` rows) with b % N == r -- interleaved, so every rank gets
+the same mix of sky and ground -- into a compact float4 tile, and the tiles
+meet on rank 0 in ONE gather (the only data-path collective: there is no other
+exchange in the algorithm).  The counter-based RNG keys every sample by
+(seed, pixel, sample), so the gathered image is bit-identical to a 1-GPU
+render for any N.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import List, Optional, Tuple
+
+from . import _abi
+
+
+def shard_rows(height: int, rows_per_block: int, n_shards: int, shard: int) -> List[int]:
+    """Image rows owned by `shard`, in tile order (rtw_shard_rows / map_row)."""
+    rows = []
+    n_blk = (height + rows_per_block - 1) // rows_per_block
+    for b in range(shard, n_blk, n_shards):
+        for k in range(rows_per_block):
+            y = b * rows_per_block + k
+            if y < height:
+                rows.append(y)
+    return rows
+
+
+def tile_rows_capacity(height: int, rows_per_block: int, n_shards: int) -> int:
+    """Rows of the (padded) per-rank tile: equal on every rank so the gather is uniform."""
+    n_blk = (height + rows_per_block - 1) // rows_per_block
+    return ((n_blk + n_shards - 1) // n_shards) * rows_per_block
+
+
+def reassembly_index(height: int, rows_per_block: int, n_shards: int) -> Tuple[List[int], List[int]]:
+    """(src, dst): row src of the stacked [n_shards * cap] tile buffer -> image row dst."""
+    cap = tile_rows_capacity(height, rows_per_block, n_shards)
+    src, dst = [], []
+    for s in range(n_shards):
+        for r in range(cap):
+            y = ((r // rows_per_block) * n_shards + s) * rows_per_block + r % rows_per_block
+            if y < height:
+                src.append(s * cap + r)
+                dst.append(y)
+    return src, dst
+
+
+class ShardedRender:
+    """Per-rank state of a row-interleaved render + gather (used by bench.py)."""
+
+    def __init__(self, world, cam, rank: int, world_size: int, rows_per_block: int = 16, device=None):
+        import torch
+
+        self.world, self.cam = world, cam
+        self.rank, self.world_size, self.rpb = rank, world_size, rows_per_block
+        self.W, self.H = cam.derived.image_width, cam.derived.image_height
+        self.cap = tile_rows_capacity(self.H, rows_per_block, world_size)
+        dev = device or torch.device("cuda", torch.cuda.current_device())
+        self.tile = torch.zeros((self.cap * self.W, 4), dtype=torch.float32, device=dev)
+        src, dst = reassembly_index(self.H, rows_per_block, world_size)
+        self.src = torch.tensor(src, device=dev)
+        self.dst = torch.tensor(dst, device=dev)
+        self.gather_list = ([torch.empty_like(self.tile) for _ in range(world_size)]
+                            if (world_size > 1 and rank == 0) else None)
+        self.image = torch.zeros((self.H, self.W, 4), dtype=torch.float32, device=dev) if rank == 0 else None
+        self.rows = len(shard_rows(self.H, rows_per_block, world_size, rank))
+
+    def render(self, spp_begin: int, spp_end: int, seed: int = 0, stream=None, spp_batch: int = 0,
+               counters: Optional[int] = None, sync: bool = False) -> None:
+        """Enqueue this rank's rows x samples [spp_begin, spp_end) on `stream`."""
+        self.tile.zero_()
+        flags = 0 if sync else _abi.RTW_RENDER_NO_SYNC
+        opts = _abi.RtwRenderOpts(spp_batch or (spp_end - spp_begin), flags, counters)
+        rc = _abi.lib().rtw_render_rows_device(self.world.handle, C.byref(self.cam.derived), self.rpb,
+                                               self.world_size, self.rank, spp_begin, spp_end, seed,
+                                               self.tile.data_ptr(),
+                                               C.c_void_p(stream.cuda_stream if stream is not None else 0),
+                                               C.byref(opts))
+        _abi.check(rc, "rtw_render_rows_device")
+
+    def gather(self) -> None:
+        """Tiles -> rank 0 (one RCCL gather), then scatter rows into the image."""
+        gather_tiles(self.tile, self.image, self.gather_list, self.src, self.dst, self.W, self.world_size,
+                     self.rank)
+
+
+def gather_tiles(tile, image, gather_list, src, dst, W: int, world_size: int, rank: int) -> None:
+    import torch
+    import torch.distributed as dist
+
+    if world_size > 1:
+        dist.gather(tile, gather_list=gather_list, dst=0)
+        if rank == 0:
+            allt = torch.stack(gather_list).view(-1, W, 4)
+            image.index_copy_(0, dst, allt.index_select(0, src))
+    else:
+        image.index_copy_(0, dst, tile.view(-1, W, 4).index_select(0, src))
