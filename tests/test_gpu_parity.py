@@ -294,14 +294,33 @@ def test_persistent_v1_bit_identical_to_v0(rtw, earth_rgba, scene, monkeypatch):
     assert np.array_equal(outs["v0"], outs["v1"])
 
 
-@pytest.mark.parametrize("shade_min", ["1", "64"])
-def test_v1_shade_threshold_invariant(rtw, book1, shade_min, monkeypatch):
-    """The ballot threshold only reorders work between lanes, never arithmetic."""
+@pytest.mark.parametrize("knob", [("RTW_SHADE_MIN", "1"), ("RTW_SHADE_MIN", "64"), ("RTW_COOP", "0"),
+                                  ("RTW_TILE_ORDER", "0"), ("RTW_WAVES", "8")])
+def test_v1_knobs_invariant(rtw, book1, knob, monkeypatch):
+    """Scheduling knobs (ballot threshold, cooperative vs per-lane rejection
+    sampling, tile order, launch bounds) only move work between lanes: outputs
+    are bit-identical."""
     arr, world = book1
     cam = rtw.book1_camera(image_width=300, aspect_ratio=1.5, spp=3).init()
     ref = render_rows(rtw, world, cam, 0, 200, 0, 3, 4)
-    monkeypatch.setenv("RTW_SHADE_MIN", shade_min)
+    monkeypatch.setenv(*knob)
     w2 = rtw.World(arr)
     got = render_rows(rtw, w2, cam, 0, 200, 0, 3, 4)
     w2.close()
     assert np.array_equal(ref, got)
+
+
+@pytest.mark.parametrize("scene", ["book1", "stress"])
+def test_fast_reject_is_exact(rtw, scene, monkeypatch):
+    """The sphere fast-reject (hardware sqrt/rcp estimate + error margin) never
+    changes a result: bit-identical to the always-IEEE path."""
+    objs = rtw.worlds.generate_world(0, "book1") if scene == "book1" else rtw.worlds.stress_world(20000, 3)
+    arr = rtw.flatten(objs)
+    cam = rtw.book1_camera(image_width=600, aspect_ratio=1.5, spp=4).init()
+    outs = []
+    for fr in ("0", "1"):
+        monkeypatch.setenv("RTW_FAST_REJECT", fr)
+        w = rtw.World(arr)
+        outs.append(render_rows(rtw, w, cam, 0, cam.derived.image_height, 0, 4, 5))
+        w.close()
+    assert np.array_equal(outs[0], outs[1])

@@ -36,23 +36,7 @@ int hip_fail(hipError_t e, const char* where) {
 
 }  // namespace
 
-struct rtw_ctx {
-    int device = 0;
-    hipStream_t stream = nullptr;
-    void* d_blob = nullptr;       // single allocation holding every scene array
-    size_t blob_bytes = 0;
-    rtw_launch base{};
-    rtw_scene_stats stats{};
-    std::vector<rtw_node> nodes_host;
-    float* d_scratch = nullptr;    // host-API accum staging
-    size_t scratch_bytes = 0;
-    float* d_dbg = nullptr;        // debug kernels output
-    uint32_t* d_work = nullptr;    // persistent-kernel work counter (zeroed before each launch)
-    uint32_t feat = 0;             // RTW_F_* scene features
-    int grid = 0;                  // resident blocks of the persistent kernel
-    int variant = 1;               // 1 = persistent v1 (default), 0 = simple v0 (RTW_KERNEL=v0)
-    uint32_t shade_min = 48;       // RTW_SHADE_MIN (tuned on C2: 8..64 -> 48 best)
-};
+// struct rtw_ctx: see rtw_internal.h
 
 namespace {
 uint32_t scene_features(const rtw_scene_desc* d) {
@@ -286,9 +270,15 @@ int rtw_scene_create(const rtw_scene_desc* d, int device, rtw_ctx** out) {
     L.shade_min = ctx->shade_min;
     L.waves = 1;
     L.tile_order = 1;
+    L.fast_reject = 1;
+    L.coop = 0;   // wave-cooperative rejection sampling: exact but no gain measured on C2
+    if (const char* cp = std::getenv("RTW_COOP")) L.coop = (uint32_t)std::atoi(cp);
+    if (const char* fr = std::getenv("RTW_FAST_REJECT")) L.fast_reject = (uint32_t)std::atoi(fr);
     if (const char* to = std::getenv("RTW_TILE_ORDER")) L.tile_order = (uint32_t)std::atoi(to);
     if (const char* wv = std::getenv("RTW_WAVES")) L.waves = (uint32_t)std::atoi(wv);
-    ctx->grid = rtw_persistent_grid(ctx->feat, (uint32_t)n_nodes, (int)L.waves);
+    L.use_lds = 1;
+    if (const char* ul = std::getenv("RTW_LDS")) L.use_lds = (uint32_t)std::atoi(ul);
+    ctx->grid = rtw_persistent_grid(ctx->feat, (uint32_t)n_nodes, (int)L.waves, L.use_lds != 0);
 
     ctx->stats.n_nodes = (uint32_t)n_nodes;
     ctx->stats.n_leaves = d->n_spheres;
@@ -554,8 +544,19 @@ int rtw_debug_sample(rtw_ctx* ctx, const rtw_camera* cam, uint64_t seed, uint32_
     rtw_launch L = make_launch(ctx, cam, seed);
     rtw_launch_debug_sample(L, pixel, sample, ctx->d_dbg, ctx->stream);
     HIP_TRY(hipGetLastError());
-    float tmp[6];
+    float tmp[32];
     HIP_TRY(hipMemcpyAsync(tmp, ctx->d_dbg, sizeof tmp, hipMemcpyDeviceToHost, ctx->stream));
+    if (const char* dbg = std::getenv("RTW_DEBUG_FILTER")) {
+        (void)dbg;
+        if (tmp[8] != 0)
+            std::fprintf(stderr, "filter miss: node %g hb %.9g c %.9g disc %.9g sq %.9g sa %.9g a %.9g rcp %.9g r1 %.9g r2 %.9g q1 %.9g q2 %.9g e %.9g\n",
+                         tmp[9], tmp[10], tmp[11], tmp[12], tmp[13], tmp[14], tmp[15], tmp[16], tmp[17], tmp[18], tmp[19], tmp[20], tmp[21]);
+        else
+            std::fprintf(stderr, "filter ok\n");
+        if (tmp[22] != 0)
+            std::fprintf(stderr, "closest mismatch at bounce %g: trav hit %g t %.9g brute hit %g t %.9g origin %.9g %.9g %.9g\n",
+                         tmp[23], tmp[24], tmp[25], tmp[26], tmp[27], tmp[28], tmp[29], tmp[30]);
+    }
     HIP_TRY(hipStreamSynchronize(ctx->stream));
     out[0] = tmp[0];
     out[1] = tmp[1];

@@ -7,6 +7,7 @@
 #include <vector>
 
 #include "rtw_layout.h"
+#include "../../include/rtw_gpu.h"
 
 struct rtw_scene_desc;
 
@@ -49,6 +50,9 @@ struct rtw_launch {
     uint32_t feat;               // RTW_F_* scene features (selects the kernel instantiation)
     uint32_t waves;              // launch-bound variant (min waves per SIMD): 1, 6 or 8
     uint32_t tile_order;         // 1 = last tile row first (default), 0 = first row first
+    uint32_t use_lds;            // 1 = stage the BVH in LDS when it fits (default), 0 = read nodes from L1/L2
+    uint32_t coop;               // 1 = wave-cooperative rejection sampling (default), 0 = per-lane loops
+    uint32_t fast_reject;        // 1 = exact sphere fast-reject filter (default), 0 = always the IEEE path
 };
 
 #define RTW_TILE_W 16
@@ -71,7 +75,7 @@ struct rtw_kernel_info {
     int blocks_per_cu;
     int n_cu;
 };
-int rtw_persistent_grid(uint32_t feat, uint32_t n_nodes, int waves);
+int rtw_persistent_grid(uint32_t feat, uint32_t n_nodes, int waves, bool use_lds);
 
 void rtw_launch_render(const rtw_launch& L, void* stream, int variant, int grid);
 void rtw_launch_debug_rng(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t n, float* d_out, void* stream);
@@ -79,3 +83,22 @@ void rtw_launch_debug_sample(const rtw_launch& L, uint32_t pixel, uint32_t sampl
 
 int rtw_build_bvh(const rtw_scene_desc& desc, std::vector<rtw_node>& nodes, std::vector<float>& cvec,
                   uint32_t* depth, uint32_t* axis_draws);
+
+// One scene on one device (the opaque rtw_ctx of include/rtw_gpu.h).
+struct rtw_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    void* d_blob = nullptr;        // single allocation holding every scene array
+    size_t blob_bytes = 0;
+    rtw_launch base{};
+    rtw_scene_stats stats{};
+    std::vector<rtw_node> nodes_host;
+    float* d_scratch = nullptr;    // host-API accum staging
+    size_t scratch_bytes = 0;
+    float* d_dbg = nullptr;        // debug kernels output
+    uint32_t* d_work = nullptr;    // persistent-kernel work counter (zeroed before each launch)
+    uint32_t feat = 0;             // RTW_F_* scene features
+    int grid = 0;                  // resident blocks of the persistent kernel
+    int variant = 1;               // 1 = persistent v1 (default), 0 = simple v0 (RTW_KERNEL=v0)
+    uint32_t shade_min = 48;       // RTW_SHADE_MIN (tuned on C2: 8..64 -> 48 best)
+};

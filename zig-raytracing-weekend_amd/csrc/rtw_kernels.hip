@@ -19,6 +19,10 @@
 
 #pragma clang fp contract(off)
 
+#ifndef RTW_STEPS
+#define RTW_STEPS 1
+#endif
+
 #if defined(RTW_ABLATE_MATH)
 // timing ablation only (not IEEE): hardware sqrt / reciprocal
 #define __builtin_sqrtf(x) __builtin_amdgcn_sqrtf(x)
@@ -63,6 +67,12 @@ __device__ __forceinline__ uint32_t fbits(float f) { return __float_as_uint(f); 
 // ---- RNG helpers (rtweekend.zig / vec3.zig samplers) ----
 __device__ __forceinline__ float rnd(rtw_rng& r) { return rtw_rng_float(r); }
 __device__ __forceinline__ f3 random_unit_vector(rtw_rng& r) {  // vec3.zig:59-68
+#if defined(RTW_ABLATE_REJECT)
+    {   // timing ablation only: one candidate, no rejection loop (wrong distribution)
+        float x = rtw_rng_range(r, -1, 1), y = rtw_rng_range(r, -1, 1), z = rtw_rng_range(r, -1, 1);
+        return unit_vector(mk(x, y, z + 1e-3f));
+    }
+#endif
     for (;;) {
         float x = rtw_rng_range(r, -1, 1);
         float y = rtw_rng_range(r, -1, 1);
@@ -243,11 +253,14 @@ struct Counters {
 struct RayTrav {
     f3 inv;      // 1 / d per axis (aabb.zig:87)
     float a;     // lengthSquared(d) (objects.zig:124)
+    float rcp_a; // hardware 1/a estimate for the sphere fast-reject (0 disables it)
 };
 __device__ __forceinline__ RayTrav ray_trav(const Ray& r) {
     RayTrav t;
     t.inv = mk(RTW_DIV(1.0f, r.d.x), RTW_DIV(1.0f, r.d.y), RTW_DIV(1.0f, r.d.z));
     t.a = length_squared(r.d);
+    // fast-reject only where every intermediate below stays normal and finite
+    t.rcp_a = (t.a > 1e-30f && t.a < 1e30f) ? __builtin_amdgcn_rcpf(t.a) : 0.0f;
     return t;
 }
 
@@ -281,7 +294,28 @@ __device__ __forceinline__ uint32_t trav_step(const float4* __restrict__ nodes, 
         const float half_b = dot(oc, r.d);
         const float c = length_squared(oc) - B.x * B.x;
         const float disc = half_b * half_b - rt.a * c;
-        if (disc >= 0) {
+        bool exact = disc >= 0;
+#if !defined(RTW_ABLATE_MATH)
+        // Exact fast-reject: with hardware sqrt/rcp estimates (<= 1 ulp each) the
+        // candidate roots q1, q2 are within (|hb| + sq) / a * 6e-7 of the correctly
+        // rounded roots of objects.zig:130-136.  If neither can lie in
+        // (tmin, closest) even with a 2^-18 relative margin, the exact test
+        // would reject both: skip the IEEE sqrt and divisions.  Guards keep every
+        // intermediate finite and normal; otherwise the exact path runs.
+        // Written as ONE predicate (no nested branch): a nested-branch form was
+        // miscompiled by hipcc 7.2 (numerator left undefined on the guard-false edge).
+        {
+            const float sa = __builtin_amdgcn_sqrtf(disc);
+            const float e = (__builtin_fabsf(half_b) + sa) * rt.rcp_a * 3.8146973e-06f;
+            const float q1 = (-half_b - sa) * rt.rcp_a;
+            const float q2 = (-half_b + sa) * rt.rcp_a;
+            const bool guard = L.fast_reject && rt.rcp_a != 0.0f && disc > 1e-30f && disc < 1e30f &&
+                               __builtin_fabsf(half_b) < 1e15f;
+            const bool plausible = (q1 + e > kTmin && q1 - e < closest) || (q2 + e > kTmin && q2 - e < closest);
+            exact = exact && (plausible || !guard);
+        }
+#endif
+        if (exact) {
             const float sq = __builtin_sqrtf(disc);
             float root = RTW_DIV(-half_b - sq, rt.a);
             bool ok = kTmin < root && root < closest;
@@ -331,12 +365,16 @@ __device__ __forceinline__ f3 background(const rtw_launch& L, const Ray& r) {
     return ld3(L.background);  // camera.zig:207
 }
 
-// Hit record for the closest hit + Material.emitted/scatter
-// (objects.zig:139-145, material.zig:18-144).  Adds thr*emission to acc and
-// returns true with (att, sc) when the ray scatters.
+// Hit record for the closest hit (objects.zig:139-145) + the material.
+struct HitPrep {
+    f3 p, outward, normal;
+    bool front;
+    rtw_dev_material m;
+};
+
 template <uint32_t FEAT>
-__device__ __forceinline__ bool shade(const float4* __restrict__ nodes, const rtw_launch& L, const Ray& r, int hit,
-                                      float t, rtw_rng& rng, f3 thr, f3& acc, f3& att, Ray& sc) {
+__device__ __forceinline__ HitPrep hit_prep(const float4* __restrict__ nodes, const rtw_launch& L, const Ray& r,
+                                            int hit, float t) {
     const float4 A = nodes[2 * hit];
     const float4 B = nodes[2 * hit + 1];
     f3 center = mk(A.x, A.y, A.z);
@@ -346,39 +384,59 @@ __device__ __forceinline__ bool shade(const float4* __restrict__ nodes, const rt
             center = center + splat(r.time) * mk(cv.x, cv.y, cv.z);
         }
     }
-    const f3 p = r.o + splat(t) * r.d;
-    const f3 outward = divs(p - center, B.x);
-    const bool front = dot(r.d, outward) < 0;
-    const f3 normal = front ? outward : -outward;
-    const rtw_dev_material m = L.mats[fbits(B.y)];
-    sc.o = p;
+    HitPrep h;
+    h.p = r.o + splat(t) * r.d;
+    h.outward = divs(h.p - center, B.x);
+    h.front = dot(r.d, h.outward) < 0;
+    h.normal = h.front ? h.outward : -h.outward;
+    h.m = L.mats[fbits(B.y)];
+    return h;
+}
+
+// Does Material.scatter start by drawing vec3.randomUnitVector?
+// (Lambertian material.zig:44, Metal :67, Isotropic :140)
+template <uint32_t FEAT>
+__device__ __forceinline__ bool needs_unit_vector(uint32_t kind) {
+    if (kind == RTW_MAT_LAMBERTIAN || kind == RTW_MAT_METAL) return true;
+    if constexpr ((FEAT & RTW_F_LIGHT) != 0) return kind == RTW_MAT_ISOTROPIC;
+    return false;
+}
+
+// Material.emitted/scatter (material.zig:18-144) given the hit and, for the
+// materials that draw one, the random unit vector `ruv` (already drawn from rng).
+// Adds thr*emission to acc; returns true with (att, sc) when the ray scatters.
+template <uint32_t FEAT>
+__device__ __forceinline__ bool scatter_finish(const rtw_launch& L, const Ray& r, const HitPrep& h, f3 ruv,
+                                               rtw_rng& rng, f3 thr, f3& acc, f3& att, Ray& sc) {
+    const rtw_dev_material& m = h.m;
+    sc.o = h.p;
     sc.time = r.time;
     switch (m.kind) {
     case RTW_MAT_LAMBERTIAN: {  // material.zig:43-54
-        f3 dir = normal + random_unit_vector(rng);
-        if (near_zero(dir)) dir = normal;
+        f3 dir = h.normal + ruv;
+        if (near_zero(dir)) dir = h.normal;
         sc.d = dir;
-        att = texture_value<FEAT>(L, m.texture, outward, p);
+        att = texture_value<FEAT>(L, m.texture, h.outward, h.p);
         return true;
     }
     case RTW_MAT_METAL: {  // material.zig:65-70
-        f3 refl = reflect(unit_vector(r.d), normal);
-        sc.d = refl + splat(m.fuzz) * random_unit_vector(rng);
+        f3 refl = reflect(unit_vector(r.d), h.normal);
+        sc.d = refl + splat(m.fuzz) * ruv;
         att = ld3(m.albedo);
-        return dot(sc.d, normal) > 0;
+        return dot(sc.d, h.normal) > 0;
     }
     case RTW_MAT_DIELECTRIC: {  // material.zig:80-98
         att = mk(1, 1, 1);
-        const float ratio = front ? (1.0f / m.ir) : m.ir;
+        const float ratio = h.front ? (1.0f / m.ir) : m.ir;
         const f3 ud = unit_vector(r.d);
-        const float dd = dot(-ud, normal);
+        const float dd = dot(-ud, h.normal);
         const float cos_theta = dd < 1.0f ? dd : 1.0f;
         const float sin_theta = __builtin_sqrtf(1.0f - cos_theta * cos_theta);
         const bool cannot = ratio * sin_theta > 1.0f;
         if (cannot || reflectance(cos_theta, ratio) > rnd(rng))
-            sc.d = reflect(ud, normal);
+            sc.d = reflect(ud, h.normal);
         else
-            sc.d = refract(ud, normal, ratio);
+            sc.d = refract(ud, h.normal, ratio);
         return true;
     }
     default:
@@ -386,15 +444,136 @@ __device__ __forceinline__ bool shade(const float4* __restrict__ nodes, const rt
     }
     if constexpr ((FEAT & RTW_F_LIGHT) != 0) {
         if (m.kind == RTW_MAT_DIFFUSE_LIGHT) {  // material.zig:119-125
-            acc = acc + thr * texture_value<FEAT>(L, m.texture, outward, p);
+            acc = acc + thr * texture_value<FEAT>(L, m.texture, h.outward, h.p);
             return false;
         }
         // RTW_MAT_ISOTROPIC (material.zig:139-143)
-        sc.d = random_unit_vector(rng);
-        att = texture_value<FEAT>(L, m.texture, outward, p);
+        sc.d = ruv;
+        att = texture_value<FEAT>(L, m.texture, h.outward, h.p);
         return true;
     }
     return false;
+}
+
+// Sequential form (one lane at a time): used by v0 and the debug kernel.
+template <uint32_t FEAT>
+__device__ __forceinline__ bool shade(const float4* __restrict__ nodes, const rtw_launch& L, const Ray& r, int hit,
+                                      float t, rtw_rng& rng, f3 thr, f3& acc, f3& att, Ray& sc) {
+    const HitPrep h = hit_prep<FEAT>(nodes, L, r, hit, t);
+    f3 ruv = mk(0, 0, 0);
+    if (needs_unit_vector<FEAT>(h.m.kind)) ruv = random_unit_vector(rng);
+    return scatter_finish<FEAT>(L, r, h, ruv, rng, thr, acc, att, sc);
+}
+
+// ---------------------------------------------------------------------------
+// Wave-cooperative rejection sampling (vec3.randomInUnitSphere D=3 /
+// randomInUnitDisk D=2, vec3.zig:40-45, 59-64).  The sequential loop runs until
+// the slowest lane of the wave accepts (E[max] ~ 6 iterations for 48 lanes at
+// p = 0.52).  The RNG is counter-based, so candidate j of a lane is simply draws
+// j*D+1 .. j*D+D after its current state: every round, all 64 lanes evaluate
+// candidates of the still-unresolved lanes (64/n helpers each, consecutive j),
+// and each lane takes its FIRST accepted candidate -- exactly the sequential
+// result and stream position.  A draw on Zig's rare extra-draw path
+// (clz >= 41, p = 2^-41) would shift positions: such a lane falls back to the
+// sequential loop from its start.  Must be called with every lane of the wave
+// converged (helpers are idle lanes).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float float_from_draw(uint64_t x, int lz) {
+    const uint32_t bits = ((uint32_t)(126 - lz) << 23) | (uint32_t)(x & 0x7FFFFFu);
+    return __uint_as_float(bits);
+}
+
+template <int D>
+__device__ __forceinline__ void seq_reject(rtw_rng& rng, float (&out)[D]) {
+    for (;;) {
+        float w[D];
+        float ls;
+#pragma unroll
+        for (int d = 0; d < D; d++) w[d] = rtw_rng_range(rng, -1, 1);
+        if constexpr (D == 3) ls = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
+        else ls = w[0] * w[0] + w[1] * w[1];
+        if (ls < 1.0f) {
+#pragma unroll
+            for (int d = 0; d < D; d++) out[d] = w[d];
+            return;
+        }
+    }
+}
+
+template <int D>
+__device__ __forceinline__ void coop_reject(bool active, rtw_rng& rng, float (&out)[D], uint32_t* slot,
+                                            bool coop = true) {
+    if (!coop) {  // A/B knob (RTW_COOP=0): plain per-lane loop, same results
+        if (active) seq_reject<D>(rng, out);
+        return;
+    }
+    const uint32_t lane = __lane_id();
+    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+    uint64_t pend = __ballot(active);
+    if (!pend) return;
+    const uint64_t s0 = rng.s;
+    uint32_t base = 0;
+    bool done = !active, fall = false;
+    while (pend) {
+        const uint32_t n = (uint32_t)__popcll(pend);
+        const uint32_t k = 64u / n;
+        const bool me = (pend >> lane) & 1ull;
+        const uint32_t rank = (uint32_t)__popcll(pend & lt);
+        if (me) slot[rank] = lane;
+        const uint32_t tr = lane / k;
+        const bool helper = tr < n;
+        const uint32_t tl = helper ? slot[tr] : lane;
+        const uint32_t ts_lo = __shfl((uint32_t)s0, (int)tl), ts_hi = __shfl((uint32_t)(s0 >> 32), (int)tl);
+        const uint32_t tj = (uint32_t)__shfl((int)base, (int)tl) + (lane - tr * k);
+        float v[D];
+        bool acc = false, rare = false;
+        if (helper) {
+            uint64_t st = (((uint64_t)ts_hi << 32) | ts_lo) + (uint64_t)(tj * (uint32_t)D) * RTW_GOLDEN;
+            float ls = 0.0f;
+#pragma unroll
+            for (int d = 0; d < D; d++) {
+                st += RTW_GOLDEN;
+                const uint64_t x = rtw_mix64(st);
+                const int lz = rtw_clz64(x);
+                rare = rare || lz >= 41;
+                v[d] = -1.0f + 2.0f * float_from_draw(x, lz);  // randomDoubleRange(-1, 1)
+            }
+            if constexpr (D == 3) ls = v[0] * v[0] + v[1] * v[1] + v[2] * v[2];
+            else ls = v[0] * v[0] + v[1] * v[1];            // + 0*0 of the disk's z (exact)
+            acc = !rare && ls < 1.0f;
+        } else {
+#pragma unroll
+            for (int d = 0; d < D; d++) v[d] = 0.0f;
+        }
+        const uint64_t accb = __ballot(acc), rareb = __ballot(rare);
+        const uint32_t off = me ? rank * k : 0u;
+        const uint64_t m = (k >= 64u) ? ~0ull : ((1ull << k) - 1ull);
+        const uint64_t a = me ? ((accb >> off) & m) : 0ull;
+        const uint64_t q = me ? ((rareb >> off) & m) : 0ull;
+        const uint32_t fa = a ? (uint32_t)__builtin_ctzll(a) : 64u;
+        const uint32_t fq = q ? (uint32_t)__builtin_ctzll(q) : 64u;
+        const int src = (int)((me && fa < 64u) ? off + fa : lane);
+        float got[D];
+#pragma unroll
+        for (int d = 0; d < D; d++) got[d] = __shfl(v[d], src);
+        if (me) {
+            if (fq < 64u && fq <= fa) {
+                fall = true;
+            } else if (fa < 64u) {
+#pragma unroll
+                for (int d = 0; d < D; d++) out[d] = got[d];
+                rng.s = s0 + (uint64_t)((base + fa + 1u) * (uint32_t)D) * RTW_GOLDEN;
+                done = true;
+            } else {
+                base += k;
+            }
+        }
+        pend = __ballot(!done && !fall);
+    }
+    if (fall) {  // exact sequential path (rare-draw safe)
+        rng.s = s0;
+        seq_reject<D>(rng, out);
+    }
 }
 
 // One sample's radiance: getRay + iterative rayColor (camera.zig:169-208).
@@ -520,6 +699,8 @@ __global__ __launch_bounds__(256, WAVES) void render_persistent_v1(rtw_launch L)
     const uint32_t lane = __lane_id();
     const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     const uint32_t n_nodes = L.n_nodes;
+    __shared__ uint32_t coop_slots[4][64];  // per-wave scratch of coop_reject (1 KiB, multiple of 16 B)
+    uint32_t* const coop_slot = coop_slots[threadIdx.x >> 6];
 
     // wave-uniform queue state
     uint32_t q_cur = 0, q_end = 0;
@@ -600,23 +781,42 @@ __global__ __launch_bounds__(256, WAVES) void render_persistent_v1(rtw_launch L)
         if (!live) break;
         STAMP(t1) STAMP_ADD(c_assign, t0, t1)
 
-        // ---- 2. start a new sample: getRay (camera.zig:169-180)
-        if (st == ST_NEWSAMPLE) {
-            rng.s = rtw_mix64(L.key0 ^ (((uint64_t)pixel << 32) | (uint64_t)s));
-            ray = get_ray(L, px, py, rng);
-            thr = mk(1, 1, 1);
-            Ls = mk(0, 0, 0);
-            depth = L.max_depth;
-            if (depth == 0) {
-                st = ST_SHADE;  // rayColor(r, 0) = 0: finishes below without tracing
-                hit = -2;
-            } else {
-                rt = ray_trav(ray);
-                ti = 0;
-                closest = kInf;
-                hit = -1;
-                st = ST_TRAV;
-                cnt.rays++;
+        // ---- 2. start a new sample: getRay (camera.zig:169-180).  Jitter draws
+        // per lane, the defocus-disk rejection loop wave-cooperatively, then time.
+        {
+            const bool starting = st == ST_NEWSAMPLE;
+            f3 pixel_sample = mk(0, 0, 0);
+            if (starting) {
+                rng.s = rtw_mix64(L.key0 ^ (((uint64_t)pixel << 32) | (uint64_t)s));
+                const f3 du = ld3(L.du), dv = ld3(L.dv);
+                const f3 pixel_center = (ld3(L.pixel00) + du * splat((float)px)) + dv * splat((float)py);
+                const float jx = -0.5f + rnd(rng);
+                const float jy = -0.5f + rnd(rng);
+                pixel_sample = pixel_center + (splat(jx) * du + splat(jy) * dv);
+            }
+            float dsk[2] = {0.0f, 0.0f};
+            const bool defocus = L.defocus_angle > 0;
+            if (defocus) coop_reject<2>(starting, rng, dsk, coop_slot, L.coop != 0);
+            if (starting) {
+                f3 origin = ld3(L.center);
+                if (defocus) origin = (origin + ld3(L.disk_u) * splat(dsk[0])) + ld3(L.disk_v) * splat(dsk[1]);
+                ray.o = origin;
+                ray.d = pixel_sample - origin;
+                ray.time = rnd(rng);
+                thr = mk(1, 1, 1);
+                Ls = mk(0, 0, 0);
+                depth = L.max_depth;
+                if (depth == 0) {
+                    st = ST_SHADE;  // rayColor(r, 0) = 0: finishes below without tracing
+                    hit = -2;
+                } else {
+                    rt = ray_trav(ray);
+                    ti = 0;
+                    closest = kInf;
+                    hit = -1;
+                    st = ST_TRAV;
+                    cnt.rays++;
+                }
             }
         }
 
@@ -629,9 +829,13 @@ __global__ __launch_bounds__(256, WAVES) void render_persistent_v1(rtw_launch L)
                 const uint64_t trav = __ballot(st == ST_TRAV);
                 if (!trav) break;
                 if (popc64(__ballot(st == ST_SHADE)) >= want) break;
-                if (st == ST_TRAV) {
-                    ti = trav_step<FEAT>(nodes, L, ray, rt, ti, closest, hit, cnt);
-                    if (ti >= n_nodes) st = ST_SHADE;
+                // RTW_STEPS node steps per readiness check (amortises the ballot/branch bookkeeping)
+#pragma unroll
+                for (int u = 0; u < RTW_STEPS; u++) {
+                    if (st == ST_TRAV) {
+                        ti = trav_step<FEAT>(nodes, L, ray, rt, ti, closest, hit, cnt);
+                        if (ti >= n_nodes) st = ST_SHADE;
+                    }
                 }
 #if defined(RTW_STAMPS)
                 c_steps++;
@@ -643,37 +847,50 @@ __global__ __launch_bounds__(256, WAVES) void render_persistent_v1(rtw_launch L)
         c_passes++;
 #endif
 
-        // ---- 4. shade lanes whose walk is complete
-        if (st == ST_SHADE) {
-            bool cont = false;
-            if (hit == -1) {
-                Ls = Ls + thr * background(L, ray);
-            } else if (hit >= 0) {
-                f3 att;
-                Ray sc;
-                if (shade<FEAT>(nodes, L, ray, hit, closest, rng, thr, Ls, att, sc) && depth > 1) {
-                    thr = thr * att;
-                    ray = sc;
-                    depth--;
-                    rt = ray_trav(ray);
-                    ti = 0;
-                    closest = kInf;
-                    hit = -1;
-                    st = ST_TRAV;
-                    cnt.rays++;
-                    cont = true;
-                }
+        // ---- 4. shade lanes whose walk is complete: hit record per lane, the
+        // randomUnitVector rejection loop wave-cooperatively, then the material.
+        {
+            const bool shading = st == ST_SHADE;
+            HitPrep hp;
+            bool need_uv = false;
+            if (shading && hit >= 0) {
+                hp = hit_prep<FEAT>(nodes, L, ray, hit, closest);
+                need_uv = needs_unit_vector<FEAT>(hp.m.kind);
             }
-            if (!cont) {
-                if (is_nan3(Ls)) cnt.nans++;
-                acc = acc + Ls;
-                samples_done++;
-                s++;
-                if (s < L.s1) {
-                    st = ST_NEWSAMPLE;
-                } else {
-                    L.accum[out_idx] = make_float4(acc.x, acc.y, acc.z, (float)L.s1);  // camera.zig:55-56
-                    st = ST_NEWPIXEL;
+            float ruv3[3] = {0.0f, 0.0f, 0.0f};
+            coop_reject<3>(need_uv, rng, ruv3, coop_slot, L.coop != 0);
+            if (shading) {
+                bool cont = false;
+                if (hit == -1) {
+                    Ls = Ls + thr * background(L, ray);
+                } else if (hit >= 0) {
+                    f3 att;
+                    Ray sc;
+                    const f3 ruv = need_uv ? unit_vector(mk(ruv3[0], ruv3[1], ruv3[2])) : mk(0, 0, 0);
+                    if (scatter_finish<FEAT>(L, ray, hp, ruv, rng, thr, Ls, att, sc) && depth > 1) {
+                        thr = thr * att;
+                        ray = sc;
+                        depth--;
+                        rt = ray_trav(ray);
+                        ti = 0;
+                        closest = kInf;
+                        hit = -1;
+                        st = ST_TRAV;
+                        cnt.rays++;
+                        cont = true;
+                    }
+                }
+                if (!cont) {
+                    if (is_nan3(Ls)) cnt.nans++;
+                    acc = acc + Ls;
+                    samples_done++;
+                    s++;
+                    if (s < L.s1) {
+                        st = ST_NEWSAMPLE;
+                    } else {
+                        L.accum[out_idx] = make_float4(acc.x, acc.y, acc.z, (float)L.s1);  // camera.zig:55-56
+                        st = ST_NEWPIXEL;
+                    }
                 }
             }
         }
@@ -699,8 +916,37 @@ __global__ void debug_rng_kernel(uint64_t seed, uint32_t pixel, uint32_t sample,
     for (uint32_t k = 0; k < n; k++) out[k] = rtw_rng_float(r);
 }
 
+// Diagnostic: for every bounce of one sample, brute-force all leaves with the
+// exact test and with the fast-reject filter; record the first leaf the filter
+// would wrongly reject (out[8..]).
+__device__ void debug_filter_check(const rtw_launch& L, const Ray& r, float* out) {
+    const RayTrav rt = ray_trav(r);
+    for (uint32_t i = 0; i < L.n_nodes; i++) {
+        const float4 A = L.nodes[2 * i];
+        const float4 B = L.nodes[2 * i + 1];
+        if (!(fbits(A.w) & RTW_LEAF_BIT)) continue;
+        const f3 oc = r.o - mk(A.x, A.y, A.z);
+        const float half_b = dot(oc, r.d);
+        const float c = length_squared(oc) - B.x * B.x;
+        const float disc = half_b * half_b - rt.a * c;
+        if (!(disc >= 0)) continue;
+        const float sq = __builtin_sqrtf(disc);
+        const float r1 = (-half_b - sq) / rt.a, r2 = (-half_b + sq) / rt.a;
+        const bool acc_exact = (kTmin < r1) || (kTmin < r2);
+        const float sa = __builtin_amdgcn_sqrtf(disc);
+        const float e = (__builtin_fabsf(half_b) + sa) * rt.rcp_a * 3.8146973e-06f;
+        const float q1 = (-half_b - sa) * rt.rcp_a, q2 = (-half_b + sa) * rt.rcp_a;
+        const bool acc_fast = (q1 + e > kTmin) || (q2 + e > kTmin);
+        if (acc_exact && !acc_fast && out[8] == 0) {
+            out[8] = 1; out[9] = (float)i; out[10] = half_b; out[11] = c; out[12] = disc; out[13] = sq; out[14] = sa;
+            out[15] = rt.a; out[16] = rt.rcp_a; out[17] = r1; out[18] = r2; out[19] = q1; out[20] = q2; out[21] = e;
+        }
+    }
+}
+
 __global__ void debug_sample_kernel(rtw_launch L, uint32_t pixel, uint32_t sample, float* out) {
     if (threadIdx.x | blockIdx.x) return;
+    for (int k = 0; k < 32; k++) out[k] = 0;
     Counters cnt;
     const uint32_t x = pixel % L.W, y = pixel / L.W;
     f3 c = sample_radiance<RTW_F_ALL>(L.nodes, L, pixel, x + L.pixel_offset, y + L.pixel_offset, sample, cnt);
@@ -710,6 +956,46 @@ __global__ void debug_sample_kernel(rtw_launch L, uint32_t pixel, uint32_t sampl
     out[3] = (float)cnt.rays;
     out[4] = (float)cnt.nodes;
     out[5] = (float)cnt.leaves;
+    // replay the path to run the filter check on every bounce ray
+    rtw_rng rng;
+    rng.s = rtw_mix64(L.key0 ^ (((uint64_t)pixel << 32) | (uint64_t)sample));
+    Ray r = get_ray(L, x + L.pixel_offset, y + L.pixel_offset, rng);
+    f3 acc = mk(0, 0, 0), thr = mk(1, 1, 1);
+    int bounce = 0;
+    for (uint32_t depth = L.max_depth; depth > 0; depth--, bounce++) {
+        debug_filter_check(L, r, out);
+        float t;
+        const int hit = traverse<RTW_F_ALL>(L.nodes, L, r, t, cnt);
+        // brute-force exact closest over all leaves
+        {
+            const RayTrav rt = ray_trav(r);
+            float best = kInf;
+            int besti = -1;
+            for (uint32_t i = 0; i < L.n_nodes; i++) {
+                const float4 A = L.nodes[2 * i];
+                const float4 B = L.nodes[2 * i + 1];
+                if (!(fbits(A.w) & RTW_LEAF_BIT)) continue;
+                const f3 oc = r.o - mk(A.x, A.y, A.z);
+                const float half_b = dot(oc, r.d);
+                const float c = length_squared(oc) - B.x * B.x;
+                const float disc = half_b * half_b - rt.a * c;
+                if (!(disc >= 0)) continue;
+                const float sq = __builtin_sqrtf(disc);
+                float root = (-half_b - sq) / rt.a;
+                if (!(kTmin < root)) root = (-half_b + sq) / rt.a;
+                if (kTmin < root && root < best) { best = root; besti = (int)i; }
+            }
+            if ((besti != hit || (hit >= 0 && best != t)) && out[22] == 0) {
+                out[22] = 1; out[23] = (float)bounce; out[24] = (float)hit; out[25] = t; out[26] = (float)besti;
+                out[27] = best; out[28] = r.o.x; out[29] = r.o.y; out[30] = r.o.z;
+            }
+        }
+        if (hit < 0) break;
+        f3 att;
+        Ray sc;
+        if (!shade<RTW_F_ALL>(L.nodes, L, r, hit, t, rng, thr, acc, att, sc)) break;
+        r = sc;
+    }
 }
 
 template <uint32_t FEAT, bool LDS, int WAVES>
@@ -757,7 +1043,7 @@ void rtw_launch_render(const rtw_launch& L, void* stream, int variant, int grid)
         hipLaunchKernelGGL(render_pixels_v0, g, block, 0, st, L);
         return;
     }
-    const bool lds = L.n_nodes <= RTW_LDS_NODES;
+    const bool lds = L.n_nodes <= RTW_LDS_NODES && L.use_lds;
     const int w = (int)L.waves;
     switch (pick_feat(L.feat)) {
     case 0u:
@@ -772,12 +1058,12 @@ void rtw_launch_render(const rtw_launch& L, void* stream, int variant, int grid)
     }
 }
 
-int rtw_persistent_grid(uint32_t feat, uint32_t n_nodes, int waves) {
+int rtw_persistent_grid(uint32_t feat, uint32_t n_nodes, int waves, bool use_lds) {
     int dev = 0, n_cu = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
     if (n_cu <= 0) n_cu = 256;
-    const bool lds = n_nodes <= RTW_LDS_NODES;
+    const bool lds = n_nodes <= RTW_LDS_NODES && use_lds;
     const size_t bytes = (size_t)n_nodes * 32;
     int b;
     switch (pick_feat(feat)) {
