@@ -22,8 +22,9 @@ out = torch.zeros(8, dtype=torch.int64, device="cuda")
 for bvh in ("sah", "reference"):
     arr = rtw.flatten(objs, bvh_mode=rtw._abi.RTW_BVH_SAH if bvh == "sah" else rtw._abi.RTW_BVH_REFERENCE)
     w = rtw.World(arr)
-    for mode, name in ((0, "lds/random"), (1, "global/random"), (2, "lds/coherent"), (3, "global/coherent")):
-        for blocks, rpl in ((2048, 8), (8192, 8)):
+    for mode, name in ((2, "lds/coherent"), (3, "global/coherent"), (6, "lds/coh+bounce"),
+                       (7, "global/coh+bounce")):
+        for blocks, rpl in ((8192, 8),):
             ms = C.c_float()
             for rep in range(3):
                 out.zero_()

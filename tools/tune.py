@@ -23,13 +23,16 @@ cam.samples_per_pixel = spp
 cam.init()
 acc = torch.zeros((cam.size, 4), dtype=torch.float32, device="cuda")
 stream = torch.cuda.Stream()
-for st in settings:
+prev_keys = []
+rounds = int(os.environ.get("TUNE_ROUNDS", "1"))  # round-robin repeats (box noise)
+for st in [s for _ in range(rounds) for s in settings]:
     st = dict(st)
-    for k in ("RTW_KERNEL", "RTW_SHADE_MIN", "RTW_WAVES"):
+    for k in prev_keys + ["RTW_KERNEL", "RTW_SHADE_MIN", "RTW_WAVES"]:
         os.environ.pop(k, None)
-    arr.bvh_mode = {"ref": 0, "sah": 1}[st.pop("bvh", "ref")]
+    arr.bvh_mode = {"ref": 0, "sah": 1}[st.pop("bvh", "sah")]
     arr.order_dir = tuple(st.pop("order", (0.0, 0.0, 0.0)))
     os.environ.update(st)
+    prev_keys = list(st.keys())
     world = pkg.World(arr)
     cnt = torch.zeros(8, dtype=torch.int64, device="cuda")
     copts = pkg._abi.RtwRenderOpts(spp, 0, cnt.data_ptr())
@@ -38,6 +41,7 @@ for st in settings:
     c = cnt.cpu().tolist()
     st["nodes_per_ray"] = round((c[1] + c[2]) / max(1, c[0]), 2)
     st["inner_per_ray"] = round(c[1] / max(1, c[0]), 2)
+    st["rays_per_sample"] = round(c[0] / (cam.size * 2), 3)
     opts = pkg._abi.RtwRenderOpts(spp, 0, None)
     best = 1e9
     for it in range(3):

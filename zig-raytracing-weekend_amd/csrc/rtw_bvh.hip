@@ -354,12 +354,38 @@ private:
 }  // namespace
 
 int rtw_build_bvh(const rtw_scene_desc& desc, std::vector<rtw_node>& nodes, std::vector<float>& cvec,
-                  uint32_t* depth, uint32_t* axis_draws) {
+                  uint32_t* depth, uint32_t* axis_draws, float* box_pad, float* extent) {
+    if (box_pad) *box_pad = 0;
+    if (extent) *extent = 0;
     if (desc.bvh_mode == RTW_BVH_SAH) {
         SahBuilder b(desc, nodes, cvec);
         b.build();
         if (depth) *depth = b.depth();
         if (axis_draws) *axis_draws = 0;
+        // Pad the inner boxes for the FMA slab test: its t error for a plane P and
+        // origin o is < 4 ulp of (|P| + |o|) in space, so a pad of E * 2^-19
+        // (E = max |coordinate| of the scene) keeps the test conservative for
+        // every origin with |o| <= 7E (checked per launch, else the exact test runs).
+        // A superset of boxes is visited; sphere tests decide the hit.
+        float e = 0;
+        for (const rtw_node& n : nodes) {
+            uint32_t w;
+            std::memcpy(&w, &n.a[3], 4);
+            if (w & RTW_LEAF_BIT) continue;
+            for (int k = 0; k < 3; k++) e = std::max(e, std::max(std::fabs(n.a[k]), std::fabs(n.b[k])));
+        }
+        const float pad = e * 1.9073486e-06f;  // 2^-19
+        for (rtw_node& n : nodes) {
+            uint32_t w;
+            std::memcpy(&w, &n.a[3], 4);
+            if (w & RTW_LEAF_BIT) continue;
+            for (int k = 0; k < 3; k++) {
+                n.a[k] -= pad;
+                n.b[k] += pad;
+            }
+        }
+        if (box_pad) *box_pad = pad;
+        if (extent) *extent = e;
         return RTW_OK;
     }
     if (desc.bvh_mode != RTW_BVH_REFERENCE) return RTW_E_INVALID;

@@ -1,0 +1,678 @@
+// rtw_device.h -- device-side building blocks of the path tracer, shared by
+// the megakernels (rtw_kernels.hip) and the wavefront kernels (rtw_wavefront.hip).
+//
+// The per-pixel sample loop Camera.render -> rayColor -> BVHNode.hit / Aabb.hit ->
+// Sphere.hit -> Material.scatter -> Texture.value (src/camera.zig:93-208).
+//
+// Arithmetic contract: compiled with -ffp-contract=off (Zig's strict float
+// mode never fuses), correctly rounded fp32 div/sqrt (hipcc default), fp32
+// denormals kept.  Every geometric quantity (ray, t, p, normal, scatter
+// direction) is evaluated with the same IEEE-754 operations in the same order
+// as the Zig source, so paths are bit-identical to the CPU restatement under
+// the same RNG key.  The radiance of a path is accumulated iteratively
+// (L += T*e; T *= a) instead of the reference's recursive e0 + a0*(e1 + ...),
+// a re-association bounded by max_depth * 2^-24 relative.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "../../include/rtw_gpu.h"
+#include "rtw_internal.h"
+#include "rtw_layout.h"
+#include "rtw_rng.h"
+
+#pragma clang fp contract(off)
+
+#ifndef RTW_STEPS
+#define RTW_STEPS 1
+#endif
+
+#if defined(RTW_ABLATE_MATH)
+// timing ablation only (not IEEE): hardware sqrt / reciprocal
+#define __builtin_sqrtf(x) __builtin_amdgcn_sqrtf(x)
+#define RTW_DIV(a, b) ((a) * __builtin_amdgcn_rcpf(b))
+#else
+#define RTW_DIV(a, b) ((a) / (b))
+#endif
+
+namespace {
+
+constexpr float kPi = 3.1415926535897932385f;  // rtweekend.zig:4
+constexpr float kInf = __builtin_inff();
+
+struct f3 {
+    float x, y, z;
+};
+__device__ __forceinline__ f3 mk(float x, float y, float z) { return f3{x, y, z}; }
+__device__ __forceinline__ f3 operator+(f3 a, f3 b) { return f3{a.x + b.x, a.y + b.y, a.z + b.z}; }
+__device__ __forceinline__ f3 operator-(f3 a, f3 b) { return f3{a.x - b.x, a.y - b.y, a.z - b.z}; }
+__device__ __forceinline__ f3 operator*(f3 a, f3 b) { return f3{a.x * b.x, a.y * b.y, a.z * b.z}; }
+__device__ __forceinline__ f3 operator-(f3 a) { return f3{-a.x, -a.y, -a.z}; }
+__device__ __forceinline__ f3 splat(float s) { return f3{s, s, s}; }
+__device__ __forceinline__ f3 divs(f3 a, float s) { return f3{RTW_DIV(a.x, s), RTW_DIV(a.y, s), RTW_DIV(a.z, s)}; }
+__device__ __forceinline__ float dot(f3 u, f3 v) { return u.x * v.x + u.y * v.y + u.z * v.z; }
+__device__ __forceinline__ float length_squared(f3 u) { return u.x * u.x + u.y * u.y + u.z * u.z; }
+__device__ __forceinline__ f3 unit_vector(f3 v) { return divs(v, __builtin_sqrtf(length_squared(v))); }
+__device__ __forceinline__ f3 ld3(const float* p) { return f3{p[0], p[1], p[2]}; }
+__device__ __forceinline__ bool near_zero(f3 u) {  // vec3.zig:19-22
+    const float s = 1e-8f;
+    return __builtin_fabsf(u.x) < s && __builtin_fabsf(u.y) < s && __builtin_fabsf(u.z) < s;
+}
+__device__ __forceinline__ f3 reflect(f3 v, f3 n) { return v - n * splat(dot(v, n) * 2); }  // vec3.zig:77-79
+__device__ __forceinline__ f3 refract(f3 uv, f3 n, float e) {                             // vec3.zig:81-86
+    float c = dot(-uv, n);
+    float cos_theta = c < 1.0f ? c : 1.0f;
+    f3 perp = splat(e) * (uv + n * splat(cos_theta));
+    f3 par = n * splat(-__builtin_sqrtf(__builtin_fabsf(1.0f - length_squared(perp))));
+    return perp + par;
+}
+__device__ __forceinline__ uint32_t fbits(float f) { return __float_as_uint(f); }
+
+// ---- RNG helpers (rtweekend.zig / vec3.zig samplers) ----
+__device__ __forceinline__ float rnd(rtw_rng& r) { return rtw_rng_float(r); }
+__device__ __forceinline__ f3 random_unit_vector(rtw_rng& r) {  // vec3.zig:59-68
+#if defined(RTW_ABLATE_REJECT)
+    {   // timing ablation only: one candidate, no rejection loop (wrong distribution)
+        float x = rtw_rng_range(r, -1, 1), y = rtw_rng_range(r, -1, 1), z = rtw_rng_range(r, -1, 1);
+        return unit_vector(mk(x, y, z + 1e-3f));
+    }
+#endif
+    for (;;) {
+        float x = rtw_rng_range(r, -1, 1);
+        float y = rtw_rng_range(r, -1, 1);
+        float z = rtw_rng_range(r, -1, 1);
+        f3 p = mk(x, y, z);
+        if (length_squared(p) < 1) return unit_vector(p);
+    }
+}
+
+// Zig std.math.pow(f32, x, 5) via frexp-significand square-and-multiply +
+// scalbn (restated; identical fp32 operations to the CPU restatement).
+__device__ __forceinline__ float scalbn_f(float x, int n) {
+    float y = x;
+    if (n > 127) {
+        y *= 1.7014118346046923e38f; n -= 127;
+        if (n > 127) { y *= 1.7014118346046923e38f; n -= 127; if (n > 127) n = 127; }
+    } else if (n < -126) {
+        y *= 1.1754943508222875e-38f * 16777216.0f; n += 126 - 24;
+        if (n < -126) { y *= 1.1754943508222875e-38f * 16777216.0f; n += 126 - 24; if (n < -126) n = -126; }
+    }
+    return y * __uint_as_float((uint32_t)(0x7f + n) << 23);
+}
+__device__ __forceinline__ float frexp_sig(float x, int* e) {
+    uint32_t u = fbits(x);
+    int ee = (int)((u >> 23) & 0xFF);
+    int extra = 0;
+    if (ee == 0) {
+        if (x == 0) { *e = 0; return x; }
+        x = x * 18446744073709551616.0f;
+        u = fbits(x);
+        ee = (int)((u >> 23) & 0xFF);
+        extra = -64;
+    }
+    *e = ee - 126 + extra;
+    return __uint_as_float((u & 0x807FFFFFu) | 0x3F000000u);
+}
+__device__ __forceinline__ float pow5(float x) {
+    if (x == 1) return 1;
+    if (x == 0) return x;  // pow(+-0, odd int > 0) = +-0
+    if (!(x == x)) return x;
+    int xe;
+    float x1 = frexp_sig(x, &xe);
+    float a1 = 1.0f;
+    int ae = 0;
+    // i = 5 = 0b101
+    a1 *= x1; ae += xe;
+    x1 *= x1; xe <<= 1; if (x1 < 0.5f) { x1 += x1; xe -= 1; }
+    x1 *= x1; xe <<= 1; if (x1 < 0.5f) { x1 += x1; xe -= 1; }
+    a1 *= x1; ae += xe;
+    return scalbn_f(a1, ae);
+}
+__device__ __forceinline__ float reflectance(float cosine, float ref_idx) {  // material.zig:101-106
+    float r0 = (1 - ref_idx) / (1 + ref_idx);
+    r0 = r0 * r0;
+    return r0 + (1 - r0) * pow5(1 - cosine);
+}
+
+struct Ray {
+    f3 o, d;
+    float time;
+};
+
+// Camera.getRay (camera.zig:156-180)
+__device__ __forceinline__ Ray get_ray(const rtw_launch& L, uint32_t i, uint32_t j, rtw_rng& rng) {
+    const f3 du = ld3(L.du), dv = ld3(L.dv);
+    f3 pixel_center = (ld3(L.pixel00) + du * splat((float)i)) + dv * splat((float)j);
+    float px = -0.5f + rnd(rng);
+    float py = -0.5f + rnd(rng);
+    f3 pixel_sample = pixel_center + (splat(px) * du + splat(py) * dv);
+    f3 origin;
+    if (L.defocus_angle <= 0) {
+        origin = ld3(L.center);
+    } else {
+        float dx, dy;
+        for (;;) {  // vec3.randomInUnitDisk (vec3.zig:40-45)
+            dx = rtw_rng_range(rng, -1, 1);
+            dy = rtw_rng_range(rng, -1, 1);
+            if (dx * dx + dy * dy + 0.0f * 0.0f < 1) break;
+        }
+        origin = (ld3(L.center) + ld3(L.disk_u) * splat(dx)) + ld3(L.disk_v) * splat(dy);
+    }
+    Ray r;
+    r.o = origin;
+    r.d = pixel_sample - origin;
+    r.time = rnd(rng);
+    return r;
+}
+
+// Texture.value (textures.zig:22-123)
+__device__ float perlin_noise(const float4* tab, f3 p) {  // perlin.zig:117-162 + perlin_interp 30-53
+    const uint32_t* perm = reinterpret_cast<const uint32_t*>(tab + 256);
+    float u = p.x - __builtin_floorf(p.x);
+    float v = p.y - __builtin_floorf(p.y);
+    float w = p.z - __builtin_floorf(p.z);
+    int i = (int)__builtin_floorf(p.x);
+    int j = (int)__builtin_floorf(p.y);
+    int k = (int)__builtin_floorf(p.z);
+    float uu = u * u * (3 - 2 * u);
+    float vv = v * v * (3 - 2 * v);
+    float ww = w * w * (3 - 2 * w);
+    float accum = 0;
+#pragma unroll
+    for (int di = 0; di < 2; di++)
+#pragma unroll
+        for (int dj = 0; dj < 2; dj++)
+#pragma unroll
+            for (int dk = 0; dk < 2; dk++) {
+                uint32_t idx = perm[(i + di) & 255] ^ perm[256 + ((j + dj) & 255)] ^ perm[512 + ((k + dk) & 255)];
+                float4 c = tab[idx & 255];
+                const float i_f = (float)di, j_f = (float)dj, k_f = (float)dk;
+                f3 wv = mk(u - i_f, v - j_f, w - k_f);
+                accum += (i_f * uu + (1 - i_f) * (1 - uu)) * (j_f * vv + (1 - j_f) * (1 - vv)) *
+                         (k_f * ww + (1 - k_f) * (1 - ww)) * dot(mk(c.x, c.y, c.z), wv);
+            }
+    return accum;
+}
+
+__device__ __forceinline__ void sphere_uv(f3 p, float& u, float& v) {  // objects.zig:101-114
+    float theta = acosf(-p.y);
+    float phi = atan2f(-p.z, p.x) + kPi;
+    u = phi / (2 * kPi);
+    v = theta / kPi;
+}
+
+template <uint32_t FEAT>
+__device__ f3 texture_value(const rtw_launch& L, uint32_t ti, f3 outward, f3 p) {
+    const rtw_dev_texture& t = L.texs[ti];
+    const uint32_t kind = t.kind;
+    if constexpr ((FEAT & RTW_F_CHECKER) != 0) {
+        if (kind == RTW_TEX_CHECKER) {  // textures.zig:60-72
+            int xi = (int)__builtin_floorf(t.scale * p.x);
+            int yi = (int)__builtin_floorf(t.scale * p.y);
+            int zi = (int)__builtin_floorf(t.scale * p.z);
+            return ((xi + yi + zi) % 2 == 0) ? ld3(t.even) : ld3(t.odd);
+        }
+    }
+    if constexpr ((FEAT & RTW_F_IMAGE) != 0) {
+        if (kind == RTW_TEX_IMAGE) {  // textures.zig:85-104, rtw_image.zig:37-62
+            const rtw_dev_image im = L.img_info[t.image];
+            if (im.height <= 0) return mk(0, 1, 1);
+            float u, v;
+            sphere_uv(outward, u, v);
+            float nu = u < 0 ? 0 : (u > 1 ? 1 : u);
+            float nv = 1.0f - (v < 0 ? 0 : (v > 1 ? 1 : v));
+            uint32_t i = (uint32_t)__builtin_floorf(nu * (float)im.width);
+            uint32_t j = (uint32_t)__builtin_floorf(nv * (float)im.height);
+            uint32_t x = i < im.width ? i : im.width - 1;
+            uint32_t y = j < im.height ? j : im.height - 1;
+            const uchar4 px =
+                *reinterpret_cast<const uchar4*>(L.images + im.offset + (uint64_t)y * im.bytes_per_row + 4ull * x);
+            const float cs = 1.0f / 255.0f;
+            return mk(cs * (float)px.x, cs * (float)px.y, cs * (float)px.z);
+        }
+    }
+    if constexpr ((FEAT & RTW_F_NOISE) != 0) {
+        if (kind == RTW_TEX_NOISE) {  // textures.zig:118-123, perlin.zig:103-115
+            const float4* tab = L.perlin + (size_t)t.perlin * (RTW_PERLIN_BYTES / 16);
+            f3 s = splat(t.scale) * p;
+            float accum = 0, weight = 1.0f;
+            f3 tp = s;
+            for (int k = 0; k < 7; k++) {
+                accum += weight * perlin_noise(tab, tp);
+                weight *= 0.5f;
+                tp = tp * splat(2);
+            }
+            float turb = __builtin_fabsf(accum);
+            return splat(0.5f * (1 + sinf(s.z + 10 * turb)));
+        }
+    }
+    return ld3(t.even);  // RTW_TEX_SOLID (textures.zig:43-45)
+}
+
+struct Counters {
+    uint32_t rays = 0, nodes = 0, leaves = 0, nans = 0;
+};
+
+// Per-ray constants of the traversal.
+struct RayTrav {
+    f3 inv;      // 1 / d per axis (aabb.zig:87); fast box: clamped hardware reciprocal
+    f3 oinv;     // fast box only: -o * inv
+    float a;     // lengthSquared(d) (objects.zig:124)
+    float rcp_a; // hardware 1/a estimate for the sphere fast-reject (0 disables it)
+};
+__device__ __forceinline__ RayTrav ray_trav(const Ray& r, bool fast_box) {
+    RayTrav t;
+    if (fast_box) {
+        // |inv| <= 1e30 keeps every product finite (no inf*0 / inf-inf); a zero
+        // component gives slabs of +-1e30 * (P - o), i.e. still +-"infinite"
+        // given the >= E*2^-19 box pad
+        auto ci = [](float d) {
+            return __builtin_fmaxf(__builtin_fminf(__builtin_amdgcn_rcpf(d), 1e30f), -1e30f);
+        };
+        t.inv = mk(ci(r.d.x), ci(r.d.y), ci(r.d.z));
+        t.oinv = mk(-(r.o.x * t.inv.x), -(r.o.y * t.inv.y), -(r.o.z * t.inv.z));
+    } else {
+        t.inv = mk(RTW_DIV(1.0f, r.d.x), RTW_DIV(1.0f, r.d.y), RTW_DIV(1.0f, r.d.z));
+        t.oinv = mk(0, 0, 0);
+    }
+    t.a = length_squared(r.d);
+    // fast-reject only where every intermediate below stays normal and finite
+    t.rcp_a = (t.a > 1e-30f && t.a < 1e30f) ? __builtin_amdgcn_rcpf(t.a) : 0.0f;
+    return t;
+}
+
+constexpr float kTmin = 0.001f;  // camera.zig:187
+
+// Node i of the pre-order walk: two 16-B loads issued together (both halves are
+// needed on either path; a split load would put a second memory round trip on
+// the inner-node path).
+__device__ __forceinline__ void load_node(const float4* __restrict__ nodes, uint32_t i, float4& A, float4& B) {
+    A = nodes[2 * i];
+    B = nodes[2 * i + 1];
+    asm volatile("" ::"v"(A.x), "v"(A.y), "v"(A.z), "v"(A.w), "v"(B.x), "v"(B.y), "v"(B.z), "v"(B.w));
+}
+
+// Leaf: Sphere.hit (objects.zig:116-136) on the open interval (0.001, closest),
+// no box test (bvh.zig:123-125).  Updates closest/hit.
+template <uint32_t FEAT>
+__device__ __forceinline__ void leaf_test(const rtw_launch& L, const Ray& r, const RayTrav& rt, float4 A, float4 B,
+                                          uint32_t i, float& closest, int& hit, Counters& cnt) {
+    cnt.leaves++;
+    f3 center = mk(A.x, A.y, A.z);
+    if constexpr ((FEAT & RTW_F_MOVING) != 0) {
+        if (fbits(B.w)) {  // Sphere.getCenter (objects.zig:94-98)
+            const float4 cv = L.cvec[fbits(B.z)];
+            center = center + splat(r.time) * mk(cv.x, cv.y, cv.z);
+        }
+    }
+    const f3 oc = r.o - center;
+    const float half_b = dot(oc, r.d);
+    const float c = length_squared(oc) - B.x * B.x;
+    const float disc = half_b * half_b - rt.a * c;
+    bool exact = disc >= 0;
+#if !defined(RTW_ABLATE_MATH)
+    // Exact fast-reject: with hardware sqrt/rcp estimates (<= 1 ulp each) the
+    // candidate roots q1, q2 are within (|hb| + sq) / a * 6e-7 of the correctly
+    // rounded roots of objects.zig:130-136.  If neither can lie in
+    // (tmin, closest) even with a 2^-18 relative margin, the exact test
+    // would reject both: skip the IEEE sqrt and divisions.  Guards keep every
+    // intermediate finite and normal; otherwise the exact path runs.
+    // Written as ONE predicate (no nested branch): a nested-branch form was
+    // miscompiled by hipcc 7.2 (numerator left undefined on the guard-false edge).
+    {
+        const float sa = __builtin_amdgcn_sqrtf(disc);
+        const float e = (__builtin_fabsf(half_b) + sa) * rt.rcp_a * 3.8146973e-06f;
+        const float q1 = (-half_b - sa) * rt.rcp_a;
+        const float q2 = (-half_b + sa) * rt.rcp_a;
+        const bool guard = L.fast_reject && rt.rcp_a != 0.0f && disc > 1e-30f && disc < 1e30f &&
+                           __builtin_fabsf(half_b) < 1e15f;
+        const bool plausible = (q1 + e > kTmin && q1 - e < closest) || (q2 + e > kTmin && q2 - e < closest);
+        exact = exact && (plausible || !guard);
+    }
+#endif
+    if (exact) {
+        const float sq = __builtin_sqrtf(disc);
+        float root = RTW_DIV(-half_b - sq, rt.a);
+        bool ok = kTmin < root && root < closest;
+        if (!ok) {
+            root = RTW_DIV(-half_b + sq, rt.a);
+            ok = kTmin < root && root < closest;
+        }
+        if (ok) {
+            closest = root;
+            hit = (int)i;
+        }
+    }
+}
+
+// Inner node: Aabb.hit (aabb.zig:82-114) with [0.001, closest]; returns the next
+// node (i + 1 = descend, skip = past the subtree).
+//  exact: the reference arithmetic.  hi/lo use fmax/fmin: for the NaN slabs of a
+//    zero direction component (0*inf) maxNum keeps the other operand exactly like
+//    the reference's `if (t0 > min) min = t0`, and lo/hi only grow/shrink, so the
+//    single final `hi <= lo` equals the per-axis early exit of aabb.zig:111.
+//  fast (SAH trees): t = fma(P, inv, -o*inv) with min/max instead of swaps, on
+//    boxes padded by E*2^-19 -- conservative (never rejects a box the exact test
+//    on the unpadded box accepts), so the closest hit is unchanged.
+__device__ __forceinline__ uint32_t box_next(const Ray& r, const RayTrav& rt, float4 A, float4 B, uint32_t i,
+                                             float closest, bool fast) {
+    const uint32_t w = fbits(A.w);
+    if (fast) {
+        const float t0x = __builtin_fmaf(A.x, rt.inv.x, rt.oinv.x), t1x = __builtin_fmaf(B.x, rt.inv.x, rt.oinv.x);
+        const float t0y = __builtin_fmaf(A.y, rt.inv.y, rt.oinv.y), t1y = __builtin_fmaf(B.y, rt.inv.y, rt.oinv.y);
+        const float t0z = __builtin_fmaf(A.z, rt.inv.z, rt.oinv.z), t1z = __builtin_fmaf(B.z, rt.inv.z, rt.oinv.z);
+        const float lo = __builtin_fmaxf(__builtin_fmaxf(kTmin, __builtin_fminf(t0x, t1x)),
+                                         __builtin_fmaxf(__builtin_fminf(t0y, t1y), __builtin_fminf(t0z, t1z)));
+        const float hi = __builtin_fminf(__builtin_fminf(closest, __builtin_fmaxf(t0x, t1x)),
+                                         __builtin_fminf(__builtin_fmaxf(t0y, t1y), __builtin_fmaxf(t0z, t1z)));
+        return (hi <= lo) ? w : i + 1;
+    }
+    float t0x = (A.x - r.o.x) * rt.inv.x, t1x = (B.x - r.o.x) * rt.inv.x;
+    float t0y = (A.y - r.o.y) * rt.inv.y, t1y = (B.y - r.o.y) * rt.inv.y;
+    float t0z = (A.z - r.o.z) * rt.inv.z, t1z = (B.z - r.o.z) * rt.inv.z;
+    if (rt.inv.x < 0) { float tt = t1x; t1x = t0x; t0x = tt; }
+    if (rt.inv.y < 0) { float tt = t1y; t1y = t0y; t0y = tt; }
+    if (rt.inv.z < 0) { float tt = t1z; t1z = t0z; t0z = tt; }
+    const float lo = __builtin_fmaxf(__builtin_fmaxf(kTmin, t0x), __builtin_fmaxf(t0y, t0z));
+    const float hi = __builtin_fminf(__builtin_fminf(closest, t1x), __builtin_fminf(t1y, t1z));
+    return (hi <= lo) ? w : i + 1;
+}
+
+// One node of the stackless pre-order walk of the reference BVH
+// (bvh.zig:122-136).  Returns the next node index.
+template <uint32_t FEAT>
+__device__ __forceinline__ uint32_t trav_step(const float4* __restrict__ nodes, const rtw_launch& L, const Ray& r,
+                                              const RayTrav& rt, uint32_t i, float& closest, int& hit,
+                                              Counters& cnt) {
+    float4 A, B;
+    load_node(nodes, i, A, B);
+    const uint32_t w = fbits(A.w);
+    if (w & RTW_LEAF_BIT) {
+        leaf_test<FEAT>(L, r, rt, A, B, i, closest, hit, cnt);
+        return w & RTW_SKIP_MASK;
+    }
+    cnt.nodes++;
+    return box_next(r, rt, A, B, i, closest, L.fast_box != 0);
+}
+
+// World hit for one ray (whole walk).  Returns leaf node index or -1.
+template <uint32_t FEAT>
+__device__ __forceinline__ int traverse(const float4* __restrict__ nodes, const rtw_launch& L, const Ray& r,
+                                        float& t_out, Counters& cnt) {
+    const RayTrav rt = ray_trav(r, L.fast_box != 0);
+    float closest = kInf;
+    int hit = -1;
+    uint32_t i = 0;
+    const uint32_t n = L.n_nodes;
+    while (i < n) i = trav_step<FEAT>(nodes, L, r, rt, i, closest, hit, cnt);
+    t_out = closest;
+    return hit;
+}
+
+__device__ __forceinline__ f3 background(const rtw_launch& L, const Ray& r) {
+    if (L.bg_mode == RTW_BG_GRADIENT) {  // camera.zig:204-206
+        f3 ud = unit_vector(r.d);
+        float a = 0.5f * (ud.y + 1.0f);
+        return mk(1, 1, 1) * splat(1.0f - a) + mk(0.5f, 0.7f, 1.0f) * splat(a);
+    }
+    return ld3(L.background);  // camera.zig:207
+}
+
+// Hit record for the closest hit (objects.zig:139-145) + the material.
+struct HitPrep {
+    f3 p, outward, normal;
+    bool front;
+    rtw_dev_material m;
+};
+
+template <uint32_t FEAT>
+__device__ __forceinline__ HitPrep hit_prep(const float4* __restrict__ nodes, const rtw_launch& L, const Ray& r,
+                                            int hit, float t) {
+    const float4 A = nodes[2 * hit];
+    const float4 B = nodes[2 * hit + 1];
+    f3 center = mk(A.x, A.y, A.z);
+    if constexpr ((FEAT & RTW_F_MOVING) != 0) {
+        if (fbits(B.w)) {
+            const float4 cv = L.cvec[fbits(B.z)];
+            center = center + splat(r.time) * mk(cv.x, cv.y, cv.z);
+        }
+    }
+    HitPrep h;
+    h.p = r.o + splat(t) * r.d;
+    h.outward = divs(h.p - center, B.x);
+    h.front = dot(r.d, h.outward) < 0;
+    h.normal = h.front ? h.outward : -h.outward;
+    h.m = L.mats[fbits(B.y)];
+    return h;
+}
+
+// Does Material.scatter start by drawing vec3.randomUnitVector?
+// (Lambertian material.zig:44, Metal :67, Isotropic :140)
+template <uint32_t FEAT>
+__device__ __forceinline__ bool needs_unit_vector(uint32_t kind) {
+    if (kind == RTW_MAT_LAMBERTIAN || kind == RTW_MAT_METAL) return true;
+    if constexpr ((FEAT & RTW_F_LIGHT) != 0) return kind == RTW_MAT_ISOTROPIC;
+    return false;
+}
+
+// Material.emitted/scatter (material.zig:18-144) given the hit and, for the
+// materials that draw one, the random unit vector `ruv` (already drawn from rng).
+// Adds thr*emission to acc; returns true with (att, sc) when the ray scatters.
+template <uint32_t FEAT>
+__device__ __forceinline__ bool scatter_finish(const rtw_launch& L, const Ray& r, const HitPrep& h, f3 ruv,
+                                               rtw_rng& rng, f3 thr, f3& acc, f3& att, Ray& sc) {
+    const rtw_dev_material& m = h.m;
+    sc.o = h.p;
+    sc.time = r.time;
+    switch (m.kind) {
+    case RTW_MAT_LAMBERTIAN: {  // material.zig:43-54
+        f3 dir = h.normal + ruv;
+        if (near_zero(dir)) dir = h.normal;
+        sc.d = dir;
+        att = texture_value<FEAT>(L, m.texture, h.outward, h.p);
+        return true;
+    }
+    case RTW_MAT_METAL: {  // material.zig:65-70
+        f3 refl = reflect(unit_vector(r.d), h.normal);
+        sc.d = refl + splat(m.fuzz) * ruv;
+        att = ld3(m.albedo);
+        return dot(sc.d, h.normal) > 0;
+    }
+    case RTW_MAT_DIELECTRIC: {  // material.zig:80-98
+        att = mk(1, 1, 1);
+        const float ratio = h.front ? (1.0f / m.ir) : m.ir;
+        const f3 ud = unit_vector(r.d);
+        const float dd = dot(-ud, h.normal);
+        const float cos_theta = dd < 1.0f ? dd : 1.0f;
+        const float sin_theta = __builtin_sqrtf(1.0f - cos_theta * cos_theta);
+        const bool cannot = ratio * sin_theta > 1.0f;
+        if (cannot || reflectance(cos_theta, ratio) > rnd(rng))
+            sc.d = reflect(ud, h.normal);
+        else
+            sc.d = refract(ud, h.normal, ratio);
+        return true;
+    }
+    default:
+        break;
+    }
+    if constexpr ((FEAT & RTW_F_LIGHT) != 0) {
+        if (m.kind == RTW_MAT_DIFFUSE_LIGHT) {  // material.zig:119-125
+            acc = acc + thr * texture_value<FEAT>(L, m.texture, h.outward, h.p);
+            return false;
+        }
+        // RTW_MAT_ISOTROPIC (material.zig:139-143)
+        sc.d = ruv;
+        att = texture_value<FEAT>(L, m.texture, h.outward, h.p);
+        return true;
+    }
+    return false;
+}
+
+// Sequential form (one lane at a time): used by v0 and the debug kernel.
+template <uint32_t FEAT>
+__device__ __forceinline__ bool shade(const float4* __restrict__ nodes, const rtw_launch& L, const Ray& r, int hit,
+                                      float t, rtw_rng& rng, f3 thr, f3& acc, f3& att, Ray& sc) {
+    const HitPrep h = hit_prep<FEAT>(nodes, L, r, hit, t);
+    f3 ruv = mk(0, 0, 0);
+    if (needs_unit_vector<FEAT>(h.m.kind)) ruv = random_unit_vector(rng);
+    return scatter_finish<FEAT>(L, r, h, ruv, rng, thr, acc, att, sc);
+}
+
+// ---------------------------------------------------------------------------
+// Wave-cooperative rejection sampling (vec3.randomInUnitSphere D=3 /
+// randomInUnitDisk D=2, vec3.zig:40-45, 59-64).  The sequential loop runs until
+// the slowest lane of the wave accepts (E[max] ~ 6 iterations for 48 lanes at
+// p = 0.52).  The RNG is counter-based, so candidate j of a lane is simply draws
+// j*D+1 .. j*D+D after its current state: every round, all 64 lanes evaluate
+// candidates of the still-unresolved lanes (64/n helpers each, consecutive j),
+// and each lane takes its FIRST accepted candidate -- exactly the sequential
+// result and stream position.  A draw on Zig's rare extra-draw path
+// (clz >= 41, p = 2^-41) would shift positions: such a lane falls back to the
+// sequential loop from its start.  Must be called with every lane of the wave
+// converged (helpers are idle lanes).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float float_from_draw(uint64_t x, int lz) {
+    const uint32_t bits = ((uint32_t)(126 - lz) << 23) | (uint32_t)(x & 0x7FFFFFu);
+    return __uint_as_float(bits);
+}
+
+template <int D>
+__device__ __forceinline__ void seq_reject(rtw_rng& rng, float (&out)[D]) {
+    for (;;) {
+        float w[D];
+        float ls;
+#pragma unroll
+        for (int d = 0; d < D; d++) w[d] = rtw_rng_range(rng, -1, 1);
+        if constexpr (D == 3) ls = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
+        else ls = w[0] * w[0] + w[1] * w[1];
+        if (ls < 1.0f) {
+#pragma unroll
+            for (int d = 0; d < D; d++) out[d] = w[d];
+            return;
+        }
+    }
+}
+
+template <int D>
+__device__ __forceinline__ void coop_reject(bool active, rtw_rng& rng, float (&out)[D], uint32_t* slot,
+                                            bool coop = true) {
+    if (!coop) {  // A/B knob (RTW_COOP=0): plain per-lane loop, same results
+        if (active) seq_reject<D>(rng, out);
+        return;
+    }
+    const uint32_t lane = __lane_id();
+    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+    uint64_t pend = __ballot(active);
+    if (!pend) return;
+    const uint64_t s0 = rng.s;
+    uint32_t base = 0;
+    bool done = !active, fall = false;
+    while (pend) {
+        const uint32_t n = (uint32_t)__popcll(pend);
+        const uint32_t k = 64u / n;
+        const bool me = (pend >> lane) & 1ull;
+        const uint32_t rank = (uint32_t)__popcll(pend & lt);
+        if (me) slot[rank] = lane;
+        const uint32_t tr = lane / k;
+        const bool helper = tr < n;
+        const uint32_t tl = helper ? slot[tr] : lane;
+        const uint32_t ts_lo = __shfl((uint32_t)s0, (int)tl), ts_hi = __shfl((uint32_t)(s0 >> 32), (int)tl);
+        const uint32_t tj = (uint32_t)__shfl((int)base, (int)tl) + (lane - tr * k);
+        float v[D];
+        bool acc = false, rare = false;
+        if (helper) {
+            uint64_t st = (((uint64_t)ts_hi << 32) | ts_lo) + (uint64_t)(tj * (uint32_t)D) * RTW_GOLDEN;
+            float ls = 0.0f;
+#pragma unroll
+            for (int d = 0; d < D; d++) {
+                st += RTW_GOLDEN;
+                const uint64_t x = rtw_mix64(st);
+                const int lz = rtw_clz64(x);
+                rare = rare || lz >= 41;
+                v[d] = -1.0f + 2.0f * float_from_draw(x, lz);  // randomDoubleRange(-1, 1)
+            }
+            if constexpr (D == 3) ls = v[0] * v[0] + v[1] * v[1] + v[2] * v[2];
+            else ls = v[0] * v[0] + v[1] * v[1];            // + 0*0 of the disk's z (exact)
+            acc = !rare && ls < 1.0f;
+        } else {
+#pragma unroll
+            for (int d = 0; d < D; d++) v[d] = 0.0f;
+        }
+        const uint64_t accb = __ballot(acc), rareb = __ballot(rare);
+        const uint32_t off = me ? rank * k : 0u;
+        const uint64_t m = (k >= 64u) ? ~0ull : ((1ull << k) - 1ull);
+        const uint64_t a = me ? ((accb >> off) & m) : 0ull;
+        const uint64_t q = me ? ((rareb >> off) & m) : 0ull;
+        const uint32_t fa = a ? (uint32_t)__builtin_ctzll(a) : 64u;
+        const uint32_t fq = q ? (uint32_t)__builtin_ctzll(q) : 64u;
+        const int src = (int)((me && fa < 64u) ? off + fa : lane);
+        float got[D];
+#pragma unroll
+        for (int d = 0; d < D; d++) got[d] = __shfl(v[d], src);
+        if (me) {
+            if (fq < 64u && fq <= fa) {
+                fall = true;
+            } else if (fa < 64u) {
+#pragma unroll
+                for (int d = 0; d < D; d++) out[d] = got[d];
+                rng.s = s0 + (uint64_t)((base + fa + 1u) * (uint32_t)D) * RTW_GOLDEN;
+                done = true;
+            } else {
+                base += k;
+            }
+        }
+        pend = __ballot(!done && !fall);
+    }
+    if (fall) {  // exact sequential path (rare-draw safe)
+        rng.s = s0;
+        seq_reject<D>(rng, out);
+    }
+}
+
+// One sample's radiance: getRay + iterative rayColor (camera.zig:169-208).
+template <uint32_t FEAT>
+__device__ f3 sample_radiance(const float4* __restrict__ nodes, const rtw_launch& L, uint32_t pixel, uint32_t x,
+                              uint32_t y, uint32_t s, Counters& cnt) {
+    rtw_rng rng;
+    rng.s = rtw_mix64(L.key0 ^ (((uint64_t)pixel << 32) | (uint64_t)s));
+    Ray r = get_ray(L, x, y, rng);
+    f3 acc = mk(0, 0, 0);
+    f3 thr = mk(1, 1, 1);
+    for (uint32_t depth = L.max_depth; depth > 0; depth--) {
+        cnt.rays++;
+        float t;
+        const int hit = traverse<FEAT>(nodes, L, r, t, cnt);
+        if (hit < 0) {
+            acc = acc + thr * background(L, r);
+            break;
+        }
+        f3 att;
+        Ray sc;
+        if (!shade<FEAT>(nodes, L, r, hit, t, rng, thr, acc, att, sc)) break;
+        thr = thr * att;
+        r = sc;
+    }
+    return acc;
+}
+
+__device__ __forceinline__ bool map_row(const rtw_launch& L, uint32_t r, uint32_t& y) {
+    if (L.n_shards) {
+        const uint32_t blk = r / L.rpb;
+        y = (blk * L.n_shards + L.shard) * L.rpb + r % L.rpb;
+    } else {
+        y = r;
+    }
+    return y < L.H;
+}
+
+__device__ __forceinline__ void flush_counters(const rtw_launch& L, const Counters& c, uint32_t samples) {
+    if (!L.counters) return;
+    atomicAdd(&L.counters[RTW_STAT_RAYS], (unsigned long long)c.rays);
+    atomicAdd(&L.counters[RTW_STAT_NODES], (unsigned long long)c.nodes);
+    atomicAdd(&L.counters[RTW_STAT_LEAVES], (unsigned long long)c.leaves);
+    atomicAdd(&L.counters[RTW_STAT_SAMPLES], (unsigned long long)samples);
+    if (c.nans) atomicAdd(&L.counters[RTW_STAT_NAN], (unsigned long long)c.nans);
+}
+
+__device__ __forceinline__ bool is_nan3(f3 c) { return !(c.x == c.x) || !(c.y == c.y) || !(c.z == c.z); }
+
+}  // namespace

@@ -2,6 +2,7 @@
 // Camera.init, batched launches with cancel/progress, sharded row rendering.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -13,6 +14,7 @@
 #include "rtw_internal.h"
 #include "rtw_layout.h"
 #include "rtw_rng.h"
+#include "rtw_wavefront.h"
 
 namespace {
 
@@ -165,7 +167,7 @@ int rtw_scene_create(const rtw_scene_desc* d, int device, rtw_ctx** out) {
     ctx->device = device;
     std::vector<float> cvec;
     uint32_t depth = 0, draws = 0;
-    int rc = rtw_build_bvh(*d, ctx->nodes_host, cvec, &depth, &draws);
+    int rc = rtw_build_bvh(*d, ctx->nodes_host, cvec, &depth, &draws, &ctx->box_pad, &ctx->extent);
     if (rc != RTW_OK) {
         delete ctx;
         return fail(rc, "BVH build failed (unknown bvh_mode?)");
@@ -262,7 +264,22 @@ int rtw_scene_create(const rtw_scene_desc* d, int device, rtw_ctx** out) {
     ctx->feat = scene_features(d);
     L.feat = ctx->feat;
     L.work_counter = ctx->d_work;
-    if (const char* kv = std::getenv("RTW_KERNEL")) ctx->variant = (std::strcmp(kv, "v0") == 0) ? 0 : 1;
+    if (const char* kv = std::getenv("RTW_KERNEL"))
+        ctx->variant = (std::strcmp(kv, "v0") == 0) ? 0 : (std::strcmp(kv, "v1") == 0) ? 1 : 2;
+    if (const char* wp = std::getenv("RTW_WF_PATHS")) {
+        long long v = std::atoll(wp);
+        if (v >= 4096) ctx->wf_max_paths = (uint64_t)v;
+    }
+    if (const char* wi = std::getenv("RTW_WF_ITERS")) {
+        int v = std::atoi(wi);
+        ctx->wf_iters = (uint32_t)(v < 1 ? 1 : (v > RTW_WF_MAX_ITERS ? RTW_WF_MAX_ITERS : v));
+    }
+    {
+        int n_cu = 0;
+        if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || n_cu < 1)
+            n_cu = 256;
+        ctx->n_cu = n_cu;
+    }
     if (const char* sm = std::getenv("RTW_SHADE_MIN")) {
         int v = std::atoi(sm);
         ctx->shade_min = (uint32_t)(v < 1 ? 1 : (v > 64 ? 64 : v));
@@ -278,6 +295,18 @@ int rtw_scene_create(const rtw_scene_desc* d, int device, rtw_ctx** out) {
     if (const char* wv = std::getenv("RTW_WAVES")) L.waves = (uint32_t)std::atoi(wv);
     L.use_lds = 1;
     if (const char* ul = std::getenv("RTW_LDS")) L.use_lds = (uint32_t)std::atoi(ul);
+    // SAH trees: FMA slab test on the padded boxes + leaf postponement (both only
+    // enlarge the set of visited nodes; reference trees keep the exact aabb.zig walk)
+    const bool sah = ctx->box_pad > 0;
+    L.fast_box = sah ? 1 : 0;
+    L.postpone = sah ? 1 : 0;
+    L.leaf_min = 32;
+    if (const char* fb = std::getenv("RTW_FASTBOX")) L.fast_box = sah && std::atoi(fb) != 0;
+    if (const char* pp = std::getenv("RTW_POSTPONE")) L.postpone = (uint32_t)std::atoi(pp);
+    if (const char* lm = std::getenv("RTW_LEAF_MIN")) {
+        int v = std::atoi(lm);
+        L.leaf_min = (uint32_t)(v < 1 ? 1 : (v > 64 ? 64 : v));
+    }
     ctx->grid = rtw_persistent_grid(ctx->feat, (uint32_t)n_nodes, (int)L.waves, L.use_lds != 0);
 
     ctx->stats.n_nodes = (uint32_t)n_nodes;
@@ -298,6 +327,7 @@ void rtw_scene_destroy(rtw_ctx* ctx) {
     if (ctx->d_scratch) (void)hipFree(ctx->d_scratch);
     if (ctx->d_dbg) (void)hipFree(ctx->d_dbg);
     if (ctx->d_work) (void)hipFree(ctx->d_work);
+    if (ctx->d_wf) (void)hipFree(ctx->d_wf);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -352,6 +382,15 @@ rtw_launch make_launch(const rtw_ctx* ctx, const rtw_camera* c, uint64_t seed) {
     L.bg_mode = c->background_mode;
     L.pixel_offset = c->pixel_offset;
     L.key0 = rtw_mix64(seed);
+    if (L.fast_box) {
+        // the box pad covers ray origins with |o| <= 7 * extent (rtw_bvh.hip): primary
+        // origins are the camera centre + the defocus disk; secondary ones lie in the scene
+        float o = 0;
+        for (int k = 0; k < 3; k++)
+            o = std::max(o, std::fabs(c->center[k]) + std::fabs(c->defocus_disk_u[k]) +
+                                std::fabs(c->defocus_disk_v[k]));
+        if (!(o <= 7.0f * ctx->extent)) L.fast_box = 0;
+    }
     return L;
 }
 
@@ -372,6 +411,57 @@ int validate_cam(const rtw_camera* cam) {
 
 // Enqueue [s0, s1) in batches on `stream`, polling cancel/progress between
 // batches when `sync_each` (host API).  Returns status.
+// Wavefront (v2) render of samples [L.s0, L.s1): batches of n_s samples so that
+// n_pix * n_s paths fit the path-state buffer (grown on demand, kept in the ctx).
+int run_wavefront(rtw_ctx* ctx, rtw_launch L, hipStream_t stream) {
+    rtw_wf W{};
+    W.n_tx = (L.W + 7) / 8;
+    const uint64_t n_pix = (uint64_t)W.n_tx * ((L.n_rows + 7) / 8) * 64;
+    const uint32_t spp = L.s1 - L.s0;
+    uint64_t n_s = std::max<uint64_t>(1, ctx->wf_max_paths / n_pix);
+    if (n_s > spp) n_s = spp;
+    const uint64_t need = n_pix * n_s;
+    if (need > 0x7FFFFFFFull) return fail(RTW_E_INVALID, "wavefront batch too large");
+    if (ctx->wf_cap < need) {
+        if (ctx->d_wf) {
+            HIP_TRY(hipStreamSynchronize(stream));
+            (void)hipFree(ctx->d_wf);
+        }
+        ctx->d_wf = nullptr;
+        ctx->wf_cap = 0;
+        const uint64_t cap_seg = ((need + 63) / 64 + RTW_WF_SEGS - 1) / RTW_WF_SEGS * 64;
+        const size_t bytes = need * RTW_WF_PATH_BYTES + 2 * cap_seg * RTW_WF_SEGS * 4 + 2 * RTW_WF_SEGS * 4 + 256;
+        HIP_TRY(hipMalloc(&ctx->d_wf, bytes));
+        ctx->wf_cap = need;
+    }
+    const uint64_t P = ctx->wf_cap;
+    const uint64_t cap_seg = ((P + 63) / 64 + RTW_WF_SEGS - 1) / RTW_WF_SEGS * 64;
+    W.ray_o = (float4*)ctx->d_wf;
+    W.ray_d = W.ray_o + P;
+    W.thr = W.ray_d + P;
+    W.ls = W.thr + P;
+    W.rng = (uint64_t*)(W.ls + P);
+    W.hit = (float2*)(W.rng + P);
+    W.queue[0] = (uint32_t*)(W.hit + P);
+    W.queue[1] = W.queue[0] + cap_seg * RTW_WF_SEGS;
+    W.seg_len[0] = W.queue[1] + cap_seg * RTW_WF_SEGS;
+    W.seg_len[1] = W.seg_len[0] + RTW_WF_SEGS;
+    W.n_pix = (uint32_t)n_pix;
+    W.iters = ctx->wf_iters;
+    const uint32_t s_end = L.s1;
+    for (uint32_t s = L.s0; s < s_end; s += (uint32_t)n_s) {
+        L.s0 = s;
+        L.s1 = (s_end - s < n_s) ? s_end : s + (uint32_t)n_s;
+        W.n_s = L.s1 - L.s0;
+        W.n_paths = (uint32_t)(n_pix * W.n_s);
+        W.seg_cap = (uint32_t)((((uint64_t)W.n_paths + 63) / 64 + RTW_WF_SEGS - 1) / RTW_WF_SEGS * 64);
+        rtw_wavefront_batch(L, W, stream, ctx->n_cu);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return hip_fail(e, "wavefront launch");
+    }
+    return RTW_OK;
+}
+
 int run_batches(rtw_ctx* ctx, rtw_launch L, uint32_t s0, uint32_t s1, uint32_t batch, hipStream_t stream,
                 bool sync_each, const volatile int32_t* cancel, rtw_progress_fn progress, void* user,
                 uint64_t pixels) {
@@ -380,10 +470,14 @@ int run_batches(rtw_ctx* ctx, rtw_launch L, uint32_t s0, uint32_t s1, uint32_t b
         if (cancel && *cancel) return fail(RTW_E_CANCELLED, "cancelled");
         L.s0 = s;
         L.s1 = (s1 - s < batch) ? s1 : s + batch;
-        if (ctx->variant == 1) HIP_TRY(hipMemsetAsync(ctx->d_work, 0, 256, stream));
-        rtw_launch_render(L, stream, ctx->variant, ctx->grid);
-        hipError_t e = hipGetLastError();
-        if (e != hipSuccess) return hip_fail(e, "render launch");
+        if (ctx->variant == 2) {
+            if (int rc = run_wavefront(ctx, L, stream)) return rc;
+        } else {
+            if (ctx->variant == 1) HIP_TRY(hipMemsetAsync(ctx->d_work, 0, 256, stream));
+            rtw_launch_render(L, stream, ctx->variant, ctx->grid);
+            hipError_t e = hipGetLastError();
+            if (e != hipSuccess) return hip_fail(e, "render launch");
+        }
         if (sync_each) {
             HIP_TRY(hipStreamSynchronize(stream));
             if (progress && progress(pixels * (uint64_t)(L.s1 - s0), total, user)) return fail(RTW_E_CANCELLED, "cancelled by progress callback");

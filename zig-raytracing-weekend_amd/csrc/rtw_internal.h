@@ -53,6 +53,9 @@ struct rtw_launch {
     uint32_t use_lds;            // 1 = stage the BVH in LDS when it fits (default), 0 = read nodes from L1/L2
     uint32_t coop;               // 1 = wave-cooperative rejection sampling (default), 0 = per-lane loops
     uint32_t fast_reject;        // 1 = exact sphere fast-reject filter (default), 0 = always the IEEE path
+    uint32_t fast_box;           // 1 = FMA slab test on padded boxes (SAH trees only), 0 = aabb.zig arithmetic
+    uint32_t postpone;           // 1 = postpone leaf tests until leaf_min/64 of the walking lanes hold one
+    uint32_t leaf_min;           // postponement threshold in 1/64ths of the walking lanes
 };
 
 #define RTW_TILE_W 16
@@ -81,8 +84,10 @@ void rtw_launch_render(const rtw_launch& L, void* stream, int variant, int grid)
 void rtw_launch_debug_rng(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t n, float* d_out, void* stream);
 void rtw_launch_debug_sample(const rtw_launch& L, uint32_t pixel, uint32_t sample, float* d_out, void* stream);
 
+// box_pad/extent (out, may be null): SAH trees pad every inner box by
+// extent * 2^-19 so the FMA slab test (rtw_kernels.hip box_next) stays conservative.
 int rtw_build_bvh(const rtw_scene_desc& desc, std::vector<rtw_node>& nodes, std::vector<float>& cvec,
-                  uint32_t* depth, uint32_t* axis_draws);
+                  uint32_t* depth, uint32_t* axis_draws, float* box_pad = nullptr, float* extent = nullptr);
 
 // One scene on one device (the opaque rtw_ctx of include/rtw_gpu.h).
 struct rtw_ctx {
@@ -99,6 +104,13 @@ struct rtw_ctx {
     uint32_t* d_work = nullptr;    // persistent-kernel work counter (zeroed before each launch)
     uint32_t feat = 0;             // RTW_F_* scene features
     int grid = 0;                  // resident blocks of the persistent kernel
-    int variant = 1;               // 1 = persistent v1 (default), 0 = simple v0 (RTW_KERNEL=v0)
+    int variant = 2;               // 2 = wavefront v2 (default), 1 = persistent v1, 0 = simple v0 (RTW_KERNEL)
     uint32_t shade_min = 48;       // RTW_SHADE_MIN (tuned on C2: 8..64 -> 48 best)
+    void* d_wf = nullptr;          // wavefront path state (rtw_wavefront.h), wf_cap paths
+    uint64_t wf_cap = 0;
+    uint64_t wf_max_paths = 1u << 24;  // RTW_WF_PATHS: paths per wavefront batch (x 88 B)
+    uint32_t wf_iters = 8;         // RTW_WF_ITERS: wavefront bounces before the tail kernel
+    int n_cu = 256;                // compute units of the device (wavefront grids)
+    float box_pad = 0;             // absolute pad baked into the inner boxes (SAH trees), 0 = none
+    float extent = 0;              // max |coordinate| over the scene's boxes
 };
