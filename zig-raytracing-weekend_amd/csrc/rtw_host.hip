@@ -422,6 +422,12 @@ int run_wavefront(rtw_ctx* ctx, rtw_launch L, hipStream_t stream) {
     if (n_s > spp) n_s = spp;
     const uint64_t need = n_pix * n_s;
     if (need > 0x7FFFFFFFull) return fail(RTW_E_INVALID, "wavefront batch too large");
+    // stripe capacity: a stripe receives the survivors of nw/STRIPES waves that
+    // each take <= ceil(chunks / nw) 64-path chunks (rtw_wavefront.h)
+    const uint64_t max_waves = rtw_wavefront_max_waves(ctx->n_cu);
+    auto stripe_cap = [&](uint64_t paths) {
+        return ((paths + 63) / 64 / RTW_WF_STRIPES + 1 + max_waves / RTW_WF_STRIPES) * 64;
+    };
     if (ctx->wf_cap < need) {
         if (ctx->d_wf) {
             HIP_TRY(hipStreamSynchronize(stream));
@@ -429,13 +435,12 @@ int run_wavefront(rtw_ctx* ctx, rtw_launch L, hipStream_t stream) {
         }
         ctx->d_wf = nullptr;
         ctx->wf_cap = 0;
-        const uint64_t cap_seg = ((need + 63) / 64 + RTW_WF_SEGS - 1) / RTW_WF_SEGS * 64;
-        const size_t bytes = need * RTW_WF_PATH_BYTES + 2 * cap_seg * RTW_WF_SEGS * 4 + 2 * RTW_WF_SEGS * 4 + 256;
+        const size_t bytes = need * RTW_WF_PATH_BYTES + 2 * stripe_cap(need) * RTW_WF_STRIPES * 4 +
+                             2 * RTW_WF_STRIPES * RTW_WF_LEN_STRIDE * 4 + 256;
         HIP_TRY(hipMalloc(&ctx->d_wf, bytes));
         ctx->wf_cap = need;
     }
-    const uint64_t P = ctx->wf_cap;
-    const uint64_t cap_seg = ((P + 63) / 64 + RTW_WF_SEGS - 1) / RTW_WF_SEGS * 64;
+    const uint64_t P = ctx->wf_cap, qcap = stripe_cap(P) * RTW_WF_STRIPES;
     W.ray_o = (float4*)ctx->d_wf;
     W.ray_d = W.ray_o + P;
     W.thr = W.ray_d + P;
@@ -443,9 +448,9 @@ int run_wavefront(rtw_ctx* ctx, rtw_launch L, hipStream_t stream) {
     W.rng = (uint64_t*)(W.ls + P);
     W.hit = (float2*)(W.rng + P);
     W.queue[0] = (uint32_t*)(W.hit + P);
-    W.queue[1] = W.queue[0] + cap_seg * RTW_WF_SEGS;
-    W.seg_len[0] = W.queue[1] + cap_seg * RTW_WF_SEGS;
-    W.seg_len[1] = W.seg_len[0] + RTW_WF_SEGS;
+    W.queue[1] = W.queue[0] + qcap;
+    W.len[0] = W.queue[1] + qcap;
+    W.len[1] = W.len[0] + RTW_WF_STRIPES * RTW_WF_LEN_STRIDE;
     W.n_pix = (uint32_t)n_pix;
     W.iters = ctx->wf_iters;
     const uint32_t s_end = L.s1;
@@ -454,7 +459,7 @@ int run_wavefront(rtw_ctx* ctx, rtw_launch L, hipStream_t stream) {
         L.s1 = (s_end - s < n_s) ? s_end : s + (uint32_t)n_s;
         W.n_s = L.s1 - L.s0;
         W.n_paths = (uint32_t)(n_pix * W.n_s);
-        W.seg_cap = (uint32_t)((((uint64_t)W.n_paths + 63) / 64 + RTW_WF_SEGS - 1) / RTW_WF_SEGS * 64);
+        W.stripe_cap = (uint32_t)stripe_cap(W.n_paths);
         rtw_wavefront_batch(L, W, stream, ctx->n_cu);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return hip_fail(e, "wavefront launch");

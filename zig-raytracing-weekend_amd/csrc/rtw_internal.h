@@ -108,8 +108,8 @@ struct rtw_ctx {
     uint32_t shade_min = 48;       // RTW_SHADE_MIN (tuned on C2: 8..64 -> 48 best)
     void* d_wf = nullptr;          // wavefront path state (rtw_wavefront.h), wf_cap paths
     uint64_t wf_cap = 0;
-    uint64_t wf_max_paths = 1u << 24;  // RTW_WF_PATHS: paths per wavefront batch (x 88 B)
-    uint32_t wf_iters = 8;         // RTW_WF_ITERS: wavefront bounces before the tail kernel
+    uint64_t wf_max_paths = 1u << 26;  // RTW_WF_PATHS: paths per wavefront batch (x ~90 B)
+    uint32_t wf_iters = 6;         // RTW_WF_ITERS: wavefront bounces before the tail kernel
     int n_cu = 256;                // compute units of the device (wavefront grids)
     float box_pad = 0;             // absolute pad baked into the inner boxes (SAH trees), 0 = none
     float extent = 0;              // max |coordinate| over the scene's boxes

@@ -37,23 +37,60 @@ __device__ __forceinline__ bool wf_pixel(const rtw_launch& L, const rtw_wf& W, u
     return true;
 }
 
-// Entry k of segment g at iteration it -> path id (false: padding or no path).
-// Iteration 0 deals 64-path chunks round-robin (chunk c -> segment c % SEGS).
-__device__ __forceinline__ bool wf_entry(const rtw_wf& W, uint32_t it, uint32_t g, uint32_t k, uint32_t& p) {
-    if (it == 0) {
-        p = (((k >> 6) * RTW_WF_SEGS + g) << 6) | (k & 63u);
-        return p < W.n_paths;
-    }
-    p = W.queue[it & 1u][(size_t)g * W.seg_cap + k];
-    return true;
-}
-
-__device__ __forceinline__ uint32_t wf_seg_len(const rtw_wf& W, uint32_t it, uint32_t g) {
-    return it == 0 ? W.seg_cap : W.seg_len[it & 1u][g];
-}
-
 __device__ __forceinline__ uint32_t wf_wave() { return blockIdx.x * 4u + (threadIdx.x >> 6); }
 __device__ __forceinline__ uint32_t wf_nwaves() { return gridDim.x * 4u; }
+
+// The paths of iteration `it` handed to this wave, 64 at a time:
+//   for (WfIter e(W, it); e.more(); e.next()) { uint32_t p; if (e.get(W, p)) ... }
+// (wave-uniform loop; get() is per lane)
+struct WfIter {
+    uint32_t it, j, step, n, base;
+    const uint32_t* q;
+    __device__ WfIter(const rtw_wf& W, uint32_t it_) : it(it_) {
+        const uint32_t w = wf_wave(), nw = wf_nwaves();
+        if (it == 0) {
+            j = w;
+            step = nw;
+            n = (W.n_paths + 63u) >> 6;  // chunks
+            q = nullptr;
+            base = 0;
+        } else {
+            const uint32_t s = w % RTW_WF_STRIPES;
+            j = w / RTW_WF_STRIPES;
+            step = nw / RTW_WF_STRIPES;
+            n = (W.len[it & 1u][s * RTW_WF_LEN_STRIDE] + 63u) >> 6;
+            q = W.queue[it & 1u] + (size_t)s * W.stripe_cap;
+            base = W.len[it & 1u][s * RTW_WF_LEN_STRIDE];  // entries in the stripe
+        }
+    }
+    __device__ bool more() const { return j < n; }
+    __device__ void next() { j += step; }
+    __device__ bool get(const rtw_wf& W, uint32_t& p) const {
+        const uint32_t k = (j << 6) | __lane_id();
+        if (it == 0) {
+            p = k;
+            return p < W.n_paths;
+        }
+        if (k >= base) return false;
+        p = q[k];
+        return true;
+    }
+};
+
+// wave-aggregated append of `p` (where push) to this wave's output stripe
+__device__ __forceinline__ void wf_push(const rtw_wf& W, uint32_t it, bool push, uint32_t p) {
+    const uint64_t m = __ballot(push);
+    if (!m) return;
+    const uint32_t s = wf_wave() % RTW_WF_STRIPES, lane = __lane_id();
+    uint32_t* len = &W.len[(it + 1u) & 1u][s * RTW_WF_LEN_STRIDE];
+    uint32_t base = 0;
+    if (lane == 0) base = atomicAdd(len, (uint32_t)__popcll(m));
+    base = __shfl(base, 0);
+    if (push) {
+        const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+        W.queue[(it + 1u) & 1u][(size_t)s * W.stripe_cap + base + (uint32_t)__popcll(m & lt)] = p;
+    }
+}
 
 __device__ __forceinline__ Ray wf_load_ray(const rtw_wf& W, uint32_t p, uint32_t& depth) {
     const float4 o = W.ray_o[p], d = W.ray_d[p];
@@ -93,104 +130,116 @@ __global__ __launch_bounds__(256) void wf_gen(rtw_launch L, rtw_wf W) {
 // trace: closest hit per queued ray (no shading state in registers)
 template <uint32_t FEAT>
 __global__ __launch_bounds__(256) void wf_trace(rtw_launch L, rtw_wf W, uint32_t it) {
+    // the stripes shade(it) appends to start empty (they were iteration it-1's input)
+    if (blockIdx.x == 0) W.len[(it + 1u) & 1u][threadIdx.x * RTW_WF_LEN_STRIDE] = 0;
+    static_assert(RTW_WF_STRIPES == 256, "one block zeroes the stripe counters");
     Counters cnt;
-    for (uint32_t g = wf_wave(); g < RTW_WF_SEGS; g += wf_nwaves()) {
-        const uint32_t n = wf_seg_len(W, it, g);
-        for (uint32_t k = __lane_id(); k - __lane_id() < n; k += 64) {
-            uint32_t p;
-            if (k < n && wf_entry(W, it, g, k, p)) {
-                uint32_t depth;
-                const Ray r = wf_load_ray(W, p, depth);
-                if (depth) {
-                    float t;
-                    const int h = traverse<FEAT>(L.nodes, L, r, t, cnt);
-                    W.hit[p] = make_float2(t, __int_as_float(h));
-                    cnt.rays++;
-                }
+    for (WfIter e(W, it); e.more(); e.next()) {
+        uint32_t p;
+        if (e.get(W, p)) {
+            uint32_t depth;
+            const Ray r = wf_load_ray(W, p, depth);
+            if (depth) {
+                float t;
+                const int h = traverse<FEAT>(L.nodes, L, r, t, cnt);
+                W.hit[p] = make_float2(t, __int_as_float(h));
+                cnt.rays++;
             }
         }
     }
     flush_counters(L, cnt, 0);
 }
 
-// shade: emission / background and Material.scatter; survivors -> the same
-// segment of the next queue, compacted with a ballot prefix (no atomics)
+// shade: emission / background and Material.scatter; survivors -> next queue
 template <uint32_t FEAT>
 __global__ __launch_bounds__(256) void wf_shade(rtw_launch L, rtw_wf W, uint32_t it) {
-    uint32_t* next = W.queue[(it + 1u) & 1u];
-    const uint32_t lane = __lane_id();
-    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    for (uint32_t g = wf_wave(); g < RTW_WF_SEGS; g += wf_nwaves()) {
-        const uint32_t n = wf_seg_len(W, it, g);
-        uint32_t* out = next + (size_t)g * W.seg_cap;
-        uint32_t n_out = 0;
-        for (uint32_t k = lane; k - lane < n; k += 64) {
-            bool push = false;
-            uint32_t p = 0;
-            if (k < n && wf_entry(W, it, g, k, p)) {
-                uint32_t depth;
-                const Ray r = wf_load_ray(W, p, depth);
-                if (depth) {
-                    const float2 h = W.hit[p];
-                    const int hit = __float_as_int(h.y);
-                    const float4 t4 = W.thr[p], l4 = W.ls[p];
-                    f3 thr = mk(t4.x, t4.y, t4.z), acc = mk(l4.x, l4.y, l4.z);
-                    if (hit < 0) {
-                        acc = acc + thr * background(L, r);
-                    } else {
-                        rtw_rng rng;
-                        rng.s = W.rng[p];
-                        f3 att;
-                        Ray sc;
-                        if (shade<FEAT>(L.nodes, L, r, hit, h.x, rng, thr, acc, att, sc) && depth > 1) {
-                            wf_store_ray(W, p, sc, depth - 1);
-                            thr = thr * att;
-                            W.thr[p] = make_float4(thr.x, thr.y, thr.z, 0);
-                            W.rng[p] = rng.s;
-                            push = true;
-                        }
+    for (WfIter e(W, it); e.more(); e.next()) {
+        bool push = false;
+        uint32_t p = 0;
+        if (e.get(W, p)) {
+            uint32_t depth;
+            const Ray r = wf_load_ray(W, p, depth);
+            if (depth) {
+                const float2 h = W.hit[p];
+                const int hit = __float_as_int(h.y);
+                const float4 t4 = W.thr[p], l4 = W.ls[p];
+                f3 thr = mk(t4.x, t4.y, t4.z), acc = mk(l4.x, l4.y, l4.z);
+                if (hit < 0) {
+                    acc = acc + thr * background(L, r);
+                } else {
+                    rtw_rng rng;
+                    rng.s = W.rng[p];
+                    f3 att;
+                    Ray sc;
+                    if (shade<FEAT>(L.nodes, L, r, hit, h.x, rng, thr, acc, att, sc) && depth > 1) {
+                        wf_store_ray(W, p, sc, depth - 1);
+                        thr = thr * att;
+                        W.thr[p] = make_float4(thr.x, thr.y, thr.z, 0);
+                        W.rng[p] = rng.s;
+                        push = true;
                     }
-                    W.ls[p] = make_float4(acc.x, acc.y, acc.z, 0);
                 }
+                W.ls[p] = make_float4(acc.x, acc.y, acc.z, 0);
             }
-            const uint64_t m = __ballot(push);
-            if (push) out[n_out + (uint32_t)__popcll(m & lt)] = p;
-            n_out += (uint32_t)__popcll(m);
         }
-        if (lane == 0) W.seg_len[(it + 1u) & 1u][g] = n_out;
+        wf_push(W, it, push, p);
     }
 }
 
-// tail: the paths still queued after the last wavefront iteration, each to completion
+// tail: the paths still queued after the last wavefront iteration, each to
+// completion; a lane whose path ends takes the wave's next path at once
 template <uint32_t FEAT>
 __global__ __launch_bounds__(256) void wf_tail(rtw_launch L, rtw_wf W, uint32_t it) {
+    const uint32_t w = wf_wave(), lane = __lane_id();
+    const uint32_t s = w % RTW_WF_STRIPES, r0 = w / RTW_WF_STRIPES, R = wf_nwaves() / RTW_WF_STRIPES;
+    const uint32_t n = W.len[it & 1u][s * RTW_WF_LEN_STRIDE];
+    const uint32_t* q = W.queue[it & 1u] + (size_t)s * W.stripe_cap;
+    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     Counters cnt;
-    for (uint32_t g = wf_wave(); g < RTW_WF_SEGS; g += wf_nwaves()) {
-        const uint32_t n = wf_seg_len(W, it, g);
-        for (uint32_t k = __lane_id(); k - __lane_id() < n; k += 64) {
-            uint32_t p;
-            if (k < n && wf_entry(W, it, g, k, p)) {
-                uint32_t depth;
-                Ray r = wf_load_ray(W, p, depth);
+    uint32_t cursor = 0, p = 0, depth = 0;
+    bool active = false;
+    Ray r;
+    f3 thr = mk(0, 0, 0), acc = mk(0, 0, 0);
+    rtw_rng rng;
+    rng.s = 0;
+    for (;;) {
+        const uint64_t need = __ballot(!active);
+        if (need) {
+            // m-th path of this wave = stripe entry ((m / 64) * R + r0) * 64 + m % 64
+            const uint32_t m = cursor + (uint32_t)__popcll(need & lt);
+            cursor += (uint32_t)__popcll(need);
+            const uint32_t k = (((m >> 6) * R + r0) << 6) | (m & 63u);
+            if (!active && k < n) {
+                p = q[k];
+                r = wf_load_ray(W, p, depth);
                 const float4 t4 = W.thr[p], l4 = W.ls[p];
-                f3 thr = mk(t4.x, t4.y, t4.z), acc = mk(l4.x, l4.y, l4.z);
-                rtw_rng rng;
+                thr = mk(t4.x, t4.y, t4.z);
+                acc = mk(l4.x, l4.y, l4.z);
                 rng.s = W.rng[p];
-                for (; depth > 0; depth--) {  // the rest of rayColor's iterations
-                    cnt.rays++;
-                    float t;
-                    const int hit = traverse<FEAT>(L.nodes, L, r, t, cnt);
-                    if (hit < 0) {
-                        acc = acc + thr * background(L, r);
-                        break;
-                    }
-                    f3 att;
-                    Ray sc;
-                    if (!shade<FEAT>(L.nodes, L, r, hit, t, rng, thr, acc, att, sc)) break;
+                active = true;
+            }
+        }
+        if (!__ballot(active)) break;
+        if (active) {  // one more iteration of rayColor
+            cnt.rays++;
+            float t;
+            const int hit = traverse<FEAT>(L.nodes, L, r, t, cnt);
+            bool done = true;
+            if (hit < 0) {
+                acc = acc + thr * background(L, r);
+            } else {
+                f3 att;
+                Ray sc;
+                if (shade<FEAT>(L.nodes, L, r, hit, t, rng, thr, acc, att, sc) && depth > 1) {
                     thr = thr * att;
                     r = sc;
+                    depth--;
+                    done = false;
                 }
+            }
+            if (done) {
                 W.ls[p] = make_float4(acc.x, acc.y, acc.z, 0);
+                active = false;
             }
         }
     }
@@ -221,26 +270,40 @@ __global__ __launch_bounds__(256) void wf_reduce(rtw_launch L, rtw_wf W) {
     flush_counters(L, cnt, samples);
 }
 
+// resident blocks of `kernel`, rounded down to whole stripes of waves
 template <typename K>
-uint32_t wf_resident(K kernel, int n_cu) {
+uint32_t wf_grid(K kernel, int n_cu) {
     int b = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kernel, 256, 0) != hipSuccess || b < 1) b = 1;
-    return (uint32_t)(b * n_cu);
+    uint32_t g = (uint32_t)(b * n_cu);
+    g -= g % (RTW_WF_STRIPES / 4);
+    return g ? g : RTW_WF_STRIPES / 4;
+}
+
+template <uint32_t FEAT>
+struct WfGrids {
+    uint32_t trace, shade, tail;
+    explicit WfGrids(int n_cu)
+        : trace(wf_grid(wf_trace<FEAT>, n_cu)), shade(wf_grid(wf_shade<FEAT>, n_cu)),
+          tail(wf_grid(wf_tail<FEAT>, n_cu)) {}
+};
+
+template <uint32_t FEAT>
+const WfGrids<FEAT>& wf_grids(int n_cu) {
+    static const WfGrids<FEAT> g(n_cu);
+    return g;
 }
 
 template <uint32_t FEAT>
 void wf_run(const rtw_launch& L, const rtw_wf& W, hipStream_t st, int n_cu) {
-    // grids = resident blocks (each wave then walks SEGS / waves segments)
-    static const uint32_t g_trace = wf_resident(wf_trace<FEAT>, n_cu);
-    static const uint32_t g_shade = wf_resident(wf_shade<FEAT>, n_cu);
-    static const uint32_t g_tail = wf_resident(wf_tail<FEAT>, n_cu);
+    const WfGrids<FEAT>& g = wf_grids<FEAT>(n_cu);
     hipLaunchKernelGGL(wf_gen<FEAT>, dim3((W.n_paths + 255u) / 256u), dim3(256), 0, st, L, W);
     const uint32_t iters = L.max_depth < W.iters ? L.max_depth : W.iters;
     for (uint32_t it = 0; it < iters; it++) {
-        hipLaunchKernelGGL(wf_trace<FEAT>, dim3(g_trace), dim3(256), 0, st, L, W, it);
-        hipLaunchKernelGGL(wf_shade<FEAT>, dim3(g_shade), dim3(256), 0, st, L, W, it);
+        hipLaunchKernelGGL(wf_trace<FEAT>, dim3(g.trace), dim3(256), 0, st, L, W, it);
+        hipLaunchKernelGGL(wf_shade<FEAT>, dim3(g.shade), dim3(256), 0, st, L, W, it);
     }
-    if (iters < L.max_depth) hipLaunchKernelGGL(wf_tail<FEAT>, dim3(g_tail), dim3(256), 0, st, L, W, iters);
+    if (iters < L.max_depth) hipLaunchKernelGGL(wf_tail<FEAT>, dim3(g.tail), dim3(256), 0, st, L, W, iters);
     hipLaunchKernelGGL(wf_reduce, dim3((W.n_pix + 255u) / 256u), dim3(256), 0, st, L, W);
 }
 
@@ -258,4 +321,11 @@ void rtw_wavefront_batch(const rtw_launch& L, const rtw_wf& W, void* stream, int
     case RTW_F_CHECKER: wf_run<RTW_F_CHECKER>(L, W, st, n_cu); break;
     default: wf_run<RTW_F_ALL>(L, W, st, n_cu); break;
     }
+}
+
+uint32_t rtw_wavefront_max_waves(int n_cu) {
+    uint32_t m = 0;
+    for (uint32_t g : {wf_grids<0u>(n_cu).shade, wf_grids<RTW_F_CHECKER>(n_cu).shade, wf_grids<RTW_F_ALL>(n_cu).shade})
+        m = g > m ? g : m;
+    return 4 * m;
 }
