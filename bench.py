@@ -85,10 +85,10 @@ def main():
     my_rows = shard.rows
     assert my_rows == L.rtw_shard_rows(H, ROWS_PER_BLOCK, world_size, rank)
 
-    def render_step(counters=None, w=None):
+    def render_step(counters=None, w=None, timing=None):
         if w is not None:
             saved, shard.world = shard.world, w
-        shard.render(0, spp, seed=0, stream=stream, counters=counters)
+        shard.render(0, spp, seed=0, stream=stream, counters=counters, timing=timing)
         if w is not None:
             shard.world = saved
 
@@ -103,7 +103,7 @@ def main():
         torch.cuda.synchronize()
         c = cnt.cpu().numpy()
         return {k: int(c[getattr(pkg._abi, "RTW_STAT_" + k.upper())]) for k in ("nodes", "leaves", "rays", "samples",
-                                                                                 "nan")}
+                                                                                 "nan", "tail_rays")}
     cref = counted(world_ref)
     cdev = counted(world)
     world_ref.close()
@@ -117,6 +117,8 @@ def main():
         gather_step()
     torch.cuda.synchronize()
 
+    # per-kernel HIP events, recorded by the library on the render stream around every launch
+    timings = [pkg._abi.RtwKernelTiming() for _ in range(args.steps)]
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     if distributed:
         dist.barrier()
@@ -124,7 +126,7 @@ def main():
     t_start = time.perf_counter()
     for k in range(args.steps):
         ev[k][0].record(stream)
-        render_step()
+        render_step(timing=timings[k])
         ev[k][1].record(stream)
         gather_step()
     torch.cuda.synchronize()
@@ -139,8 +141,18 @@ def main():
 
     total_samples = W * H * spp * args.steps
     value = total_samples / elapsed / 1e6
-    avg_kernel_s = sum(kernel_ms) / len(kernel_ms) / 1e3
-    achieved = alg_bytes / avg_kernel_s / 1e9
+    render_s = sum(kernel_ms) / len(kernel_ms) / 1e3          # whole render call (all kernels) per step
+    kms = {n: sum(t.ms[i] for t in timings) for i, n in enumerate(pkg._abi.RTW_K_NAMES)}
+    kcalls = {n: sum(t.launches[i] for t in timings) for i, n in enumerate(pkg._abi.RTW_K_NAMES)}
+    dom = max(kms, key=lambda n: kms[n])                        # dominant kernel (device time)
+    # algorithmic bytes (reference topology) of the rays each kernel kind traces
+    b_ray = NODE_BYTES * (nodes + leaves) / max(1, rays)
+    dom_bytes_step = {"trace": b_ray * (rays - cref["tail_rays"]), "tail": b_ray * cref["tail_rays"],
+                      "mega": alg_bytes}.get(dom, 0.0)
+    dom_launch_s = kms[dom] / max(1, kcalls[dom]) / 1e3
+    dom_bytes_launch = dom_bytes_step * args.steps / max(1, kcalls[dom])
+    achieved = dom_bytes_launch / dom_launch_s / 1e9 if dom_launch_s > 0 else 0.0
+    path_achieved = alg_bytes / render_s / 1e9
 
     cpu = None
     if rank == 0 and world_size == 1 and not args.no_cpu_baseline:
@@ -167,10 +179,18 @@ def main():
                        + (" + RCCL gather" if distributed else ""), "rows_per_block": ROWS_PER_BLOCK},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                         "kernel": "render_persistent_v1", "avg_launch_ms": round(avg_kernel_s * 1e3, 3),
-                         "alg_bytes_per_launch": alg_bytes,
+                         "kernel": {"trace": "wf_trace", "tail": "wf_tail", "mega": "render_persistent_v1"}.get(dom, dom),
+                         "avg_launch_ms": round(dom_launch_s * 1e3, 4),
+                         "launches_per_step": kcalls[dom] / args.steps,
+                         "alg_bytes_per_launch": round(dom_bytes_launch),
+                         "path": {"achieved": round(path_achieved, 2), "frac": round(path_achieved / HBM_PEAK_GBS, 4),
+                                  "render_ms": round(render_s * 1e3, 3), "alg_bytes_per_step": alg_bytes},
+                         "kernel_ms_per_step": {n: round(v / args.steps, 3) for n, v in kms.items() if kcalls[n]},
+                         "launches": {n: v // args.steps for n, v in kcalls.items() if v},
                          "alg_bytes_per_sample": round(alg_bytes / max(1, samples), 2),
                          "rays_per_sample": round(rays / max(1, samples), 4),
+                         "tail_ray_frac": round(cref["tail_rays"] / max(1, rays), 5),
+                         "alg_bytes_per_ray": round(b_ray, 2),
                          "nodes_per_ray_reference": round((nodes + leaves) / max(1, rays), 3),
                          "nodes_per_ray_device": round((cdev["nodes"] + cdev["leaves"]) / max(1, cdev["rays"]), 3),
                          "bvh": args.bvh},

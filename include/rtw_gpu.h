@@ -166,14 +166,24 @@ typedef struct rtw_ctx rtw_ctx;
  * Return non-zero to cancel (like RenderThread.stop, src/main.zig:58-60). */
 typedef int (*rtw_progress_fn)(uint64_t samples_done, uint64_t samples_total, void* user);
 
+/* Device time per kernel kind of one render call (rtw_render_opts.timing). */
+enum { RTW_K_GEN = 0, RTW_K_TRACE = 1, RTW_K_SHADE = 2, RTW_K_TAIL = 3, RTW_K_REDUCE = 4, RTW_K_MEGA = 5,
+       RTW_K_COUNT = 8 };
+typedef struct rtw_kernel_timing {
+    float ms[RTW_K_COUNT];         /* summed HIP-event time of the launches of each kind */
+    uint32_t launches[RTW_K_COUNT];
+} rtw_kernel_timing;
+
 typedef struct rtw_render_opts {
     uint32_t spp_batch;        /* samples per kernel launch (cancel/progress granularity); 0 = auto */
     uint32_t flags;            /* RTW_RENDER_* */
     uint64_t* counters;        /* optional device-side stats out (RTW_STAT_COUNT u64) or NULL */
+    rtw_kernel_timing* timing; /* optional host out: per-kernel device time (the call then synchronises) */
 } rtw_render_opts;
 
 enum { RTW_RENDER_NO_SYNC = 1u };  /* rtw_render_device: do not synchronise the stream */
 enum { RTW_STAT_RAYS = 0, RTW_STAT_NODES = 1, RTW_STAT_LEAVES = 2, RTW_STAT_SAMPLES = 3, RTW_STAT_NAN = 4,
+       RTW_STAT_TAIL_RAYS = 5, /* rays traced by the wavefront tail kernel (subset of RAYS) */
        RTW_STAT_COUNT = 8 };
 
 int rtw_version(void);

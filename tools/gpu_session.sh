@@ -22,5 +22,11 @@ if [ -n "${TUNE_ARGS:-}" ]; then step tune 600 python tools/tune.py ${TUNE_ARGS}
 step bench 900 python bench.py ${BENCH_ARGS:-}
 if [ "${PROFILE:-1}" = 1 ]; then
   step rocprof 900 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python bench.py --no-cpu-baseline --steps 2 --warmup 0 ${BENCH_ARGS:-}
+  grep "^{" "$OUT/rocprof.log" > "$OUT/rocprof_bench.json" || true
+  python tools/prof_summary.py "$OUT/prof/run_kernel_trace.csv" --json "$OUT/rocprof_bench.json" > "$OUT/prof_timed_summary.txt" 2>&1 || true
+  cat "$OUT/prof_timed_summary.txt"
+fi
+if [ "${PMC:-0}" = 1 ]; then
+  step pmc 1300 bash tools/pmc_traffic.sh
 fi
 echo "== done $(date +%T)"

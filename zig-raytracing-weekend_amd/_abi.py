@@ -20,7 +20,10 @@ RTW_TEX_SOLID, RTW_TEX_CHECKER, RTW_TEX_IMAGE, RTW_TEX_NOISE = range(4)
 RTW_BG_CONSTANT, RTW_BG_GRADIENT = 0, 1
 RTW_BVH_REFERENCE, RTW_BVH_SAH = 0, 1
 RTW_RENDER_NO_SYNC = 1
-RTW_STAT_RAYS, RTW_STAT_NODES, RTW_STAT_LEAVES, RTW_STAT_SAMPLES, RTW_STAT_NAN, RTW_STAT_COUNT = 0, 1, 2, 3, 4, 8
+RTW_STAT_RAYS, RTW_STAT_NODES, RTW_STAT_LEAVES, RTW_STAT_SAMPLES, RTW_STAT_NAN, RTW_STAT_TAIL_RAYS = 0, 1, 2, 3, 4, 5
+RTW_STAT_COUNT = 8
+RTW_K_GEN, RTW_K_TRACE, RTW_K_SHADE, RTW_K_TAIL, RTW_K_REDUCE, RTW_K_MEGA, RTW_K_COUNT = 0, 1, 2, 3, 4, 5, 8
+RTW_K_NAMES = ("gen", "trace", "shade", "tail", "reduce", "mega")
 
 # numpy record layouts == the C structs (asserted against sizeof in tests)
 SPHERE_DT = np.dtype([("center1", "<f4", 3), ("radius", "<f4"), ("center2", "<f4", 3), ("is_moving", "<u4"),
@@ -69,8 +72,13 @@ class RtwCamera(C.Structure):
                 ("defocus_angle", C.c_float), ("background", F3)]
 
 
+class RtwKernelTiming(C.Structure):
+    _fields_ = [("ms", C.c_float * 8), ("launches", C.c_uint32 * 8)]
+
+
 class RtwRenderOpts(C.Structure):
-    _fields_ = [("spp_batch", C.c_uint32), ("flags", C.c_uint32), ("counters", C.c_void_p)]
+    _fields_ = [("spp_batch", C.c_uint32), ("flags", C.c_uint32), ("counters", C.c_void_p),
+                ("timing", C.POINTER(RtwKernelTiming))]
 
 
 class RtwSceneStats(C.Structure):

@@ -249,7 +249,7 @@ __device__ f3 texture_value(const rtw_launch& L, uint32_t ti, f3 outward, f3 p) 
 }
 
 struct Counters {
-    uint32_t rays = 0, nodes = 0, leaves = 0, nans = 0;
+    uint32_t rays = 0, nodes = 0, leaves = 0, nans = 0, tail_rays = 0;
 };
 
 // Per-ray constants of the traversal.
@@ -671,6 +671,7 @@ __device__ __forceinline__ void flush_counters(const rtw_launch& L, const Counte
     atomicAdd(&L.counters[RTW_STAT_LEAVES], (unsigned long long)c.leaves);
     atomicAdd(&L.counters[RTW_STAT_SAMPLES], (unsigned long long)samples);
     if (c.nans) atomicAdd(&L.counters[RTW_STAT_NAN], (unsigned long long)c.nans);
+    if (c.tail_rays) atomicAdd(&L.counters[RTW_STAT_TAIL_RAYS], (unsigned long long)c.tail_rays);
 }
 
 __device__ __forceinline__ bool is_nan3(f3 c) { return !(c.x == c.x) || !(c.y == c.y) || !(c.z == c.z); }

@@ -301,6 +301,11 @@ int rtw_scene_create(const rtw_scene_desc* d, int device, rtw_ctx** out) {
     L.fast_box = sah ? 1 : 0;
     L.postpone = sah ? 1 : 0;
     L.leaf_min = 32;
+    L.refill_min = 0;
+    if (const char* rm = std::getenv("RTW_REFILL_MIN")) {
+        int v = std::atoi(rm);
+        L.refill_min = (uint32_t)(v < 0 ? 0 : (v > 64 ? 64 : v));
+    }
     if (const char* fb = std::getenv("RTW_FASTBOX")) L.fast_box = sah && std::atoi(fb) != 0;
     if (const char* pp = std::getenv("RTW_POSTPONE")) L.postpone = (uint32_t)std::atoi(pp);
     if (const char* lm = std::getenv("RTW_LEAF_MIN")) {
@@ -328,6 +333,7 @@ void rtw_scene_destroy(rtw_ctx* ctx) {
     if (ctx->d_dbg) (void)hipFree(ctx->d_dbg);
     if (ctx->d_work) (void)hipFree(ctx->d_work);
     if (ctx->d_wf) (void)hipFree(ctx->d_wf);
+    for (hipEvent_t e : ctx->ev_pool) (void)hipEventDestroy(e);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -413,7 +419,7 @@ int validate_cam(const rtw_camera* cam) {
 // batches when `sync_each` (host API).  Returns status.
 // Wavefront (v2) render of samples [L.s0, L.s1): batches of n_s samples so that
 // n_pix * n_s paths fit the path-state buffer (grown on demand, kept in the ctx).
-int run_wavefront(rtw_ctx* ctx, rtw_launch L, hipStream_t stream) {
+int run_wavefront(rtw_ctx* ctx, rtw_launch L, hipStream_t stream, rtw_timer* T) {
     rtw_wf W{};
     W.n_tx = (L.W + 7) / 8;
     const uint64_t n_pix = (uint64_t)W.n_tx * ((L.n_rows + 7) / 8) * 64;
@@ -460,7 +466,7 @@ int run_wavefront(rtw_ctx* ctx, rtw_launch L, hipStream_t stream) {
         W.n_s = L.s1 - L.s0;
         W.n_paths = (uint32_t)(n_pix * W.n_s);
         W.stripe_cap = (uint32_t)stripe_cap(W.n_paths);
-        rtw_wavefront_batch(L, W, stream, ctx->n_cu);
+        rtw_wavefront_batch(L, W, stream, ctx->n_cu, T);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return hip_fail(e, "wavefront launch");
     }
@@ -469,17 +475,19 @@ int run_wavefront(rtw_ctx* ctx, rtw_launch L, hipStream_t stream) {
 
 int run_batches(rtw_ctx* ctx, rtw_launch L, uint32_t s0, uint32_t s1, uint32_t batch, hipStream_t stream,
                 bool sync_each, const volatile int32_t* cancel, rtw_progress_fn progress, void* user,
-                uint64_t pixels) {
+                uint64_t pixels, rtw_timer* T = nullptr) {
     const uint64_t total = pixels * (uint64_t)(s1 - s0);
     for (uint32_t s = s0; s < s1; s += batch) {
         if (cancel && *cancel) return fail(RTW_E_CANCELLED, "cancelled");
         L.s0 = s;
         L.s1 = (s1 - s < batch) ? s1 : s + batch;
         if (ctx->variant == 2) {
-            if (int rc = run_wavefront(ctx, L, stream)) return rc;
+            if (int rc = run_wavefront(ctx, L, stream, T)) return rc;
         } else {
             if (ctx->variant == 1) HIP_TRY(hipMemsetAsync(ctx->d_work, 0, 256, stream));
+            RTW_TIME_BEGIN(T, RTW_K_MEGA)
             rtw_launch_render(L, stream, ctx->variant, ctx->grid);
+            RTW_TIME_END(T)
             hipError_t e = hipGetLastError();
             if (e != hipSuccess) return hip_fail(e, "render launch");
         }
@@ -488,6 +496,24 @@ int run_batches(rtw_ctx* ctx, rtw_launch L, uint32_t s0, uint32_t s1, uint32_t b
             if (progress && progress(pixels * (uint64_t)(L.s1 - s0), total, user)) return fail(RTW_E_CANCELLED, "cancelled by progress callback");
         }
     }
+    return RTW_OK;
+}
+
+// Synchronise and sum the timer's events per kernel kind into `out`.
+int harvest_timing(rtw_ctx* ctx, rtw_timer& T, rtw_kernel_timing* out) {
+    HIP_TRY(hipStreamSynchronize(T.stream));
+    std::memset(out, 0, sizeof *out);
+    for (const rtw_timer::rec& r : T.recs) {
+        float ms = 0;
+        HIP_TRY(hipEventElapsedTime(&ms, r.a, r.b));
+        if (r.kind >= 0 && r.kind < RTW_K_COUNT) {
+            out->ms[r.kind] += ms;
+            out->launches[r.kind]++;
+        }
+        ctx->ev_pool.push_back(r.a);
+        ctx->ev_pool.push_back(r.b);
+    }
+    T.recs.clear();
     return RTW_OK;
 }
 
@@ -557,7 +583,13 @@ int rtw_render_device(rtw_ctx* ctx, const rtw_camera* cam, uint32_t pix_begin, u
     L.counters = opts ? reinterpret_cast<unsigned long long*>(opts->counters) : nullptr;
     set_tiles(L);
     uint32_t batch = opts && opts->spp_batch ? opts->spp_batch : auto_batch(pix_end - pix_begin, spp_end - spp_begin);
-    int rc = run_batches(ctx, L, spp_begin, spp_end, batch, s, false, nullptr, nullptr, nullptr, pix_end - pix_begin);
+    rtw_timer T;
+    T.stream = s;
+    T.pool.swap(ctx->ev_pool);
+    rtw_timer* tp = (opts && opts->timing) ? &T : nullptr;
+    int rc = run_batches(ctx, L, spp_begin, spp_end, batch, s, false, nullptr, nullptr, nullptr, pix_end - pix_begin, tp);
+    ctx->ev_pool.swap(T.pool);
+    if (tp && rc == RTW_OK) rc = harvest_timing(ctx, T, opts->timing);
     if (rc) return rc;
     if (!(opts && (opts->flags & RTW_RENDER_NO_SYNC))) HIP_TRY(hipStreamSynchronize(s));
     return RTW_OK;
@@ -600,8 +632,14 @@ int rtw_render_rows_device(rtw_ctx* ctx, const rtw_camera* cam, uint32_t rpb, ui
     L.counters = opts ? reinterpret_cast<unsigned long long*>(opts->counters) : nullptr;
     set_tiles(L);
     uint32_t batch = opts && opts->spp_batch ? opts->spp_batch : auto_batch((uint64_t)rows * cam->image_width, spp_end - spp_begin);
+    rtw_timer T;
+    T.stream = s;
+    T.pool.swap(ctx->ev_pool);
+    rtw_timer* tp = (opts && opts->timing) ? &T : nullptr;
     int rc = run_batches(ctx, L, spp_begin, spp_end, batch, s, false, nullptr, nullptr, nullptr,
-                         (uint64_t)rows * cam->image_width);
+                         (uint64_t)rows * cam->image_width, tp);
+    ctx->ev_pool.swap(T.pool);
+    if (tp && rc == RTW_OK) rc = harvest_timing(ctx, T, opts->timing);
     if (rc) return rc;
     if (!(opts && (opts->flags & RTW_RENDER_NO_SYNC))) HIP_TRY(hipStreamSynchronize(s));
     return RTW_OK;

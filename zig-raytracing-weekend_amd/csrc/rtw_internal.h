@@ -56,6 +56,7 @@ struct rtw_launch {
     uint32_t fast_box;           // 1 = FMA slab test on padded boxes (SAH trees only), 0 = aabb.zig arithmetic
     uint32_t postpone;           // 1 = postpone leaf tests until leaf_min/64 of the walking lanes hold one
     uint32_t leaf_min;           // postponement threshold in 1/64ths of the walking lanes
+    uint32_t refill_min;         // wavefront trace: refill idle lanes once >= refill_min are idle (0 = off)
 };
 
 #define RTW_TILE_W 16
@@ -84,6 +85,41 @@ void rtw_launch_render(const rtw_launch& L, void* stream, int variant, int grid)
 void rtw_launch_debug_rng(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t n, float* d_out, void* stream);
 void rtw_launch_debug_sample(const rtw_launch& L, uint32_t pixel, uint32_t sample, float* d_out, void* stream);
 
+// Per-kernel HIP-event timing of one render call (rtw_render_opts.timing).
+struct rtw_timer {
+    struct rec {
+        int kind;
+        hipEvent_t a, b;
+    };
+    std::vector<rec> recs;
+    std::vector<hipEvent_t> pool;
+    hipStream_t stream = nullptr;
+    int cur = -1;
+    hipEvent_t ev() {
+        hipEvent_t e = nullptr;
+        if (!pool.empty()) {
+            e = pool.back();
+            pool.pop_back();
+        } else {
+            (void)hipEventCreate(&e);
+        }
+        return e;
+    }
+    void begin(int kind) {
+        recs.push_back({kind, ev(), nullptr});
+        (void)hipEventRecord(recs.back().a, stream);
+    }
+    void end() {
+        recs.back().b = ev();
+        (void)hipEventRecord(recs.back().b, stream);
+    }
+};
+// begin/end a timed launch when a timer is attached
+#define RTW_TIME_BEGIN(T, kind) \
+    if (T) (T)->begin(kind);
+#define RTW_TIME_END(T) \
+    if (T) (T)->end();
+
 // box_pad/extent (out, may be null): SAH trees pad every inner box by
 // extent * 2^-19 so the FMA slab test (rtw_kernels.hip box_next) stays conservative.
 int rtw_build_bvh(const rtw_scene_desc& desc, std::vector<rtw_node>& nodes, std::vector<float>& cvec,
@@ -111,6 +147,7 @@ struct rtw_ctx {
     uint64_t wf_max_paths = 1u << 26;  // RTW_WF_PATHS: paths per wavefront batch (x ~90 B)
     uint32_t wf_iters = 6;         // RTW_WF_ITERS: wavefront bounces before the tail kernel
     int n_cu = 256;                // compute units of the device (wavefront grids)
+    std::vector<hipEvent_t> ev_pool;  // recycled timing events
     float box_pad = 0;             // absolute pad baked into the inner boxes (SAH trees), 0 = none
     float extent = 0;              // max |coordinate| over the scene's boxes
 };

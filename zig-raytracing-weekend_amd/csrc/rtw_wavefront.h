@@ -36,6 +36,6 @@ struct rtw_wf {
 // bytes of device state per path (queues extra)
 #define RTW_WF_PATH_BYTES (4 * 16 + 8 + 8)
 
-void rtw_wavefront_batch(const rtw_launch& L, const rtw_wf& W, void* stream, int n_cu);
+void rtw_wavefront_batch(const rtw_launch& L, const rtw_wf& W, void* stream, int n_cu, rtw_timer* T);
 // waves of the largest wavefront grid (bounds the stripe capacity)
 uint32_t rtw_wavefront_max_waves(int n_cu);

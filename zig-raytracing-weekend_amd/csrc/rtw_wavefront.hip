@@ -107,24 +107,60 @@ __device__ __forceinline__ void wf_store_ray(const rtw_wf& W, uint32_t p, const 
     W.ray_d[p] = make_float4(r.d.x, r.d.y, r.d.z, __uint_as_float(depth));
 }
 
+// throughput and radiance of path p: implicit (1, 0) on its first bounce; the
+// radiance is only ever non-zero before the path ends in scenes with emitters
+template <uint32_t FEAT>
+__device__ __forceinline__ void wf_load_state(const rtw_launch& L, const rtw_wf& W, uint32_t p, uint32_t depth,
+                                              f3& thr, f3& acc) {
+    thr = mk(1, 1, 1);
+    acc = mk(0, 0, 0);
+    if (depth != L.max_depth) {
+        const float4 t4 = W.thr[p];
+        thr = mk(t4.x, t4.y, t4.z);
+        if constexpr ((FEAT & RTW_F_LIGHT) != 0) {
+            const float4 l4 = W.ls[p];
+            acc = mk(l4.x, l4.y, l4.z);
+        }
+    }
+}
+
 template <uint32_t FEAT>
 __global__ __launch_bounds__(256) void wf_gen(rtw_launch L, rtw_wf W) {
     const uint32_t p = blockIdx.x * 256u + threadIdx.x;
     if (p >= W.n_paths) return;
     const uint32_t s_local = p / W.n_pix, q = p - s_local * W.n_pix;
     uint32_t pixel, out_idx, x, y;
-    W.ls[p] = make_float4(0, 0, 0, 0);
+    // thr = 1 and radiance = 0 are implicit while depth == max_depth (not stored)
     if (wf_pixel(L, W, q, pixel, out_idx, x, y) && L.max_depth > 0) {
         const uint32_t s = L.s0 + s_local;
         rtw_rng rng;
         rng.s = rtw_mix64(L.key0 ^ (((uint64_t)pixel << 32) | (uint64_t)s));
         const Ray r = get_ray(L, x + L.pixel_offset, y + L.pixel_offset, rng);  // camera.zig:100-101
         wf_store_ray(W, p, r, L.max_depth);
-        W.thr[p] = make_float4(1, 1, 1, 0);
         W.rng[p] = rng.s;
     } else {
         W.ray_d[p] = make_float4(0, 0, 0, 0);  // depth 0: no path (padding / outside the range)
+        W.ls[p] = make_float4(0, 0, 0, 0);     // rayColor(r, 0) = 0
     }
+}
+
+// m-th path of this wave's list at iteration it (see WfIter); false past the end
+// or for padding.  `end` (wave-uniform) is set when m is past the list.
+__device__ __forceinline__ bool wf_nth(const rtw_wf& W, uint32_t it, uint32_t m, uint32_t& p, bool& end) {
+    const uint32_t w = wf_wave(), nw = wf_nwaves();
+    if (it == 0) {
+        const uint32_t chunk = w + (m >> 6) * nw;
+        p = (chunk << 6) | (m & 63u);
+        end = chunk >= ((W.n_paths + 63u) >> 6);
+        return p < W.n_paths;
+    }
+    const uint32_t s = w % RTW_WF_STRIPES, R = nw / RTW_WF_STRIPES;
+    const uint32_t k = ((((m >> 6) * R) + w / RTW_WF_STRIPES) << 6) | (m & 63u);
+    const uint32_t n = W.len[it & 1u][s * RTW_WF_LEN_STRIDE];
+    end = (k & ~63u) >= n;
+    if (k >= n) return false;
+    p = W.queue[it & 1u][(size_t)s * W.stripe_cap + k];
+    return true;
 }
 
 // trace: closest hit per queued ray (no shading state in registers)
@@ -134,6 +170,59 @@ __global__ __launch_bounds__(256) void wf_trace(rtw_launch L, rtw_wf W, uint32_t
     if (blockIdx.x == 0) W.len[(it + 1u) & 1u][threadIdx.x * RTW_WF_LEN_STRIDE] = 0;
     static_assert(RTW_WF_STRIPES == 256, "one block zeroes the stripe counters");
     Counters cnt;
+    if (L.refill_min) {
+        // per-lane refill: a lane whose walk is done takes the wave's next ray
+        // once refill_min lanes are idle (the refill stalls the wave on the loads)
+        const uint32_t lane = __lane_id();
+        const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+        const bool fast = L.fast_box != 0;
+        uint32_t cursor = 0, p = 0, ti = 0;
+        bool active = false, exhausted = false;
+        Ray r;
+        r.o = r.d = mk(0, 0, 0);
+        r.time = 0;
+        RayTrav rt = ray_trav(r, false);
+        float closest = kInf;
+        int hit = -1;
+        for (;;) {
+            const uint64_t idle = __ballot(!active);
+            const uint32_t n_idle = (uint32_t)__popcll(idle);
+            if (!exhausted && (n_idle >= L.refill_min || n_idle == 64)) {
+                const uint32_t m = cursor + (uint32_t)__popcll(idle & lt);
+                cursor += n_idle;
+                bool end = false;
+                uint32_t q = 0;
+                const bool ok = wf_nth(W, it, m, q, end);
+                exhausted = __ballot(end && !active) == idle;  // every idle lane ran past the list
+                if (!active && ok) {
+                    uint32_t depth;
+                    r = wf_load_ray(W, q, depth);
+                    if (depth) {
+                        p = q;
+                        rt = ray_trav(r, fast);
+                        ti = 0;
+                        closest = kInf;
+                        hit = -1;
+                        active = true;
+                        cnt.rays++;
+                    }
+                }
+            }
+            if (!__ballot(active)) {
+                if (exhausted) break;
+                continue;
+            }
+            if (active) {
+                ti = trav_step<FEAT>(L.nodes, L, r, rt, ti, closest, hit, cnt);
+                if (ti >= L.n_nodes) {
+                    W.hit[p] = make_float2(closest, __int_as_float(hit));
+                    active = false;
+                }
+            }
+        }
+        flush_counters(L, cnt, 0);
+        return;
+    }
     for (WfIter e(W, it); e.more(); e.next()) {
         uint32_t p;
         if (e.get(W, p)) {
@@ -162,8 +251,8 @@ __global__ __launch_bounds__(256) void wf_shade(rtw_launch L, rtw_wf W, uint32_t
             if (depth) {
                 const float2 h = W.hit[p];
                 const int hit = __float_as_int(h.y);
-                const float4 t4 = W.thr[p], l4 = W.ls[p];
-                f3 thr = mk(t4.x, t4.y, t4.z), acc = mk(l4.x, l4.y, l4.z);
+                f3 thr, acc;
+                wf_load_state<FEAT>(L, W, p, depth, thr, acc);
                 if (hit < 0) {
                     acc = acc + thr * background(L, r);
                 } else {
@@ -179,7 +268,8 @@ __global__ __launch_bounds__(256) void wf_shade(rtw_launch L, rtw_wf W, uint32_t
                         push = true;
                     }
                 }
-                W.ls[p] = make_float4(acc.x, acc.y, acc.z, 0);
+                // without emitters the radiance stays 0 until the path ends
+                if (!push || (FEAT & RTW_F_LIGHT) != 0) W.ls[p] = make_float4(acc.x, acc.y, acc.z, 0);
             }
         }
         wf_push(W, it, push, p);
@@ -212,9 +302,7 @@ __global__ __launch_bounds__(256) void wf_tail(rtw_launch L, rtw_wf W, uint32_t 
             if (!active && k < n) {
                 p = q[k];
                 r = wf_load_ray(W, p, depth);
-                const float4 t4 = W.thr[p], l4 = W.ls[p];
-                thr = mk(t4.x, t4.y, t4.z);
-                acc = mk(l4.x, l4.y, l4.z);
+                wf_load_state<FEAT>(L, W, p, depth, thr, acc);
                 rng.s = W.rng[p];
                 active = true;
             }
@@ -222,6 +310,7 @@ __global__ __launch_bounds__(256) void wf_tail(rtw_launch L, rtw_wf W, uint32_t 
         if (!__ballot(active)) break;
         if (active) {  // one more iteration of rayColor
             cnt.rays++;
+            cnt.tail_rays++;
             float t;
             const int hit = traverse<FEAT>(L.nodes, L, r, t, cnt);
             bool done = true;
@@ -295,16 +384,28 @@ const WfGrids<FEAT>& wf_grids(int n_cu) {
 }
 
 template <uint32_t FEAT>
-void wf_run(const rtw_launch& L, const rtw_wf& W, hipStream_t st, int n_cu) {
+void wf_run(const rtw_launch& L, const rtw_wf& W, hipStream_t st, int n_cu, rtw_timer* T) {
     const WfGrids<FEAT>& g = wf_grids<FEAT>(n_cu);
+    RTW_TIME_BEGIN(T, RTW_K_GEN)
     hipLaunchKernelGGL(wf_gen<FEAT>, dim3((W.n_paths + 255u) / 256u), dim3(256), 0, st, L, W);
+    RTW_TIME_END(T)
     const uint32_t iters = L.max_depth < W.iters ? L.max_depth : W.iters;
     for (uint32_t it = 0; it < iters; it++) {
+        RTW_TIME_BEGIN(T, RTW_K_TRACE)
         hipLaunchKernelGGL(wf_trace<FEAT>, dim3(g.trace), dim3(256), 0, st, L, W, it);
+        RTW_TIME_END(T)
+        RTW_TIME_BEGIN(T, RTW_K_SHADE)
         hipLaunchKernelGGL(wf_shade<FEAT>, dim3(g.shade), dim3(256), 0, st, L, W, it);
+        RTW_TIME_END(T)
     }
-    if (iters < L.max_depth) hipLaunchKernelGGL(wf_tail<FEAT>, dim3(g.tail), dim3(256), 0, st, L, W, iters);
+    if (iters < L.max_depth) {
+        RTW_TIME_BEGIN(T, RTW_K_TAIL)
+        hipLaunchKernelGGL(wf_tail<FEAT>, dim3(g.tail), dim3(256), 0, st, L, W, iters);
+        RTW_TIME_END(T)
+    }
+    RTW_TIME_BEGIN(T, RTW_K_REDUCE)
     hipLaunchKernelGGL(wf_reduce, dim3((W.n_pix + 255u) / 256u), dim3(256), 0, st, L, W);
+    RTW_TIME_END(T)
 }
 
 uint32_t wf_pick_feat(uint32_t f) {
@@ -314,12 +415,12 @@ uint32_t wf_pick_feat(uint32_t f) {
 
 }  // namespace
 
-void rtw_wavefront_batch(const rtw_launch& L, const rtw_wf& W, void* stream, int n_cu) {
+void rtw_wavefront_batch(const rtw_launch& L, const rtw_wf& W, void* stream, int n_cu, rtw_timer* T) {
     hipStream_t st = (hipStream_t)stream;
     switch (wf_pick_feat(L.feat)) {
-    case 0u: wf_run<0u>(L, W, st, n_cu); break;
-    case RTW_F_CHECKER: wf_run<RTW_F_CHECKER>(L, W, st, n_cu); break;
-    default: wf_run<RTW_F_ALL>(L, W, st, n_cu); break;
+    case 0u: wf_run<0u>(L, W, st, n_cu, T); break;
+    case RTW_F_CHECKER: wf_run<RTW_F_CHECKER>(L, W, st, n_cu, T); break;
+    default: wf_run<RTW_F_ALL>(L, W, st, n_cu, T); break;
     }
 }
 

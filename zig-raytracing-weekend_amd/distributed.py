@@ -70,11 +70,13 @@ class ShardedRender:
         self.rows = len(shard_rows(self.H, rows_per_block, world_size, rank))
 
     def render(self, spp_begin: int, spp_end: int, seed: int = 0, stream=None, spp_batch: int = 0,
-               counters: Optional[int] = None, sync: bool = False) -> None:
-        """Enqueue this rank's rows x samples [spp_begin, spp_end) on `stream`."""
+               counters: Optional[int] = None, sync: bool = False, timing=None) -> None:
+        """Enqueue this rank's rows x samples [spp_begin, spp_end) on `stream`.
+        timing: optional _abi.RtwKernelTiming filled with per-kernel device time
+        (the call then synchronises the stream)."""
         self.tile.zero_()
         flags = 0 if sync else _abi.RTW_RENDER_NO_SYNC
-        opts = _abi.RtwRenderOpts(spp_batch or (spp_end - spp_begin), flags, counters)
+        opts = _abi.RtwRenderOpts(spp_batch, flags, counters, C.pointer(timing) if timing is not None else None)
         rc = _abi.lib().rtw_render_rows_device(self.world.handle, C.byref(self.cam.derived), self.rpb,
                                                self.world_size, self.rank, spp_begin, spp_end, seed,
                                                self.tile.data_ptr(),
