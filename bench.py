@@ -153,6 +153,7 @@ def main():
     dom_bytes_launch = dom_bytes_step * args.steps / max(1, kcalls[dom])
     achieved = dom_bytes_launch / dom_launch_s / 1e9 if dom_launch_s > 0 else 0.0
     path_achieved = alg_bytes / render_s / 1e9
+    traffic, traffic_src = pmc_traffic(args, {"trace": "wf_trace", "tail": "wf_tail", "mega": "render_"}.get(dom, dom))
 
     cpu = None
     if rank == 0 and world_size == 1 and not args.no_cpu_baseline:
@@ -178,7 +179,8 @@ def main():
                        "bvh_depth": stats["depth"], "parallelism": f"row-interleaved tiles x{world_size}"
                        + (" + RCCL gather" if distributed else ""), "rows_per_block": ROWS_PER_BLOCK},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "traffic_source": traffic_src,
                          "kernel": {"trace": "wf_trace", "tail": "wf_tail", "mega": "render_persistent_v1"}.get(dom, dom),
                          "avg_launch_ms": round(dom_launch_s * 1e3, 4),
                          "launches_per_step": kcalls[dom] / args.steps,
@@ -202,6 +204,20 @@ def main():
     world.close()
     if distributed:
         dist.destroy_process_group()
+
+
+def pmc_traffic(args, kernel_prefix):
+    """HBM bytes per launch of the dominant kernel from the committed PMC pass
+    (tools/pmc_traffic.sh -> profiles/pmc_traffic_<config>_<bvh>.json; FETCH_SIZE x2 + WRITE_SIZE,
+    MI355X_MICROARCH.md § HBM).  PMC counters cannot be read inside the timed run."""
+    f = os.path.join(REPO, "profiles", f"pmc_traffic_{args.config}_{args.bvh}.json")
+    if args.spp or not os.path.exists(f):
+        return None, None
+    data = json.load(open(f))
+    for name, e in data.items():
+        if name.startswith(kernel_prefix):
+            return round(e["traffic_bytes"]), os.path.relpath(f, REPO)
+    return None, None
 
 
 def cpu_baseline(pkg, arr, cam, args):
