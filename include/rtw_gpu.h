@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define RTW_ABI_VERSION 1
+#define RTW_ABI_VERSION 2
 
 enum rtw_status {
     RTW_OK = 0,
@@ -104,6 +104,62 @@ typedef struct rtw_perlin {
     uint16_t perm_x[256], perm_y[256], perm_z[256];
 } rtw_perlin;
 
+/* Quad.init (src/objects.zig:193-210): corner q, edges u, v.  The library derives
+ * normal = unitVector(cross(u, v)), d = dot(normal, q), w = n / dot(n, n) and the
+ * box fromPoints(q, q + u + v).pad() exactly as Quad.init does.  48 bytes. */
+typedef struct rtw_quad {
+    float q[3];
+    uint32_t material;
+    float u[3];
+    uint32_t _p0;
+    float v[3];
+    uint32_t _p1;
+} rtw_quad;
+
+/* A Hittable (src/objects.zig:39-48) by kind + index into its array. */
+enum rtw_object_kind {
+    RTW_OBJ_SPHERE = 0,        /* spheres[index] */
+    RTW_OBJ_QUAD = 1,          /* quads[index] */
+    RTW_OBJ_INSTANCE = 2,      /* instances[index] */
+    RTW_OBJ_MEDIUM = 3         /* media[index] */
+};
+typedef struct rtw_object {
+    uint32_t kind;
+    uint32_t index;
+} rtw_object;
+
+/* Translate / RotateY (src/objects.zig:292-443). */
+enum rtw_transform_kind {
+    RTW_XF_TRANSLATE = 0,      /* v = offset */
+    RTW_XF_ROTATE_Y = 1        /* v[0] = angle in degrees (sin/cos as RotateY.init) */
+};
+typedef struct rtw_transform {
+    uint32_t kind;
+    float v[3];
+} rtw_transform;
+
+#define RTW_MAX_XF 3
+enum { RTW_INST_LIST = 1u };   /* rtw_instance.flags: the members form a HittableList (its box
+                                  starts from the zero Aabb{}, objects.zig:264-279); else one primitive */
+/* A HittableList (createBox, src/objects.zig:264-290, 510-532) of members[first ..
+ * first + count) -- spheres or quads -- wrapped in xf[0] (innermost) .. xf[n_xf-1]
+ * (outermost), e.g. Translate(RotateY(createBox(...))) = {ROTATE_Y, TRANSLATE}.  64 bytes. */
+typedef struct rtw_instance {
+    uint32_t first, count, n_xf, flags;
+    rtw_transform xf[RTW_MAX_XF];
+} rtw_instance;
+
+/* ConstantMedium.initFromColor/initFromTexture (src/objects.zig:445-460): boundary is
+ * a sphere, quad or instance; material = the Isotropic phase function
+ * (RTW_MAT_ISOTROPIC).  The one random draw of ConstantMedium.hit (objects.zig:484)
+ * is keyed by (path RNG state at the traversal, medium index), not taken from the
+ * path's sequential stream, so the result does not depend on the BVH topology. */
+typedef struct rtw_medium {
+    rtw_object boundary;
+    float density;
+    uint32_t material;
+} rtw_medium;
+
 enum rtw_bvh_mode {
     RTW_BVH_REFERENCE = 0,     /* BVHTree.constructTree (src/bvh.zig:43-71): random axis from the
                                   seeded build stream, std.sort.heap by box min, median split */
@@ -120,6 +176,13 @@ typedef struct rtw_scene_desc {
     uint64_t bvh_seed;
     uint32_t bvh_mode;
     float order_dir[3];        /* RTW_BVH_SAH child order hint (e.g. camera forward); 0 = (0,-1,0) */
+    /* ABI 2: the rest of the Hittable union.  objects = world_objects in order (the
+     * BVH leaves); NULL/0 = every sphere in order (ABI 1 behaviour). */
+    const rtw_quad* quads;         uint32_t n_quads;
+    const rtw_object* members;     uint32_t n_members;     /* instance list entries: spheres/quads */
+    const rtw_instance* instances; uint32_t n_instances;
+    const rtw_medium* media;       uint32_t n_media;
+    const rtw_object* objects;     uint32_t n_objects;
 } rtw_scene_desc;
 
 /* ---------------------------------------------------------------------------

@@ -25,6 +25,12 @@ TEXTURE_DT = np.dtype([("kind", "<u4"), ("image", "<u4"), ("perlin", "<u4"), ("s
                        ("even", "<f4", 3), ("_p0", "<f4"), ("odd", "<f4", 3), ("_p1", "<f4")])
 PERLIN_DT = np.dtype([("ranvec", "<f4", (256, 3)), ("perm_x", "<u2", 256), ("perm_y", "<u2", 256),
                       ("perm_z", "<u2", 256)])
+QUAD_DT = np.dtype([("q", "<f4", 3), ("material", "<u4"), ("u", "<f4", 3), ("_p0", "<u4"), ("v", "<f4", 3),
+                    ("_p1", "<u4")])
+OBJECT_DT = np.dtype([("kind", "<u4"), ("index", "<u4")])
+INSTANCE_DT = np.dtype([("first", "<u4"), ("count", "<u4"), ("n_xf", "<u4"), ("flags", "<u4"),
+                        ("xf", np.dtype([("kind", "<u4"), ("v", "<f4", 3)]), 3)])
+MEDIUM_DT = np.dtype([("boundary", OBJECT_DT), ("density", "<f4"), ("material", "<u4")])
 
 F3 = C.c_float * 3
 
@@ -38,7 +44,11 @@ class OSceneDesc(C.Structure):
     _fields_ = [("spheres", C.c_void_p), ("n_spheres", C.c_uint32), ("materials", C.c_void_p),
                 ("n_materials", C.c_uint32), ("textures", C.c_void_p), ("n_textures", C.c_uint32),
                 ("images", C.c_void_p), ("n_images", C.c_uint32), ("perlins", C.c_void_p),
-                ("n_perlins", C.c_uint32), ("bvh_seed", C.c_uint64)]
+                ("n_perlins", C.c_uint32), ("bvh_seed", C.c_uint64), ("bvh_mode", C.c_uint32),
+                ("order_dir", C.c_float * 3), ("quads", C.c_void_p), ("n_quads", C.c_uint32),
+                ("members", C.c_void_p), ("n_members", C.c_uint32), ("instances", C.c_void_p),
+                ("n_instances", C.c_uint32), ("media", C.c_void_p), ("n_media", C.c_uint32),
+                ("objects", C.c_void_p), ("n_objects", C.c_uint32)]
 
 
 class OCameraParams(C.Structure):
@@ -87,6 +97,8 @@ def lib() -> C.CDLL:
             "oracle_reflectance": (C.c_float, [C.c_float, C.c_float]),
             "oracle_sphere_hit": (C.c_int, [vp, vp, vp, C.c_float, C.c_float, C.c_float, vp]),
             "oracle_texture_value": (None, [vp, u32, C.c_float, C.c_float, vp, vp]),
+            "oracle_quad_hit": (C.c_int, [vp, vp, vp, C.c_float, C.c_float, vp]),
+            "oracle_medium_draw": (C.c_float, [u64, u32]),
             "oracle_perlin_noise": (C.c_float, [vp, vp]),
             "oracle_perlin_turb": (C.c_float, [vp, vp, C.c_int]),
             "oracle_gamma2": (None, [vp, vp]),
@@ -136,10 +148,25 @@ def camera(aspect_ratio=16.0 / 9.0, image_width=800, image_height=0, samples_per
 
 # ---------------------------------------------------------------- world
 class World:
-    """A BVHTree (reference topology) over the wire-format spheres."""
+    """A BVHTree (reference topology) over the wire-format world objects."""
+
+    @staticmethod
+    def from_arrays(a, bvh_seed: Optional[int] = None) -> "World":
+        """From a product SceneArrays-like object (plain numpy records; no product import)."""
+        return World(a.spheres, a.materials, a.textures, a.perlins, [im.rgba for im in a.images],
+                     a.bvh_seed if bvh_seed is None else bvh_seed, a.quads, a.members, a.instances, a.media,
+                     a.objects)
 
     def __init__(self, spheres: np.ndarray, materials: np.ndarray, textures: np.ndarray,
-                 perlins: Optional[np.ndarray] = None, images: Sequence[np.ndarray] = (), bvh_seed: int = 0):
+                 perlins: Optional[np.ndarray] = None, images: Sequence[np.ndarray] = (), bvh_seed: int = 0,
+                 quads: Optional[np.ndarray] = None, members: Optional[np.ndarray] = None,
+                 instances: Optional[np.ndarray] = None, media: Optional[np.ndarray] = None,
+                 objects: Optional[np.ndarray] = None):
+        def rec(a, dt):
+            return np.ascontiguousarray(a if a is not None else np.zeros(0, dt)).view(dt)
+        self.quads, self.members = rec(quads, QUAD_DT), rec(members, OBJECT_DT)
+        self.instances, self.media = rec(instances, INSTANCE_DT), rec(media, MEDIUM_DT)
+        self.objects = None if objects is None else rec(objects, OBJECT_DT)
         self.spheres = np.ascontiguousarray(spheres).view(SPHERE_DT)
         self.materials = np.ascontiguousarray(materials).view(MATERIAL_DT)
         self.textures = np.ascontiguousarray(textures).view(TEXTURE_DT)
@@ -157,15 +184,24 @@ class World:
         d.images, d.n_images = (C.addressof(self._imgs) if self.images else 0), len(self.images)
         d.perlins, d.n_perlins = _p(self.perlins), len(self.perlins)
         d.bvh_seed = bvh_seed
+        d.quads, d.n_quads = _p(self.quads), len(self.quads)
+        d.members, d.n_members = _p(self.members), len(self.members)
+        d.instances, d.n_instances = _p(self.instances), len(self.instances)
+        d.media, d.n_media = _p(self.media), len(self.media)
+        if self.objects is not None:
+            d.objects, d.n_objects = _p(self.objects), len(self.objects)
         self.desc = d
         self.handle = lib().oracle_world_create(C.byref(d))
         if not self.handle:
             raise ValueError("oracle_world_create failed")
 
     def __del__(self):
-        if getattr(self, "handle", None):
-            lib().oracle_world_destroy(self.handle)
-            self.handle = None
+        try:
+            if getattr(self, "handle", None):
+                lib().oracle_world_destroy(self.handle)
+                self.handle = None
+        except Exception:  # interpreter shutdown
+            pass
 
     def stats(self):
         o = np.zeros(4, np.uint32)

@@ -594,17 +594,113 @@ static v3 emitted(const o_scene_desc* d, uint32_t mat, float u, float v, v3 p) {
 }
 
 /* ------------------------------------------------------------------------- */
-/* bvh.zig                                                                   */
+/* objects.zig: Quad, HittableList, Translate, RotateY, ConstantMedium       */
 /* ------------------------------------------------------------------------- */
+/* Interval.contains (interval.zig:8-10) */
+static inline int contains(interval_t i, float x) { return i.min <= x && x <= i.max; }
+
+/* Aabb.pad (aabb.zig:36-43), Interval.expand (interval.zig:26-29) */
+static aabb_t aabb_pad(aabb_t b) {
+    const float delta = 0.0001f;
+    for (int k = 0; k < 3; k++) {
+        if (!(b.ax[k].max - b.ax[k].min >= delta)) {
+            const float padding = delta / 2.0f;
+            b.ax[k].min = b.ax[k].min - padding;
+            b.ax[k].max = b.ax[k].max + padding;
+        }
+    }
+    return b;
+}
+
+typedef struct {
+    v3 q, u, v, normal, w;
+    float d;
+    uint32_t mat;
+    aabb_t bbox;
+} quad_t;
+
+static void quad_from_desc(const o_quad* o, quad_t* q) {      /* objects.zig:201-210 */
+    q->q = vload(o->q); q->u = vload(o->u); q->v = vload(o->v);
+    q->mat = o->material;
+    v3 n = cross(q->u, q->v);
+    q->normal = unit_vector(n);
+    q->d = dot(q->normal, q->q);
+    q->w = vdiv(n, splat(dot(n, n)));
+    q->bbox = aabb_pad(aabb_from_points(q->q, add(add(q->q, q->u), q->v)));
+}
+
+/* objects.zig:222-255 */
+static int quad_hit(const quad_t* q, const ray3* r, interval_t ray_t, hit_record_t* rec) {
+    float denom = dot(q->normal, r->direction);
+    if (fabsf(denom) < 1e-8f) return 0;
+    float t = (q->d - dot(q->normal, r->origin)) / denom;
+    if (!contains(ray_t, t)) return 0;
+    v3 intersection = ray_at(r, t);
+    v3 planar = sub(intersection, q->q);
+    float alpha = dot(q->w, cross(planar, q->v));
+    float beta = dot(q->w, cross(q->u, planar));
+    if ((alpha < 0) || (1 < alpha) || (beta < 0) || (1 < beta)) return 0;   /* isInterior :212-220 */
+    rec->u = alpha;
+    rec->v = beta;
+    rec->t = t;
+    rec->p = intersection;
+    rec->mat = q->mat;
+    set_face_normal(rec, r, q->normal);
+    return 1;
+}
+
+int oracle_quad_hit(const o_quad* o, const float origin[3], const float dir[3], float tmin, float tmax,
+                    float out[10]) {
+    quad_t q; quad_from_desc(o, &q);
+    ray3 r = {vload(origin), vload(dir), 0};
+    interval_t it = {tmin, tmax};
+    hit_record_t rec;
+    if (!quad_hit(&q, &r, it, &rec)) return 0;
+    out[0] = rec.t;
+    for (int i = 0; i < 3; i++) { out[1 + i] = rec.p.e[i]; out[4 + i] = rec.normal.e[i]; }
+    out[7] = (float)rec.front_face; out[8] = rec.u; out[9] = rec.v;
+    return 1;
+}
+
+typedef struct {
+    uint32_t kind;
+    v3 offset;                   /* translate */
+    float sin_theta, cos_theta;  /* rotate_y */
+} xf_t;
+
+typedef struct {
+    uint32_t first, count, n_xf;
+    xf_t xf[O_MAX_XF];
+    aabb_t bbox;
+} inst_t;
+
+typedef struct {
+    o_object boundary;
+    float neg_inv_density;
+    uint32_t mat;
+    aabb_t bbox;
+} medium_t;
+
+/* BVH leaf = one world object */
+typedef struct {
+    uint32_t kind, index;
+    uint32_t orig;             /* position in world_objects (dump/tests only) */
+    aabb_t bbox;
+} object_t;
+
 typedef struct bvh_node {
-    const sphere_t* leaf;
+    const object_t* leaf;
     const struct bvh_node *left, *right;
     aabb_t bbox;
 } bvh_node_t;
 
 typedef struct world {
     o_scene_desc desc;
-    sphere_t* objects;         /* world_objects.items (reordered in place by the build) */
+    sphere_t* spheres;         /* every sphere record (world objects and list members) */
+    quad_t* quads;
+    inst_t* insts;
+    medium_t* media;
+    object_t* objects;         /* world_objects.items (reordered in place by the build) */
     uint32_t n;
     bvh_node_t* pool;
     uint32_t pool_used, pool_cap;
@@ -613,16 +709,178 @@ typedef struct world {
     rng_t build_rng;
 } world_t;
 
+/* RotateY.init (objects.zig:340-388): sin/cos and the rotated box */
+static aabb_t rotate_y_box(aabb_t bbox, float sin_theta, float cos_theta) {
+    const float inf = INF_F;
+    v3 mn = V(inf, inf, inf), mx = V(-inf, -inf, -inf);
+    for (int i = 0; i < 2; i++)
+        for (int j = 0; j < 2; j++)
+            for (int k = 0; k < 2; k++) {
+                float i_f = (float)i, j_f = (float)j, k_f = (float)k;
+                float x = i_f * bbox.ax[0].max + (1 - i_f) * bbox.ax[0].min;
+                float y = j_f * bbox.ax[1].max + (1 - j_f) * bbox.ax[1].min;
+                float z = k_f * bbox.ax[2].max + (1 - k_f) * bbox.ax[2].min;
+                float newx = cos_theta * x + sin_theta * z;
+                float newz = -sin_theta * x + cos_theta * z;
+                v3 tester = V(newx, y, newz);
+                for (int c = 0; c < 3; c++) {
+                    mn.e[c] = fminf(mn.e[c], tester.e[c]);
+                    mx.e[c] = fmaxf(mx.e[c], tester.e[c]);
+                }
+            }
+    return aabb_from_points(mn, mx);
+}
+
+static aabb_t prim_box(const world_t* w, o_object ref) {
+    return ref.kind == O_OBJ_SPHERE ? w->spheres[ref.index].bbox : w->quads[ref.index].bbox;
+}
+
+static void inst_from_desc(const world_t* w, const o_instance* o, inst_t* in) {
+    in->first = o->first; in->count = o->count; in->n_xf = o->n_xf;
+    aabb_t b;
+    if (o->flags & O_INST_LIST) {                          /* HittableList.add (objects.zig:273-276) */
+        memset(&b, 0, sizeof b);                           /* Aabb{} = [0,0]^3 */
+        for (uint32_t m = 0; m < o->count; m++) b = aabb_from_boxes(b, prim_box(w, w->desc.members[o->first + m]));
+    } else {
+        b = prim_box(w, w->desc.members[o->first]);
+    }
+    for (uint32_t k = 0; k < o->n_xf; k++) {
+        xf_t* x = &in->xf[k];
+        x->kind = o->xf[k].kind;
+        if (x->kind == O_XF_TRANSLATE) {                   /* Translate.init (objects.zig:299-304) */
+            x->offset = vload(o->xf[k].v);
+            for (int c = 0; c < 3; c++) {                  /* Aabb.add / Interval.add */
+                b.ax[c].min = b.ax[c].min + x->offset.e[c];
+                b.ax[c].max = b.ax[c].max + x->offset.e[c];
+            }
+        } else {
+            float radians = o->xf[k].v[0] * PI_F / 180.0f; /* degreesToRadians (rtweekend.zig:10-12) */
+            x->sin_theta = sinf(radians);
+            x->cos_theta = cosf(radians);
+            b = rotate_y_box(b, x->sin_theta, x->cos_theta);
+        }
+    }
+    in->bbox = b;
+}
+
+static int object_hit(const world_t* w, o_object ref, const ray3* r, interval_t ray_t, hit_record_t* rec,
+                      const rng_t* rng);
+
+/* HittableList.hit (objects.zig:281-289) */
+static int list_hit(const world_t* w, const inst_t* in, const ray3* r, interval_t ray_t, hit_record_t* rec) {
+    int any = 0;
+    float closest_so_far = ray_t.max;
+    for (uint32_t m = 0; m < in->count; m++) {
+        hit_record_t h;
+        interval_t it = {ray_t.min, closest_so_far};
+        if (object_hit(w, w->desc.members[in->first + m], r, it, &h, NULL)) {
+            closest_so_far = h.t;
+            *rec = h;
+            any = 1;
+        }
+    }
+    return any;
+}
+
+/* the transform chain xf[k] .. xf[0] around the list (Translate.hit :314-330, RotateY.hit :398-442) */
+static int inst_hit_k(const world_t* w, const inst_t* in, int k, const ray3* r, interval_t ray_t,
+                      hit_record_t* rec) {
+    if (k < 0) return list_hit(w, in, r, ray_t, rec);
+    const xf_t* x = &in->xf[k];
+    if (x->kind == O_XF_TRANSLATE) {
+        ray3 moved = {sub(r->origin, x->offset), r->direction, r->time};
+        if (!inst_hit_k(w, in, k - 1, &moved, ray_t, rec)) return 0;
+        rec->p = add(rec->p, x->offset);
+        return 1;
+    }
+    const float s = x->sin_theta, c = x->cos_theta;
+    ray3 rot = *r;
+    rot.origin.e[0] = c * r->origin.e[0] - s * r->origin.e[2];
+    rot.origin.e[2] = s * r->origin.e[0] + c * r->origin.e[2];
+    rot.direction.e[0] = c * r->direction.e[0] - s * r->direction.e[2];
+    rot.direction.e[2] = s * r->direction.e[0] + c * r->direction.e[2];
+    if (!inst_hit_k(w, in, k - 1, &rot, ray_t, rec)) return 0;
+    v3 p = rec->p, n = rec->normal;
+    p.e[0] = c * rec->p.e[0] + s * rec->p.e[2];
+    p.e[2] = -s * rec->p.e[0] + c * rec->p.e[2];
+    n.e[0] = c * rec->normal.e[0] + s * rec->normal.e[2];
+    n.e[2] = -s * rec->normal.e[0] + c * rec->normal.e[2];
+    rec->p = p;
+    rec->normal = n;
+    return 1;
+}
+
+/* ConstantMedium's one random draw, keyed: u = float(mix64(state ^ K*(medium+1))) */
+float oracle_medium_draw(uint64_t path_state, uint32_t medium) {
+    rng_t r;
+    r.s = oracle_mix64(path_state ^ (0xD1B54A32D192ED03ull * (uint64_t)(medium + 1)));
+    return rnd(&r);
+}
+
+/* ConstantMedium.hit (objects.zig:470-507) */
+static int medium_hit(const world_t* w, uint32_t mi, const ray3* r, interval_t ray_t, hit_record_t* rec,
+                      const rng_t* rng) {
+    const medium_t* m = &w->media[mi];
+    const interval_t universe = {-INF_F, INF_F};
+    hit_record_t rec_1, rec_2;
+    if (!object_hit(w, m->boundary, r, universe, &rec_1, NULL)) return 0;
+    interval_t second = {rec_1.t + 0.0001f, INF_F};
+    if (!object_hit(w, m->boundary, r, second, &rec_2, NULL)) return 0;
+    if (rec_1.t < ray_t.min) rec_1.t = ray_t.min;
+    if (rec_2.t > ray_t.max) rec_2.t = ray_t.max;
+    if (rec_1.t >= rec_2.t) return 0;
+    if (rec_1.t < 0) rec_1.t = 0;
+    float ray_length = vlength(r->direction);
+    float distance_inside_boundary = (rec_2.t - rec_1.t) * ray_length;
+    float hit_distance = m->neg_inv_density * logf(oracle_medium_draw(rng ? rng->s : 0, mi));
+    if (hit_distance > distance_inside_boundary) return 0;
+    rec->t = rec_1.t + hit_distance / ray_length;
+    rec->p = ray_at(r, rec->t);
+    rec->normal = V(1, 0, 0);          /* arbitrary */
+    rec->front_face = 1;               /* also arbitrary */
+    rec->mat = m->mat;
+    rec->u = 0;
+    rec->v = 0;
+    return 1;
+}
+
+/* Hittable.hit dispatch (objects.zig:49-53) */
+static int object_hit(const world_t* w, o_object ref, const ray3* r, interval_t ray_t, hit_record_t* rec,
+                      const rng_t* rng) {
+    switch (ref.kind) {
+    case O_OBJ_SPHERE: return sphere_hit(&w->spheres[ref.index], r, ray_t, rec);
+    case O_OBJ_QUAD: return quad_hit(&w->quads[ref.index], r, ray_t, rec);
+    case O_OBJ_INSTANCE: {
+        const inst_t* in = &w->insts[ref.index];
+        return inst_hit_k(w, in, (int)in->n_xf - 1, r, ray_t, rec);
+    }
+    case O_OBJ_MEDIUM: return medium_hit(w, ref.index, r, ray_t, rec, rng);
+    }
+    return 0;
+}
+
+static aabb_t object_box(const world_t* w, o_object ref) {
+    switch (ref.kind) {
+    case O_OBJ_SPHERE: return w->spheres[ref.index].bbox;
+    case O_OBJ_QUAD: return w->quads[ref.index].bbox;
+    case O_OBJ_INSTANCE: return w->insts[ref.index].bbox;
+    default: return w->media[ref.index].bbox;
+    }
+}
+
+/* ------------------------------------------------------------------------- */
+/* bvh.zig                                                                   */
+/* ------------------------------------------------------------------------- */
 static bvh_node_t* make_node(world_t* w) { return &w->pool[w->pool_used++]; }
 
 /* bvh.zig:95-103 */
-static int box_comparator(uint32_t axis, const sphere_t* a, const sphere_t* b) {
+static int box_comparator(uint32_t axis, const object_t* a, const object_t* b) {
     uint32_t ax = axis == 0 ? 0 : (axis == 1 ? 1 : 2);
     return a->bbox.ax[ax].min < b->bbox.ax[ax].min;
 }
 
 /* Zig std.sort.heap (0.12): heapContext + siftDown */
-static void sift_down(sphere_t* it, size_t a, size_t target, size_t b, uint32_t axis) {
+static void sift_down(object_t* it, size_t a, size_t target, size_t b, uint32_t axis) {
     size_t cur = target;
     for (;;) {
         size_t child = (cur - a) * 2 + a + 1;
@@ -630,22 +888,22 @@ static void sift_down(sphere_t* it, size_t a, size_t target, size_t b, uint32_t 
         size_t next_child = child + 1;
         if (next_child < b && box_comparator(axis, &it[child], &it[next_child])) child = next_child;
         if (box_comparator(axis, &it[child], &it[cur])) break;
-        sphere_t tmp = it[cur]; it[cur] = it[child]; it[child] = tmp;
+        object_t tmp = it[cur]; it[cur] = it[child]; it[child] = tmp;
         cur = child;
     }
 }
-static void heap_sort(sphere_t* it, size_t a, size_t b, uint32_t axis) {
+static void heap_sort(object_t* it, size_t a, size_t b, uint32_t axis) {
     size_t i = a + (b - a) / 2;
     while (i > a) { i -= 1; sift_down(it, a, i, b, axis); }
     i = b;
     while (i > a) {
         i -= 1;
-        sphere_t tmp = it[a]; it[a] = it[i]; it[i] = tmp;
+        object_t tmp = it[a]; it[a] = it[i]; it[i] = tmp;
         sift_down(it, a, a, i, axis);
     }
 }
 
-static bvh_node_t* make_leaf(world_t* w, const sphere_t* s) {  /* bvh.zig:82-89 */
+static bvh_node_t* make_leaf(world_t* w, const object_t* s) {  /* bvh.zig:82-89 */
     bvh_node_t* n = make_node(w);
     n->leaf = s; n->left = n->right = NULL; n->bbox = s->bbox;
     return n;
@@ -679,29 +937,53 @@ static bvh_node_t* construct_tree(world_t* w, size_t start, size_t end) {
 }
 
 /* bvh.zig:122-136 */
-static int bvh_hit(const world_t* w, const bvh_node_t* node, const ray3* r, interval_t ray_t, hit_record_t* rec) {
+static int bvh_hit(const world_t* w, const bvh_node_t* node, const ray3* r, interval_t ray_t, hit_record_t* rec,
+                   const rng_t* rng) {
     if (node->leaf) {
         COUNT(leaves);
-        return sphere_hit(node->leaf, r, ray_t, rec);
+        o_object ref = {node->leaf->kind, node->leaf->index};
+        return object_hit(w, ref, r, ray_t, rec, rng);
     }
     COUNT(nodes);
     if (!aabb_hit(&node->bbox, r, ray_t)) return 0;
     hit_record_t left_rec, right_rec;
-    int hl = bvh_hit(w, node->left, r, ray_t, &left_rec);
+    int hl = bvh_hit(w, node->left, r, ray_t, &left_rec, rng);
     interval_t r_int = {ray_t.min, hl ? left_rec.t : ray_t.max};
-    int hr = bvh_hit(w, node->right, r, r_int, &right_rec);
+    int hr = bvh_hit(w, node->right, r, r_int, &right_rec, rng);
     if (hr) { *rec = right_rec; return 1; }
     if (hl) { *rec = left_rec; return 1; }
     return 0;
 }
 
 void* oracle_world_create(const o_scene_desc* d) {
-    if (!d || d->n_spheres == 0) return NULL;
+    if (!d) return NULL;
+    const uint32_t n_obj = d->objects ? d->n_objects : d->n_spheres;
+    if (n_obj == 0) return NULL;
     world_t* w = (world_t*)calloc(1, sizeof(world_t));
     w->desc = *d;
-    w->n = d->n_spheres;
-    w->objects = (sphere_t*)malloc(sizeof(sphere_t) * w->n);
-    for (uint32_t i = 0; i < w->n; i++) { sphere_from_desc(&d->spheres[i], &w->objects[i]); w->objects[i].orig = i; }
+    w->spheres = (sphere_t*)calloc(d->n_spheres ? d->n_spheres : 1, sizeof(sphere_t));
+    for (uint32_t i = 0; i < d->n_spheres; i++) { sphere_from_desc(&d->spheres[i], &w->spheres[i]); w->spheres[i].orig = i; }
+    w->quads = (quad_t*)calloc(d->n_quads ? d->n_quads : 1, sizeof(quad_t));
+    for (uint32_t i = 0; i < d->n_quads; i++) quad_from_desc(&d->quads[i], &w->quads[i]);
+    w->insts = (inst_t*)calloc(d->n_instances ? d->n_instances : 1, sizeof(inst_t));
+    for (uint32_t i = 0; i < d->n_instances; i++) inst_from_desc(w, &d->instances[i], &w->insts[i]);
+    w->media = (medium_t*)calloc(d->n_media ? d->n_media : 1, sizeof(medium_t));
+    for (uint32_t i = 0; i < d->n_media; i++) {
+        medium_t* m = &w->media[i];
+        m->boundary = d->media[i].boundary;
+        m->neg_inv_density = -1.0f / d->media[i].density;    /* objects.zig:451 */
+        m->mat = d->media[i].material;
+        m->bbox = object_box(w, m->boundary);
+    }
+    w->n = n_obj;
+    w->objects = (object_t*)malloc(sizeof(object_t) * w->n);
+    for (uint32_t i = 0; i < w->n; i++) {
+        o_object ref = d->objects ? d->objects[i] : (o_object){O_OBJ_SPHERE, i};
+        w->objects[i].kind = ref.kind;
+        w->objects[i].index = ref.index;
+        w->objects[i].orig = i;
+        w->objects[i].bbox = object_box(w, ref);
+    }
     w->pool_cap = 2 * w->n;
     w->pool = (bvh_node_t*)calloc(w->pool_cap, sizeof(bvh_node_t));
     w->build_rng = rng_stream(d->bvh_seed, 2, 0, 0);
@@ -712,6 +994,7 @@ void* oracle_world_create(const o_scene_desc* d) {
 void oracle_world_destroy(void* p) {
     world_t* w = (world_t*)p;
     if (!w) return;
+    free(w->spheres); free(w->quads); free(w->insts); free(w->media);
     free(w->objects); free(w->pool); free(w);
 }
 
@@ -828,7 +1111,7 @@ static v3 ray_color(const world_t* w, const o_camera* c, const ray3* r, uint32_t
     interval_t ray_t = {0.001f, INF_F};
     hit_record_t rec;
     COUNT(rays);
-    if (bvh_hit(w, w->root, r, ray_t, &rec)) {
+    if (bvh_hit(w, w->root, r, ray_t, &rec, rng)) {
         ray3 scattered;
         v3 attenuation = V(0, 0, 0);
         v3 color_from_emission = emitted(&w->desc, rec.mat, rec.u, rec.v, rec.p);

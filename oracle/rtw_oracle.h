@@ -71,6 +71,34 @@ typedef struct o_perlin {           /* 4608 B */
     uint16_t perm_x[256], perm_y[256], perm_z[256];
 } o_perlin;
 
+typedef struct o_quad {             /* 48 B: Quad.init(q, u, v, mat) (objects.zig:201-210) */
+    float q[3];
+    uint32_t material;
+    float u[3];
+    uint32_t _p0;
+    float v[3];
+    uint32_t _p1;
+} o_quad;
+
+enum { O_OBJ_SPHERE = 0, O_OBJ_QUAD = 1, O_OBJ_INSTANCE = 2, O_OBJ_MEDIUM = 3 };
+typedef struct o_object { uint32_t kind, index; } o_object;
+
+enum { O_XF_TRANSLATE = 0, O_XF_ROTATE_Y = 1 };
+typedef struct o_transform { uint32_t kind; float v[3]; } o_transform;
+
+#define O_MAX_XF 3
+enum { O_INST_LIST = 1u };
+typedef struct o_instance {         /* 64 B: xf[0] innermost .. xf[n_xf-1] outermost */
+    uint32_t first, count, n_xf, flags;
+    o_transform xf[O_MAX_XF];
+} o_instance;
+
+typedef struct o_medium {           /* 16 B: ConstantMedium (objects.zig:445-460) */
+    o_object boundary;
+    float density;
+    uint32_t material;              /* the Isotropic phase function */
+} o_medium;
+
 typedef struct o_scene_desc {
     const o_sphere* spheres;   uint32_t n_spheres;
     const o_material* materials; uint32_t n_materials;
@@ -78,6 +106,13 @@ typedef struct o_scene_desc {
     const o_image* images;     uint32_t n_images;
     const o_perlin* perlins;   uint32_t n_perlins;
     uint64_t bvh_seed;
+    uint32_t bvh_mode;              /* ignored: the oracle always builds the reference topology */
+    float order_dir[3];
+    const o_quad* quads;       uint32_t n_quads;
+    const o_object* members;   uint32_t n_members;
+    const o_instance* instances; uint32_t n_instances;
+    const o_medium* media;     uint32_t n_media;
+    const o_object* objects;   uint32_t n_objects;  /* world_objects; NULL = every sphere */
 } o_scene_desc;
 
 enum { O_BG_CONSTANT = 0, O_BG_GRADIENT = 1 };
@@ -135,11 +170,18 @@ int oracle_gen_book1(uint64_t seed, uint32_t variant, o_sphere* sp, o_material* 
 /* Camera.init (camera.zig:118-154) */
 int oracle_camera_init(const o_camera_params* p, o_camera* c);
 
-/* World = BVHTree over the spheres (bvh.zig:22-104) */
+/* Quad.hit (objects.zig:222-255): out t, p3, n3, front, u, v */
+int oracle_quad_hit(const o_quad* q, const float origin[3], const float dir[3], float tmin, float tmax,
+                    float out[10]);
+/* the keyed draw of ConstantMedium.hit (domain "medium") */
+float oracle_medium_draw(uint64_t path_state, uint32_t medium);
+
+/* World = BVHTree over world_objects (bvh.zig:22-104) */
 void* oracle_world_create(const o_scene_desc* d);
 void oracle_world_destroy(void* w);
 int oracle_world_stats(void* w, uint32_t out[4]); /* nodes, leaves, depth, axis draws */
-/* preorder dump of the pointer tree: per node 8 floats (box min3,max3, leaf sphere idx or -1, subtree size) */
+/* preorder dump of the pointer tree: per node 8 floats (box min3,max3, leaf object idx or -1, subtree size);
+ * the leaf index is the position in world_objects (= sphere index when objects is NULL) */
 int oracle_world_dump(void* w, float* out, uint32_t cap);
 
 /* Hot loop.  Camera.render (camera.zig:93-116) for one Task: samples outer,

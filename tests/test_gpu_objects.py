@@ -1,0 +1,127 @@
+"""GPU parity for the SURVEY §8f object scenes: quads, DiffuseLight, Translate /
+RotateY instances of createBox (Cornell box, HEAD's default scene) and
+ConstantMedium + Isotropic (Cornell smoke), through the C ABI against the C oracle.
+
+Tolerances: quads and instances use no transcendental
+function on the device (RotateY's sin/cos are evaluated on the host, with the
+same libm as the oracle), so paths are identical and only the radiance is
+re-associated: every channel within REL * max(1, |ref|), REL sized for depth
+200 (reference topology: every pixel; SAH tree: >= 99.9 % -- exact ties between
+quads that share an edge are won by whichever leaf the walk tests last, which
+depends on the topology, as it does run to run in the reference).  The smoke scene's ConstantMedium uses logf (device ocml vs glibc, 1 ulp)
+and simple_light's Perlin noise uses sinf: there >= 99 % of pixels must meet
+1e-4 and the image mean 1e-3.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+REL = 5e-5
+
+
+def close(gpu, ref, rel=REL):
+    return np.abs(gpu - ref) <= rel * np.maximum(1.0, np.abs(ref))
+
+
+SCENES = {
+    # name: (builder, camera kwargs for both sides, W, spp, strict)
+    "quads": (lambda w: w.quads_world(), dict(aspect_ratio=1.0, vfov=80.0, lookfrom=(0.0, 0.0, 9.0),
+                                              lookat=(0.0, 0.0, 0.0), defocus_angle=0.0,
+                                              background=(0.7, 0.8, 1.0)), 96, 8, True),
+    "cornell": (lambda w: w.cornell_box(), dict(aspect_ratio=1.0, vfov=40.0, lookfrom=(278.0, 278.0, -800.0),
+                                                lookat=(278.0, 278.0, 0.0), defocus_angle=0.0), 96, 8, True),
+    "cornell_smoke": (lambda w: w.cornell_smoke(), dict(aspect_ratio=1.0, vfov=40.0,
+                                                        lookfrom=(278.0, 278.0, -800.0), lookat=(278.0, 278.0, 0.0),
+                                                        defocus_angle=0.0), 96, 8, False),
+    "simple_light": (lambda w: w.simple_light_world(0), dict(aspect_ratio=16 / 9, vfov=20.0,
+                                                             lookfrom=(26.0, 3.0, 6.0), lookat=(0.0, 2.0, 0.0),
+                                                             defocus_angle=0.0), 128, 8, False),
+}
+
+
+def cameras(rtw, oracle, name, W, spp, depth):
+    kw = SCENES[name][1]
+    cam = rtw.Camera(image_width=W, samples_per_pixel=spp, max_depth=depth, **kw).init()
+    ocam = oracle.camera(image_width=W, samples_per_pixel=spp, max_depth=depth, **kw)
+    assert cam.derived.image_height == ocam.image_height
+    return cam, ocam
+
+
+def render_all(rtw, world, cam, spp, seed):
+    buf = np.zeros((cam.size, 4), np.float32)
+    rc = rtw.lib().rtw_render(world.handle, C.byref(cam.derived), 0, cam.size, 0, spp, seed, buf.ctypes.data, None,
+                              rtw._abi.PROGRESS_FN(0), None)
+    rtw._abi.check(rc, "rtw_render")
+    return buf
+
+
+@pytest.mark.parametrize("mode", ["sah", "reference"])
+@pytest.mark.parametrize("name", list(SCENES))
+def test_object_scene_vs_oracle(rtw, oracle, name, mode):
+    build, _, W, spp, strict = SCENES[name]
+    depth = 200 if name == "cornell" else 50
+    m = {"sah": rtw._abi.RTW_BVH_SAH, "reference": rtw._abi.RTW_BVH_REFERENCE}[mode]
+    objs = build(rtw.worlds)
+    if name == "quads" and mode == "sah":
+        # quadsWorld's upper_orange and lower_teal (main.zig:139-140) are coplanar and overlap:
+        # every hit there is an exact tie, won by whichever the BVH tests last (Interval.contains
+        # is inclusive) -- topology-dependent, random per run in the reference.  The reference
+        # topology replays the oracle's winner; the SAH tree is compared without the duplicate.
+        objs = objs[:4]
+    arr = rtw.flatten(objs, bvh_mode=m)
+    world = rtw.World(arr)
+    cam, ocam = cameras(rtw, oracle, name, W, spp, depth)
+    got = render_all(rtw, world, cam, spp, 3)
+    world.close()
+    ref = oracle.World.from_arrays(arr).render_pixels(ocam, 3, np.arange(cam.size, dtype=np.uint32), 0, spp,
+                                                     threads=os.cpu_count() or 1)
+    assert np.isfinite(got).all()
+    assert (got[:, 3] == spp).all()
+    ok = close(got[:, :3], ref[:, :3], REL if strict else 1e-4).all(axis=1)
+    if strict and mode == "reference":
+        assert ok.all(), (ok.mean(), np.abs(got[:, :3] - ref[:, :3]).max())
+    elif strict:
+        # SAH tree: quads sharing an edge (box sides, walls) tie exactly on it; the
+        # winner of a tie is whichever the walk tests last (objects.zig:242 inclusive)
+        assert ok.mean() >= 0.999, (ok.mean(), np.abs(got[:, :3] - ref[:, :3]).max())
+    else:
+        assert ok.mean() >= 0.99, ok.mean()
+        assert abs(got[:, :3].mean() - ref[:, :3].mean()) <= 1e-3 * abs(ref[:, :3].mean())
+
+
+@pytest.mark.parametrize("name", ["cornell", "cornell_smoke"])
+def test_object_kernels_bit_identical(rtw, name, monkeypatch):
+    """v0 / v1 / wavefront perform the same per-path operations: identical images."""
+    arr = rtw.flatten(SCENES[name][0](rtw.worlds))
+    cam = rtw.Camera(image_width=64, samples_per_pixel=6, max_depth=50, **SCENES[name][1]).init()
+    outs = {}
+    for k in ("v0", "v1", "wf"):
+        monkeypatch.setenv("RTW_KERNEL", k)
+        world = rtw.World(arr)
+        outs[k] = render_all(rtw, world, cam, 6, 9)
+        world.close()
+    assert np.array_equal(outs["v0"], outs["v1"]) and np.array_equal(outs["v0"], outs["wf"])
+
+
+def test_object_counters_equal_reference_traversal(rtw, oracle):
+    """Reference topology: the device walk tests exactly the oracle's boxes and leaves."""
+    import torch
+    arr = rtw.flatten(rtw.worlds.cornell_box(), bvh_mode=rtw._abi.RTW_BVH_REFERENCE)
+    world = rtw.World(arr)
+    cam, ocam = cameras(rtw, oracle, "cornell", 64, 2, 200)
+    acc = torch.zeros((cam.size, 4), dtype=torch.float32, device="cuda")
+    cnt = torch.zeros(8, dtype=torch.int64, device="cuda")
+    opts = rtw._abi.RtwRenderOpts(0, 0, cnt.data_ptr())
+    rtw._abi.check(rtw.lib().rtw_render_device(world.handle, C.byref(cam.derived), 0, cam.size, 0, 2, 0,
+                                               acc.data_ptr(), None, C.byref(opts)), "rtw_render_device")
+    g = cnt.cpu().numpy()
+    ow = oracle.World.from_arrays(arr)
+    with oracle.counters() as oc:
+        ow.render_pixels(ocam, 0, np.arange(cam.size, dtype=np.uint32), 0, 2, threads=1)
+    assert g[rtw._abi.RTW_STAT_RAYS] == oc.rays
+    assert g[rtw._abi.RTW_STAT_NODES] == oc.nodes
+    assert g[rtw._abi.RTW_STAT_LEAVES] == oc.leaves

@@ -286,26 +286,45 @@ def test_persistent_v1_bit_identical_to_v0(rtw, earth_rgba, scene, monkeypatch):
     arr = rtw.flatten(rtw.worlds.generate_world(0, scene, imgs))
     cam = rtw.book1_camera(image_width=480, aspect_ratio=1.5, spp=6).init()
     outs = {}
-    for k in ("v0", "v1"):
+    for k in ("v0", "v1", "wf"):
         monkeypatch.setenv("RTW_KERNEL", k)
         world = rtw.World(arr)
         outs[k] = render_rows(rtw, world, cam, 0, cam.derived.image_height, 0, 6, 21)
         world.close()
     assert np.array_equal(outs["v0"], outs["v1"])
+    assert np.array_equal(outs["v0"], outs["wf"])
 
 
 @pytest.mark.parametrize("knob", [("RTW_SHADE_MIN", "1"), ("RTW_SHADE_MIN", "64"), ("RTW_COOP", "0"),
-                                  ("RTW_TILE_ORDER", "0"), ("RTW_WAVES", "8")])
+                                  ("RTW_TILE_ORDER", "0"), ("RTW_POSTPONE", "1"), ("RTW_LDS", "0")])
 def test_v1_knobs_invariant(rtw, book1, knob, monkeypatch):
-    """Scheduling knobs (ballot threshold, cooperative vs per-lane rejection
-    sampling, tile order, launch bounds) only move work between lanes: outputs
-    are bit-identical."""
-    arr, world = book1
+    """Megakernel scheduling knobs (ballot threshold, cooperative vs per-lane
+    rejection sampling, tile order, leaf postponement, LDS staging) only move
+    work between lanes: outputs are bit-identical."""
+    arr, _ = book1
     cam = rtw.book1_camera(image_width=300, aspect_ratio=1.5, spp=3).init()
-    ref = render_rows(rtw, world, cam, 0, 200, 0, 3, 4)
+    monkeypatch.setenv("RTW_KERNEL", "v1")
+    w1 = rtw.World(arr)
+    ref = render_rows(rtw, w1, cam, 0, 200, 0, 3, 4)
+    w1.close()
     monkeypatch.setenv(*knob)
     w2 = rtw.World(arr)
     got = render_rows(rtw, w2, cam, 0, 200, 0, 3, 4)
+    w2.close()
+    assert np.array_equal(ref, got)
+
+
+@pytest.mark.parametrize("knob", [("RTW_WF_ITERS", "1"), ("RTW_WF_ITERS", "50"), ("RTW_WF_PATHS", "4096"),
+                                  ("RTW_REFILL_MIN", "16"), ("RTW_FASTBOX", "0")])
+def test_wavefront_knobs_invariant(rtw, book1, knob, monkeypatch):
+    """Wavefront knobs (bounces before the tail kernel, batch size -> many batches,
+    per-lane refill in trace, FMA vs reference slab test) never change a pixel."""
+    arr, world = book1
+    cam = rtw.book1_camera(image_width=300, aspect_ratio=1.5, spp=5).init()
+    ref = render_rows(rtw, world, cam, 0, 200, 0, 5, 4)
+    monkeypatch.setenv(*knob)
+    w2 = rtw.World(arr)
+    got = render_rows(rtw, w2, cam, 0, 200, 0, 5, 4)
     w2.close()
     assert np.array_equal(ref, got)
 

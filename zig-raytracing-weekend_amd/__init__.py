@@ -14,7 +14,7 @@ The hot path runs in librtw_gpu.so (include/rtw_gpu.h) on gfx950.
 from . import _abi, configs, distributed, rng, worlds  # noqa: F401
 from ._abi import RtwError, lib  # noqa: F401
 from .camera import (Camera, RayTraceState, SharedStateImageWriter, Task, book1_camera,  # noqa: F401
-                     earth_perlin_camera, start_render)
-from .scene import (BVHTree, CheckerTexture, Dielectric, DiffuseLight, Image, ImageTexture,  # noqa: F401
-                    Isotropic, Lambertian, Metal, NoiseTexture, Perlin, SceneArrays, SolidColor, Sphere, World,
-                    flatten)
+                     cornell_camera, cornell_smoke_camera, earth_perlin_camera, simple_light_camera, start_render)
+from .scene import (BVHTree, CheckerTexture, ConstantMedium, Dielectric, DiffuseLight,  # noqa: F401
+                    HittableList, Image, ImageTexture, Isotropic, Lambertian, Metal, NoiseTexture, Perlin, Quad,
+                    RotateY, SceneArrays, SolidColor, Sphere, Translate, World, createBox, flatten)

@@ -35,6 +35,18 @@ TEXTURE_DT = np.dtype([("kind", "<u4"), ("image", "<u4"), ("perlin", "<u4"), ("s
 PERLIN_DT = np.dtype([("ranvec", "<f4", (256, 3)), ("perm_x", "<u2", 256), ("perm_y", "<u2", 256),
                       ("perm_z", "<u2", 256)])
 NODE_DT = np.dtype([("a", "<f4", 4), ("b", "<f4", 4)])
+QUAD_DT = np.dtype([("q", "<f4", 3), ("material", "<u4"), ("u", "<f4", 3), ("_p0", "<u4"), ("v", "<f4", 3),
+                    ("_p1", "<u4")])
+OBJECT_DT = np.dtype([("kind", "<u4"), ("index", "<u4")])
+XF_DT = np.dtype([("kind", "<u4"), ("v", "<f4", 3)])
+RTW_MAX_XF = 3
+RTW_INST_LIST = 1
+INSTANCE_DT = np.dtype([("first", "<u4"), ("count", "<u4"), ("n_xf", "<u4"), ("flags", "<u4"),
+                        ("xf", XF_DT, RTW_MAX_XF)])
+MEDIUM_DT = np.dtype([("boundary", OBJECT_DT), ("density", "<f4"), ("material", "<u4")])
+assert QUAD_DT.itemsize == 48 and OBJECT_DT.itemsize == 8 and INSTANCE_DT.itemsize == 64 and MEDIUM_DT.itemsize == 16
+RTW_OBJ_SPHERE, RTW_OBJ_QUAD, RTW_OBJ_INSTANCE, RTW_OBJ_MEDIUM = 0, 1, 2, 3
+RTW_XF_TRANSLATE, RTW_XF_ROTATE_Y = 0, 1
 assert SPHERE_DT.itemsize == 48 and MATERIAL_DT.itemsize == 32 and TEXTURE_DT.itemsize == 48
 assert PERLIN_DT.itemsize == 4608 and NODE_DT.itemsize == 32
 
@@ -50,7 +62,12 @@ class RtwSceneDesc(C.Structure):
                 ("textures", C.c_void_p), ("n_textures", C.c_uint32),
                 ("images", C.c_void_p), ("n_images", C.c_uint32),
                 ("perlins", C.c_void_p), ("n_perlins", C.c_uint32),
-                ("bvh_seed", C.c_uint64), ("bvh_mode", C.c_uint32), ("order_dir", C.c_float * 3)]
+                ("bvh_seed", C.c_uint64), ("bvh_mode", C.c_uint32), ("order_dir", C.c_float * 3),
+                ("quads", C.c_void_p), ("n_quads", C.c_uint32),
+                ("members", C.c_void_p), ("n_members", C.c_uint32),
+                ("instances", C.c_void_p), ("n_instances", C.c_uint32),
+                ("media", C.c_void_p), ("n_media", C.c_uint32),
+                ("objects", C.c_void_p), ("n_objects", C.c_uint32)]
 
 
 F3 = C.c_float * 3

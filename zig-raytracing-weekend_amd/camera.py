@@ -172,3 +172,22 @@ def earth_perlin_camera(image_width: int = 1920, spp: int = 512, max_depth: int 
     return Camera(aspect_ratio=16.0 / 9.0, image_width=image_width, samples_per_pixel=spp, max_depth=max_depth,
                   background=(0.7, 0.8, 1.0), background_mode=_abi.RTW_BG_CONSTANT, vfov=30.0,
                   lookfrom=(13.0, 2.0, 3.0), lookat=(0.0, 1.0, 0.0), defocus_angle=0.0, focus_dist=10.0)
+
+
+def simple_light_camera(image_width: int = 800, spp: int = 100) -> Camera:
+    """Camera{} defaults as modified by simpleLightWorld (src/main.zig:157-162)."""
+    return Camera(image_width=image_width, samples_per_pixel=spp, max_depth=50, lookfrom=(26.0, 3.0, 6.0),
+                  lookat=(0.0, 2.0, 0.0), vup=(0.0, 1.0, 0.0), defocus_angle=0.0)
+
+
+def cornell_camera(image_width: int = 600, spp: int = 200, max_depth: int = 200) -> Camera:
+    """cornellBox's camera (src/main.zig:194-202): 600x600, 200 spp, depth 200, black background."""
+    return Camera(aspect_ratio=1.0, image_width=image_width, samples_per_pixel=spp, max_depth=max_depth, vfov=40.0,
+                  lookfrom=(278.0, 278.0, -800.0), lookat=(278.0, 278.0, 0.0), vup=(0.0, 1.0, 0.0),
+                  defocus_angle=0.0)
+
+
+def cornell_smoke_camera(image_width: int = 600, spp: int = 200, max_depth: int = 50) -> Camera:
+    """cornellBoxSmoke's camera (src/main.zig:238-246)."""
+    return cornell_camera(image_width, spp, max_depth)
+

@@ -5,7 +5,7 @@ from dataclasses import dataclass
 from typing import Callable, List
 
 from . import worlds
-from .camera import Camera, book1_camera, earth_perlin_camera
+from .camera import Camera, book1_camera, cornell_camera, cornell_smoke_camera, earth_perlin_camera, simple_light_camera
 from .scene import Sphere
 
 
@@ -34,4 +34,11 @@ CONFIGS = {
     "c5": Config("c5", "Textured: earthmap image sphere + Perlin noise spheres, 1920x1080, 512 spp",
                  lambda: worlds.earth_perlin_world(0),
                  lambda: earth_perlin_camera(image_width=1920, spp=512, max_depth=50)),
+    # SURVEY §8f scenes (not BASELINE configs): HEAD's default scene and its smoke variant
+    "cornell": Config("cornell", "Cornell box (HEAD default scene) 600x600, 200 spp, depth 200",
+                      worlds.cornell_box, lambda: cornell_camera(600, 200, 200)),
+    "cornell_smoke": Config("cornell_smoke", "Cornell box with two ConstantMedium boxes 600x600, 200 spp, depth 50",
+                            worlds.cornell_smoke, lambda: cornell_smoke_camera(600, 200, 50)),
+    "simple_light": Config("simple_light", "Perlin spheres + quad/sphere lights 800x450, 100 spp, depth 50",
+                           lambda: worlds.simple_light_world(0), lambda: simple_light_camera(800, 100)),
 }

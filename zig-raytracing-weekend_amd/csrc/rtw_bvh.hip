@@ -8,6 +8,12 @@
 //   * else std.sort.heap of the slice by box min on the axis, median split.
 // The tree is emitted directly in pre-order with skip links (rtw_layout.h),
 // so the kernel's stackless walk replays the reference traversal order.
+//
+// The leaves are the world objects (spheres, quads, Translate/RotateY instances
+// of a HittableList, ConstantMedium); their boxes are restated from Sphere.init,
+// Quad.init, HittableList.add, Translate.init, RotateY.init and
+// ConstantMedium.boundingBox (src/objects.zig:80-92, 201-210, 273-276, 299-304,
+// 340-388, 462-464), because the reference orders and splits by them.
 #include <algorithm>
 #include <array>
 #include <cmath>
@@ -25,9 +31,10 @@ struct Box {
     float mn[3], mx[3];
 };
 
+// a world object: kind (RTW_OBJ_*) + index into its array, and its box
 struct Obj {
     Box box;
-    uint32_t sphere;
+    uint32_t kind, index;
 };
 
 // Aabb.fromPoints (src/aabb.zig:18-26)
@@ -61,22 +68,229 @@ Box sphere_box(const rtw_sphere& s) {
     return box_union(b1, box_from_points(lo, hi));
 }
 
-class RefBuilder {
-public:
-    RefBuilder(const rtw_scene_desc& d, std::vector<rtw_node>& out, std::vector<float>& cvec)
-        : desc_(d), nodes_(out), cvec_(cvec), rng_(rtw_rng_stream(d.bvh_seed, 2, 0, 0)) {
-        objs_.resize(d.n_spheres);
-        for (uint32_t i = 0; i < d.n_spheres; i++) {
-            objs_[i].box = sphere_box(d.spheres[i]);
-            objs_[i].sphere = i;
-        }
-        cvec_.assign(4 * (size_t)d.n_spheres, 0.0f);
-        for (uint32_t i = 0; i < d.n_spheres; i++) {
-            const rtw_sphere& s = d.spheres[i];
-            if (s.is_moving)
-                for (int k = 0; k < 3; k++) cvec_[4 * i + k] = s.center2[k] - s.center1[k];
+// Aabb.pad (aabb.zig:36-43), Interval.expand (interval.zig:26-29)
+Box box_pad(Box b) {
+    const float delta = 0.0001f;
+    for (int k = 0; k < 3; k++) {
+        if (!(b.mx[k] - b.mn[k] >= delta)) {
+            const float padding = delta / 2.0f;
+            b.mn[k] = b.mn[k] - padding;
+            b.mx[k] = b.mx[k] + padding;
         }
     }
+    return b;
+}
+
+// Validated object graph + device geometry records + per-object boxes.
+class Geometry {
+public:
+    Geometry(const rtw_scene_desc& d, rtw_geometry& g) : d_(d), g_(g) {}
+
+    int build() {
+        const rtw_scene_desc& d = d_;
+        if (d.n_quads && !d.quads) return RTW_E_INVALID;
+        if (d.n_members && !d.members) return RTW_E_INVALID;
+        if (d.n_instances && !d.instances) return RTW_E_INVALID;
+        if (d.n_media && !d.media) return RTW_E_INVALID;
+        g_.feat = 0;
+        // spheres: device records + center_vec
+        g_.spheres.assign(d.n_spheres, rtw_dev_sphere{});
+        g_.cvec.assign(4 * (size_t)d.n_spheres, 0.0f);
+        sbox_.resize(d.n_spheres);
+        for (uint32_t i = 0; i < d.n_spheres; i++) {
+            const rtw_sphere& s = d.spheres[i];
+            rtw_dev_sphere& o = g_.spheres[i];
+            for (int k = 0; k < 3; k++) o.c1[k] = s.center1[k];
+            o.radius = s.radius;
+            o.mat = s.material;
+            o.moving = s.is_moving ? 1u : 0u;
+            if (s.is_moving)
+                for (int k = 0; k < 3; k++) g_.cvec[4 * i + k] = s.center2[k] - s.center1[k];
+            sbox_[i] = sphere_box(s);
+        }
+        // quads: Quad.init (objects.zig:201-210)
+        g_.quads.assign(d.n_quads, rtw_dev_quad{});
+        qbox_.resize(d.n_quads);
+        for (uint32_t i = 0; i < d.n_quads; i++) {
+            const rtw_quad& q = d.quads[i];
+            if (q.material >= d.n_materials) return RTW_E_INVALID;
+            rtw_dev_quad& o = g_.quads[i];
+            float n[3], nn[3];
+            n[0] = q.u[1] * q.v[2] - q.u[2] * q.v[1];
+            n[1] = q.u[2] * q.v[0] - q.u[0] * q.v[2];
+            n[2] = q.u[0] * q.v[1] - q.u[1] * q.v[0];
+            const float len = std::sqrt(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]);
+            for (int k = 0; k < 3; k++) nn[k] = n[k] / len;
+            const float nd = n[0] * n[0] + n[1] * n[1] + n[2] * n[2];
+            o.d = nn[0] * q.q[0] + nn[1] * q.q[1] + nn[2] * q.q[2];
+            float far[3];
+            for (int k = 0; k < 3; k++) {
+                o.q[k] = q.q[k];
+                o.n[k] = nn[k];
+                o.u[k] = q.u[k];
+                o.v[k] = q.v[k];
+                o.w[k] = n[k] / nd;
+                far[k] = (q.q[k] + q.u[k]) + q.v[k];
+            }
+            o.mat = q.material;
+            qbox_[i] = box_pad(box_from_points(q.q, far));
+        }
+        if (d.n_quads) g_.feat |= RTW_F_GEOM;
+        // instance members
+        g_.members.resize(d.n_members);
+        for (uint32_t i = 0; i < d.n_members; i++) {
+            const rtw_object& m = d.members[i];
+            if (m.kind == RTW_OBJ_SPHERE ? m.index >= d.n_spheres : (m.kind != RTW_OBJ_QUAD || m.index >= d.n_quads))
+                return RTW_E_INVALID;
+            g_.members[i] = RTW_REF(m.kind, m.index);
+        }
+        // instances: HittableList box then the transform chain (innermost first)
+        g_.insts.assign(d.n_instances, rtw_dev_instance{});
+        ibox_.resize(d.n_instances);
+        for (uint32_t i = 0; i < d.n_instances; i++) {
+            const rtw_instance& in = d.instances[i];
+            if (in.count == 0 || in.count > 127 || in.first > d.n_members || in.count > d.n_members - in.first ||
+                in.n_xf > RTW_MAX_XF)
+                return RTW_E_INVALID;
+            rtw_dev_instance& o = g_.insts[i];
+            o.first = in.first;
+            o.count = in.count;
+            o.n_xf = in.n_xf;
+            Box b;
+            if (in.flags & RTW_INST_LIST) {  // HittableList: bounding_box starts as Aabb{} = [0,0]^3
+                for (int k = 0; k < 3; k++) b.mn[k] = b.mx[k] = 0.0f;
+                for (uint32_t m = 0; m < in.count; m++) b = box_union(b, member_box(d.members[in.first + m]));
+            } else {
+                b = member_box(d.members[in.first]);
+            }
+            for (uint32_t k = 0; k < in.n_xf; k++) {
+                const rtw_transform& x = in.xf[k];
+                uint32_t kind = x.kind;
+                std::memcpy(&o.xf[k][0], &kind, 4);
+                if (x.kind == RTW_XF_TRANSLATE) {  // Translate.init: box.add(offset)
+                    for (int c = 0; c < 3; c++) {
+                        o.xf[k][1 + c] = x.v[c];
+                        b.mn[c] = b.mn[c] + x.v[c];
+                        b.mx[c] = b.mx[c] + x.v[c];
+                    }
+                } else if (x.kind == RTW_XF_ROTATE_Y) {  // RotateY.init
+                    const float pi = 3.1415926535897932385f;
+                    const float radians = x.v[0] * pi / 180.0f;  // degreesToRadians (rtweekend.zig:10-12)
+                    const float sn = std::sin(radians), cs = std::cos(radians);
+                    o.xf[k][1] = sn;
+                    o.xf[k][2] = cs;
+                    o.xf[k][3] = 0.0f;
+                    b = rotate_y_box(b, sn, cs);
+                } else {
+                    return RTW_E_INVALID;
+                }
+            }
+            ibox_[i] = b;
+        }
+        if (d.n_instances) g_.feat |= RTW_F_GEOM;
+        // media: ConstantMedium (objects.zig:445-464)
+        g_.media.assign(d.n_media, rtw_dev_medium{});
+        mbox_.resize(d.n_media);
+        for (uint32_t i = 0; i < d.n_media; i++) {
+            const rtw_medium& m = d.media[i];
+            const rtw_object& bd = m.boundary;
+            const bool ok = (bd.kind == RTW_OBJ_SPHERE && bd.index < d.n_spheres) ||
+                            (bd.kind == RTW_OBJ_QUAD && bd.index < d.n_quads) ||
+                            (bd.kind == RTW_OBJ_INSTANCE && bd.index < d.n_instances);
+            if (!ok || m.material >= d.n_materials) return RTW_E_INVALID;
+            g_.media[i].boundary = RTW_REF(bd.kind, bd.index);
+            g_.media[i].neg_inv_density = -1.0f / m.density;  // objects.zig:451
+            g_.media[i].mat = m.material;
+            mbox_[i] = object_box(bd);
+        }
+        if (d.n_media) g_.feat |= RTW_F_MEDIUM | RTW_F_GEOM;
+        // world objects
+        const uint32_t n = d.objects ? d.n_objects : d.n_spheres;
+        if (n == 0) return RTW_E_INVALID;
+        objs_.resize(n);
+        for (uint32_t i = 0; i < n; i++) {
+            const rtw_object ref = d.objects ? d.objects[i] : rtw_object{RTW_OBJ_SPHERE, i};
+            const uint32_t cap = ref.kind == RTW_OBJ_SPHERE     ? d.n_spheres
+                                 : ref.kind == RTW_OBJ_QUAD     ? d.n_quads
+                                 : ref.kind == RTW_OBJ_INSTANCE ? d.n_instances
+                                 : ref.kind == RTW_OBJ_MEDIUM   ? d.n_media
+                                                                : 0;
+            if (ref.index >= cap) return RTW_E_INVALID;
+            objs_[i].kind = ref.kind;
+            objs_[i].index = ref.index;
+            objs_[i].box = object_box(ref);
+        }
+        return RTW_OK;
+    }
+
+    const std::vector<Obj>& objects() const { return objs_; }
+
+    // leaf record of a world object (rtw_layout.h)
+    rtw_node leaf(const Obj& o, uint32_t skip) const {
+        rtw_node n{};
+        const uint32_t w = skip | RTW_LEAF_BIT;
+        std::memcpy(&n.a[3], &w, 4);
+        if (o.kind == RTW_OBJ_SPHERE) {
+            const rtw_sphere& s = d_.spheres[o.index];
+            n.a[0] = s.center1[0]; n.a[1] = s.center1[1]; n.a[2] = s.center1[2];
+            n.b[0] = s.radius;
+            std::memcpy(&n.b[1], &s.material, 4);
+            std::memcpy(&n.b[2], &o.index, 4);
+            const uint32_t mv = s.is_moving ? 1u : 0u;
+            std::memcpy(&n.b[3], &mv, 4);
+            return n;
+        }
+        const uint32_t mat = o.kind == RTW_OBJ_QUAD ? d_.quads[o.index].material
+                             : o.kind == RTW_OBJ_MEDIUM ? d_.media[o.index].material : 0u;
+        const uint32_t kind = o.kind << 8;
+        std::memcpy(&n.b[1], &mat, 4);
+        std::memcpy(&n.b[2], &o.index, 4);
+        std::memcpy(&n.b[3], &kind, 4);
+        return n;
+    }
+
+private:
+    Box member_box(const rtw_object& m) const { return m.kind == RTW_OBJ_SPHERE ? sbox_[m.index] : qbox_[m.index]; }
+    Box object_box(const rtw_object& r) const {
+        switch (r.kind) {
+        case RTW_OBJ_SPHERE: return sbox_[r.index];
+        case RTW_OBJ_QUAD: return qbox_[r.index];
+        case RTW_OBJ_INSTANCE: return ibox_[r.index];
+        default: return mbox_[r.index];
+        }
+    }
+    // RotateY.init box (objects.zig:353-386)
+    static Box rotate_y_box(const Box& bb, float sn, float cs) {
+        const float inf = __builtin_inff();
+        float mn[3] = {inf, inf, inf}, mx[3] = {-inf, -inf, -inf};
+        for (int i = 0; i < 2; i++)
+            for (int j = 0; j < 2; j++)
+                for (int k = 0; k < 2; k++) {
+                    const float i_f = (float)i, j_f = (float)j, k_f = (float)k;
+                    const float x = i_f * bb.mx[0] + (1 - i_f) * bb.mn[0];
+                    const float y = j_f * bb.mx[1] + (1 - j_f) * bb.mn[1];
+                    const float z = k_f * bb.mx[2] + (1 - k_f) * bb.mn[2];
+                    const float newx = cs * x + sn * z;
+                    const float newz = -sn * x + cs * z;
+                    const float t[3] = {newx, y, newz};
+                    for (int c = 0; c < 3; c++) {
+                        mn[c] = std::fmin(mn[c], t[c]);
+                        mx[c] = std::fmax(mx[c], t[c]);
+                    }
+                }
+        return box_from_points(mn, mx);
+    }
+
+    const rtw_scene_desc& d_;
+    rtw_geometry& g_;
+    std::vector<Box> sbox_, qbox_, ibox_, mbox_;
+    std::vector<Obj> objs_;
+};
+
+class RefBuilder {
+public:
+    RefBuilder(const rtw_scene_desc& d, const Geometry& g, std::vector<rtw_node>& out)
+        : geo_(g), nodes_(out), objs_(g.objects()), rng_(rtw_rng_stream(d.bvh_seed, 2, 0, 0)) {}
 
     void build() {
         nodes_.clear();
@@ -127,18 +341,7 @@ private:
     }
 
     Box emit_leaf(const Obj& o) {
-        const rtw_sphere& s = desc_.spheres[o.sphere];
-        rtw_node n;
-        uint32_t skip = (uint32_t)nodes_.size() + 1;
-        n.a[0] = s.center1[0]; n.a[1] = s.center1[1]; n.a[2] = s.center1[2];
-        uint32_t w = skip | RTW_LEAF_BIT;
-        std::memcpy(&n.a[3], &w, 4);
-        n.b[0] = s.radius;
-        std::memcpy(&n.b[1], &s.material, 4);
-        std::memcpy(&n.b[2], &o.sphere, 4);
-        uint32_t mv = s.is_moving ? 1u : 0u;
-        std::memcpy(&n.b[3], &mv, 4);
-        nodes_.push_back(n);
+        nodes_.push_back(geo_.leaf(o, (uint32_t)nodes_.size() + 1));
         return o.box;
     }
 
@@ -174,9 +377,8 @@ private:
         return bb;
     }
 
-    const rtw_scene_desc& desc_;
+    const Geometry& geo_;
     std::vector<rtw_node>& nodes_;
-    std::vector<float>& cvec_;
     std::vector<Obj> objs_;
     rtw_rng rng_;
     uint32_t depth_ = 0;
@@ -193,24 +395,14 @@ private:
 // first, so front-most geometry shrinks `closest` early in the fixed walk.
 class SahBuilder {
 public:
-    SahBuilder(const rtw_scene_desc& d, std::vector<rtw_node>& out, std::vector<float>& cvec)
-        : desc_(d), nodes_(out), cvec_(cvec) {
-        const uint32_t n = d.n_spheres;
-        objs_.resize(n);
+    SahBuilder(const rtw_scene_desc& d, const Geometry& g, std::vector<rtw_node>& out)
+        : geo_(g), nodes_(out), objs_(g.objects()) {
+        const size_t n = objs_.size();
         cent_.resize(n);
-        for (uint32_t i = 0; i < n; i++) {
-            objs_[i].box = sphere_box(d.spheres[i]);
-            objs_[i].sphere = i;
+        for (size_t i = 0; i < n; i++)
             for (int k = 0; k < 3; k++) cent_[i][k] = 0.5f * (objs_[i].box.mn[k] + objs_[i].box.mx[k]);
-        }
         idx_.resize(n);
-        for (uint32_t i = 0; i < n; i++) idx_[i] = i;
-        cvec_.assign(4 * (size_t)n, 0.0f);
-        for (uint32_t i = 0; i < n; i++) {
-            const rtw_sphere& s = d.spheres[i];
-            if (s.is_moving)
-                for (int k = 0; k < 3; k++) cvec_[4 * i + k] = s.center2[k] - s.center1[k];
-        }
+        for (size_t i = 0; i < n; i++) idx_[i] = (uint32_t)i;
         for (int k = 0; k < 3; k++) dir_[k] = d.order_dir[k];
         if (dir_[0] == 0 && dir_[1] == 0 && dir_[2] == 0) dir_[1] = -1;
     }
@@ -233,20 +425,8 @@ private:
         return r;
     }
     Box emit_leaf(uint32_t oi) {
-        const Obj& o = objs_[oi];
-        const rtw_sphere& s = desc_.spheres[o.sphere];
-        rtw_node n;
-        uint32_t skip = (uint32_t)nodes_.size() + 1;
-        n.a[0] = s.center1[0]; n.a[1] = s.center1[1]; n.a[2] = s.center1[2];
-        uint32_t w = skip | RTW_LEAF_BIT;
-        std::memcpy(&n.a[3], &w, 4);
-        n.b[0] = s.radius;
-        std::memcpy(&n.b[1], &s.material, 4);
-        std::memcpy(&n.b[2], &o.sphere, 4);
-        uint32_t mv = s.is_moving ? 1u : 0u;
-        std::memcpy(&n.b[3], &mv, 4);
-        nodes_.push_back(n);
-        return o.box;
+        nodes_.push_back(geo_.leaf(objs_[oi], (uint32_t)nodes_.size() + 1));
+        return objs_[oi].box;
     }
     // returns split position (index) after partitioning idx_[a, b)
     size_t split(size_t a, size_t b) {
@@ -341,9 +521,8 @@ private:
         return bb;
     }
 
-    const rtw_scene_desc& desc_;
+    const Geometry& geo_;
     std::vector<rtw_node>& nodes_;
-    std::vector<float>& cvec_;
     std::vector<Obj> objs_;
     std::vector<std::array<float, 3>> cent_;
     std::vector<uint32_t> idx_;
@@ -353,12 +532,14 @@ private:
 
 }  // namespace
 
-int rtw_build_bvh(const rtw_scene_desc& desc, std::vector<rtw_node>& nodes, std::vector<float>& cvec,
+int rtw_build_bvh(const rtw_scene_desc& desc, std::vector<rtw_node>& nodes, rtw_geometry& geom,
                   uint32_t* depth, uint32_t* axis_draws, float* box_pad, float* extent) {
     if (box_pad) *box_pad = 0;
     if (extent) *extent = 0;
+    Geometry geo(desc, geom);
+    if (int rc = geo.build()) return rc;
     if (desc.bvh_mode == RTW_BVH_SAH) {
-        SahBuilder b(desc, nodes, cvec);
+        SahBuilder b(desc, geo, nodes);
         b.build();
         if (depth) *depth = b.depth();
         if (axis_draws) *axis_draws = 0;
@@ -389,7 +570,7 @@ int rtw_build_bvh(const rtw_scene_desc& desc, std::vector<rtw_node>& nodes, std:
         return RTW_OK;
     }
     if (desc.bvh_mode != RTW_BVH_REFERENCE) return RTW_E_INVALID;
-    RefBuilder b(desc, nodes, cvec);
+    RefBuilder b(desc, geo, nodes);
     b.build();
     if (depth) *depth = b.depth();
     if (axis_draws) *axis_draws = b.axis_draws();

@@ -50,6 +50,9 @@ __device__ __forceinline__ f3 operator-(f3 a) { return f3{-a.x, -a.y, -a.z}; }
 __device__ __forceinline__ f3 splat(float s) { return f3{s, s, s}; }
 __device__ __forceinline__ f3 divs(f3 a, float s) { return f3{RTW_DIV(a.x, s), RTW_DIV(a.y, s), RTW_DIV(a.z, s)}; }
 __device__ __forceinline__ float dot(f3 u, f3 v) { return u.x * v.x + u.y * v.y + u.z * v.z; }
+__device__ __forceinline__ f3 cross(f3 u, f3 v) {  // vec3.zig:31-33
+    return f3{u.y * v.z - u.z * v.y, u.z * v.x - u.x * v.z, u.x * v.y - u.y * v.x};
+}
 __device__ __forceinline__ float length_squared(f3 u) { return u.x * u.x + u.y * u.y + u.z * u.z; }
 __device__ __forceinline__ f3 unit_vector(f3 v) { return divs(v, __builtin_sqrtf(length_squared(v))); }
 __device__ __forceinline__ f3 ld3(const float* p) { return f3{p[0], p[1], p[2]}; }
@@ -200,8 +203,17 @@ __device__ __forceinline__ void sphere_uv(f3 p, float& u, float& v) {  // object
     v = theta / kPi;
 }
 
+// (u, v) of a hit: sphere hits derive it from the outward normal (getSphereUV,
+// objects.zig:101-114, only when an image texture needs it); quads / instance
+// members / media carry it explicitly.
+struct HitUV {
+    f3 outward;
+    float u, v;
+    bool set;
+};
+
 template <uint32_t FEAT>
-__device__ f3 texture_value(const rtw_launch& L, uint32_t ti, f3 outward, f3 p) {
+__device__ f3 texture_value(const rtw_launch& L, uint32_t ti, const HitUV& uv, f3 p) {
     const rtw_dev_texture& t = L.texs[ti];
     const uint32_t kind = t.kind;
     if constexpr ((FEAT & RTW_F_CHECKER) != 0) {
@@ -216,8 +228,8 @@ __device__ f3 texture_value(const rtw_launch& L, uint32_t ti, f3 outward, f3 p) 
         if (kind == RTW_TEX_IMAGE) {  // textures.zig:85-104, rtw_image.zig:37-62
             const rtw_dev_image im = L.img_info[t.image];
             if (im.height <= 0) return mk(0, 1, 1);
-            float u, v;
-            sphere_uv(outward, u, v);
+            float u = uv.u, v = uv.v;
+            if (!uv.set) sphere_uv(uv.outward, u, v);
             float nu = u < 0 ? 0 : (u > 1 ? 1 : u);
             float nv = 1.0f - (v < 0 ? 0 : (v > 1 ? 1 : v));
             uint32_t i = (uint32_t)__builtin_floorf(nu * (float)im.width);
@@ -282,6 +294,184 @@ __device__ __forceinline__ RayTrav ray_trav(const Ray& r, bool fast_box) {
 
 constexpr float kTmin = 0.001f;  // camera.zig:187
 
+// ---------------------------------------------------------------------------
+// Non-sphere world objects (scenes with RTW_F_GEOM / RTW_F_MEDIUM): quads,
+// Translate/RotateY instances of a HittableList, ConstantMedium.  Same fp32
+// operations in the same order as objects.zig (and the CPU restatement).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float4 ldg4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+
+// Sphere.hit t only (objects.zig:116-136), open interval (tmin, tmax)
+__device__ __forceinline__ bool sphere_t(f3 center, float radius, const Ray& r, float tmin, float tmax, float& t) {
+    const f3 oc = r.o - center;
+    const float a = length_squared(r.d);
+    const float half_b = dot(oc, r.d);
+    const float c = length_squared(oc) - radius * radius;
+    const float disc = half_b * half_b - a * c;
+    if (disc < 0) return false;
+    const float sq = __builtin_sqrtf(disc);
+    float root = RTW_DIV(-half_b - sq, a);
+    if (!(tmin < root && root < tmax)) {
+        root = RTW_DIV(-half_b + sq, a);
+        if (!(tmin < root && root < tmax)) return false;
+    }
+    t = root;
+    return true;
+}
+
+template <uint32_t FEAT>
+__device__ __forceinline__ f3 member_sphere_center(const rtw_launch& L, const rtw_dev_sphere& s, uint32_t idx,
+                                                   float time) {
+    f3 c = ld3(s.c1);
+    if constexpr ((FEAT & RTW_F_MOVING) != 0) {
+        if (s.moving) {  // Sphere.getCenter (objects.zig:94-98)
+            const float4 cv = L.cvec[idx];
+            c = c + splat(time) * mk(cv.x, cv.y, cv.z);
+        }
+    }
+    return c;
+}
+
+// Quad.hit t only (objects.zig:222-255), closed interval [tmin, tmax]
+__device__ __forceinline__ bool quad_t(const rtw_dev_quad& q, const Ray& r, float tmin, float tmax, float& t) {
+    const f3 n = ld3(q.n);
+    const float denom = dot(n, r.d);
+    if (__builtin_fabsf(denom) < 1e-8f) return false;
+    const float tt = RTW_DIV(q.d - dot(n, r.o), denom);
+    if (!(tmin <= tt && tt <= tmax)) return false;
+    const f3 planar = (r.o + splat(tt) * r.d) - ld3(q.q);
+    const f3 w = ld3(q.w);
+    const float alpha = dot(w, cross(planar, ld3(q.v)));
+    const float beta = dot(w, cross(ld3(q.u), planar));
+    if ((alpha < 0) || (1 < alpha) || (beta < 0) || (1 < beta)) return false;
+    t = tt;
+    return true;
+}
+
+// world ray -> object space of an instance: the outermost transform first
+// (Translate.hit objects.zig:314-317, RotateY.hit :401-411)
+__device__ __forceinline__ Ray inst_to_object(const rtw_dev_instance& in, Ray r) {
+    for (int k = (int)in.n_xf - 1; k >= 0; k--) {
+        const float4 x = ldg4(in.xf[k]);
+        if (fbits(x.x) == RTW_XF_TRANSLATE) {
+            r.o = r.o - mk(x.y, x.z, x.w);
+        } else {
+            const float s = x.y, c = x.z;
+            const f3 o = r.o, d = r.d;
+            r.o.x = c * o.x - s * o.z;
+            r.o.z = s * o.x + c * o.z;
+            r.d.x = c * d.x - s * d.z;
+            r.d.z = s * d.x + c * d.z;
+        }
+    }
+    return r;
+}
+
+// object-space point/normal -> world: innermost transform first (RotateY.hit :419-435, Translate.hit :325-326)
+__device__ __forceinline__ void inst_to_world(const rtw_dev_instance& in, f3& p, f3& n) {
+    for (uint32_t k = 0; k < in.n_xf; k++) {
+        const float4 x = ldg4(in.xf[k]);
+        if (fbits(x.x) == RTW_XF_TRANSLATE) {
+            p = p + mk(x.y, x.z, x.w);
+        } else {
+            const float s = x.y, c = x.z;
+            const f3 p0 = p, n0 = n;
+            p.x = c * p0.x + s * p0.z;
+            p.z = -s * p0.x + c * p0.z;
+            n.x = c * n0.x + s * n0.z;
+            n.z = -s * n0.x + c * n0.z;
+        }
+    }
+}
+
+// HittableList.hit over the members in object space (objects.zig:281-289)
+template <uint32_t FEAT>
+__device__ __forceinline__ bool list_t(const rtw_launch& L, const rtw_dev_instance& in, const Ray& ro, float tmin,
+                                       float tmax, float& t, uint32_t& sub) {
+    bool any = false;
+    float closest = tmax;
+    for (uint32_t m = 0; m < in.count; m++) {
+        const uint32_t ref = L.members[in.first + m];
+        const uint32_t idx = RTW_REF_INDEX(ref);
+        float tt;
+        bool h;
+        if (RTW_REF_KIND(ref) == RTW_OBJ_SPHERE) {
+            const rtw_dev_sphere s = L.sph[idx];
+            h = sphere_t(member_sphere_center<FEAT>(L, s, idx, ro.time), s.radius, ro, tmin, closest, tt);
+        } else {
+            h = quad_t(L.quads[idx], ro, tmin, closest, tt);
+        }
+        if (h) {
+            closest = tt;
+            sub = m;
+            any = true;
+        }
+    }
+    t = closest;
+    return any;
+}
+
+// Hittable.hit of a sphere / quad / instance reference (a medium boundary)
+template <uint32_t FEAT>
+__device__ __forceinline__ bool boundary_t(const rtw_launch& L, uint32_t ref, const Ray& r, float tmin, float tmax,
+                                           float& t) {
+    const uint32_t idx = RTW_REF_INDEX(ref);
+    switch (RTW_REF_KIND(ref)) {
+    case RTW_OBJ_SPHERE: {
+        const rtw_dev_sphere s = L.sph[idx];
+        return sphere_t(member_sphere_center<FEAT>(L, s, idx, r.time), s.radius, r, tmin, tmax, t);
+    }
+    case RTW_OBJ_QUAD: return quad_t(L.quads[idx], r, tmin, tmax, t);
+    default: {
+        const rtw_dev_instance in = L.insts[idx];
+        uint32_t sub;
+        return list_t<FEAT>(L, in, inst_to_object(in, r), tmin, tmax, t, sub);
+    }
+    }
+}
+
+// ConstantMedium.hit (objects.zig:470-507); the draw is keyed by (mkey, medium)
+template <uint32_t FEAT>
+__device__ __forceinline__ bool medium_t(const rtw_launch& L, uint32_t idx, const Ray& r, float tmin, float tmax,
+                                         uint64_t mkey, float& t) {
+    const rtw_dev_medium m = L.media[idx];
+    float t1, t2;
+    if (!boundary_t<FEAT>(L, m.boundary, r, -kInf, kInf, t1)) return false;  // intervals.universe
+    if (!boundary_t<FEAT>(L, m.boundary, r, t1 + 0.0001f, kInf, t2)) return false;
+    if (t1 < tmin) t1 = tmin;
+    if (t2 > tmax) t2 = tmax;
+    if (t1 >= t2) return false;
+    if (t1 < 0) t1 = 0;
+    const float ray_length = __builtin_sqrtf(length_squared(r.d));
+    const float inside = (t2 - t1) * ray_length;
+    const float hit_distance = m.neg_inv_density * logf(rtw_medium_u(mkey, idx));
+    if (hit_distance > inside) return false;
+    t = t1 + RTW_DIV(hit_distance, ray_length);
+    return true;
+}
+
+// A non-sphere leaf tested with (0.001, closest): updates closest / hit
+// (hit = node | member << 24 for an instance's list member)
+template <uint32_t FEAT>
+__device__ __noinline__ void object_leaf(const rtw_launch& L, const Ray& r, uint32_t kind, uint32_t idx, uint32_t node,
+                                         float& closest, int& hit, uint64_t mkey) {
+    float t;
+    uint32_t sub = 0;
+    bool h = false;
+    if (kind == RTW_OBJ_QUAD) {
+        h = quad_t(L.quads[idx], r, kTmin, closest, t);
+    } else if (kind == RTW_OBJ_INSTANCE) {
+        const rtw_dev_instance in = L.insts[idx];
+        h = list_t<FEAT>(L, in, inst_to_object(in, r), kTmin, closest, t, sub);
+    } else if constexpr ((FEAT & RTW_F_MEDIUM) != 0) {
+        h = medium_t<FEAT>(L, idx, r, kTmin, closest, mkey, t);
+    }
+    if (h) {
+        closest = t;
+        hit = (int)(node | (sub << RTW_HIT_NODE_BITS));
+    }
+}
+
 // Node i of the pre-order walk: two 16-B loads issued together (both halves are
 // needed on either path; a split load would put a second memory round trip on
 // the inner-node path).
@@ -295,8 +485,15 @@ __device__ __forceinline__ void load_node(const float4* __restrict__ nodes, uint
 // no box test (bvh.zig:123-125).  Updates closest/hit.
 template <uint32_t FEAT>
 __device__ __forceinline__ void leaf_test(const rtw_launch& L, const Ray& r, const RayTrav& rt, float4 A, float4 B,
-                                          uint32_t i, float& closest, int& hit, Counters& cnt) {
+                                          uint32_t i, float& closest, int& hit, Counters& cnt, uint64_t mkey = 0) {
     cnt.leaves++;
+    if constexpr ((FEAT & RTW_F_GEOM) != 0) {
+        const uint32_t kind = RTW_LEAF_KIND(fbits(B.w));
+        if (kind != RTW_OBJ_SPHERE) {
+            object_leaf<FEAT>(L, r, kind, fbits(B.z), i, closest, hit, mkey);
+            return;
+        }
+    }
     f3 center = mk(A.x, A.y, A.z);
     if constexpr ((FEAT & RTW_F_MOVING) != 0) {
         if (fbits(B.w)) {  // Sphere.getCenter (objects.zig:94-98)
@@ -382,12 +579,12 @@ __device__ __forceinline__ uint32_t box_next(const Ray& r, const RayTrav& rt, fl
 template <uint32_t FEAT>
 __device__ __forceinline__ uint32_t trav_step(const float4* __restrict__ nodes, const rtw_launch& L, const Ray& r,
                                               const RayTrav& rt, uint32_t i, float& closest, int& hit,
-                                              Counters& cnt) {
+                                              Counters& cnt, uint64_t mkey = 0) {
     float4 A, B;
     load_node(nodes, i, A, B);
     const uint32_t w = fbits(A.w);
     if (w & RTW_LEAF_BIT) {
-        leaf_test<FEAT>(L, r, rt, A, B, i, closest, hit, cnt);
+        leaf_test<FEAT>(L, r, rt, A, B, i, closest, hit, cnt, mkey);
         return w & RTW_SKIP_MASK;
     }
     cnt.nodes++;
@@ -395,15 +592,16 @@ __device__ __forceinline__ uint32_t trav_step(const float4* __restrict__ nodes, 
 }
 
 // World hit for one ray (whole walk).  Returns leaf node index or -1.
+// mkey: the path's RNG state (keys ConstantMedium draws; unused without media)
 template <uint32_t FEAT>
 __device__ __forceinline__ int traverse(const float4* __restrict__ nodes, const rtw_launch& L, const Ray& r,
-                                        float& t_out, Counters& cnt) {
+                                        float& t_out, Counters& cnt, uint64_t mkey = 0) {
     const RayTrav rt = ray_trav(r, L.fast_box != 0);
     float closest = kInf;
     int hit = -1;
     uint32_t i = 0;
     const uint32_t n = L.n_nodes;
-    while (i < n) i = trav_step<FEAT>(nodes, L, r, rt, i, closest, hit, cnt);
+    while (i < n) i = trav_step<FEAT>(nodes, L, r, rt, i, closest, hit, cnt, mkey);
     t_out = closest;
     return hit;
 }
@@ -419,14 +617,83 @@ __device__ __forceinline__ f3 background(const rtw_launch& L, const Ray& r) {
 
 // Hit record for the closest hit (objects.zig:139-145) + the material.
 struct HitPrep {
-    f3 p, outward, normal;
+    f3 p, normal;
+    HitUV uv;
     bool front;
     rtw_dev_material m;
 };
 
+// hit record of a quad, in the frame of ray r (Quad.hit objects.zig:237-254)
+__device__ __forceinline__ void quad_prep(const rtw_dev_quad& q, const Ray& r, float t, HitPrep& h) {
+    h.p = r.o + splat(t) * r.d;
+    const f3 planar = h.p - ld3(q.q);
+    const f3 w = ld3(q.w);
+    h.uv.u = dot(w, cross(planar, ld3(q.v)));
+    h.uv.v = dot(w, cross(ld3(q.u), planar));
+    h.uv.set = true;
+    const f3 n = ld3(q.n);
+    h.front = dot(r.d, n) < 0;  // setFaceNormal (objects.zig:30-36)
+    h.normal = h.front ? n : -n;
+    h.uv.outward = n;
+}
+
+template <uint32_t FEAT>
+__device__ __noinline__ HitPrep object_prep(const rtw_launch& L, const Ray& r, uint32_t kind, uint32_t idx,
+                                            uint32_t sub, float t) {
+    HitPrep h;
+    if (kind == RTW_OBJ_QUAD) {
+        const rtw_dev_quad q = L.quads[idx];
+        quad_prep(q, r, t, h);
+        h.m = L.mats[q.mat];
+        return h;
+    }
+    if (kind == RTW_OBJ_INSTANCE) {
+        const rtw_dev_instance in = L.insts[idx];
+        const Ray ro = inst_to_object(in, r);
+        const uint32_t ref = L.members[in.first + sub];
+        const uint32_t mi = RTW_REF_INDEX(ref);
+        uint32_t mat;
+        if (RTW_REF_KIND(ref) == RTW_OBJ_SPHERE) {  // Sphere.hit record (objects.zig:138-147)
+            const rtw_dev_sphere s = L.sph[mi];
+            const f3 center = member_sphere_center<FEAT>(L, s, mi, ro.time);
+            h.p = ro.o + splat(t) * ro.d;
+            const f3 outward = divs(h.p - center, s.radius);
+            h.front = dot(ro.d, outward) < 0;
+            h.normal = h.front ? outward : -outward;
+            sphere_uv(outward, h.uv.u, h.uv.v);
+            h.uv.set = true;
+            h.uv.outward = outward;
+            mat = s.mat;
+        } else {
+            const rtw_dev_quad q = L.quads[mi];
+            quad_prep(q, ro, t, h);
+            mat = q.mat;
+        }
+        inst_to_world(in, h.p, h.normal);
+        h.m = L.mats[mat];
+        return h;
+    }
+    // ConstantMedium record (objects.zig:494-500)
+    h.p = r.o + splat(t) * r.d;
+    h.normal = mk(1, 0, 0);
+    h.front = true;
+    h.uv.outward = h.normal;
+    h.uv.u = 0;
+    h.uv.v = 0;
+    h.uv.set = true;
+    h.m = L.mats[L.media[idx].mat];
+    return h;
+}
+
 template <uint32_t FEAT>
 __device__ __forceinline__ HitPrep hit_prep(const float4* __restrict__ nodes, const rtw_launch& L, const Ray& r,
                                             int hit, float t) {
+    if constexpr ((FEAT & RTW_F_GEOM) != 0) {
+        const uint32_t node = (uint32_t)hit & ((1u << RTW_HIT_NODE_BITS) - 1u);
+        const float4 B = nodes[2 * node + 1];
+        const uint32_t kind = RTW_LEAF_KIND(fbits(B.w));
+        if (kind != RTW_OBJ_SPHERE) return object_prep<FEAT>(L, r, kind, fbits(B.z), (uint32_t)hit >> RTW_HIT_NODE_BITS, t);
+    }
     const float4 A = nodes[2 * hit];
     const float4 B = nodes[2 * hit + 1];
     f3 center = mk(A.x, A.y, A.z);
@@ -438,9 +705,11 @@ __device__ __forceinline__ HitPrep hit_prep(const float4* __restrict__ nodes, co
     }
     HitPrep h;
     h.p = r.o + splat(t) * r.d;
-    h.outward = divs(h.p - center, B.x);
-    h.front = dot(r.d, h.outward) < 0;
-    h.normal = h.front ? h.outward : -h.outward;
+    h.uv.outward = divs(h.p - center, B.x);
+    h.uv.set = false;
+    h.uv.u = h.uv.v = 0;
+    h.front = dot(r.d, h.uv.outward) < 0;
+    h.normal = h.front ? h.uv.outward : -h.uv.outward;
     h.m = L.mats[fbits(B.y)];
     return h;
 }
@@ -468,7 +737,7 @@ __device__ __forceinline__ bool scatter_finish(const rtw_launch& L, const Ray& r
         f3 dir = h.normal + ruv;
         if (near_zero(dir)) dir = h.normal;
         sc.d = dir;
-        att = texture_value<FEAT>(L, m.texture, h.outward, h.p);
+        att = texture_value<FEAT>(L, m.texture, h.uv, h.p);
         return true;
     }
     case RTW_MAT_METAL: {  // material.zig:65-70
@@ -496,12 +765,12 @@ __device__ __forceinline__ bool scatter_finish(const rtw_launch& L, const Ray& r
     }
     if constexpr ((FEAT & RTW_F_LIGHT) != 0) {
         if (m.kind == RTW_MAT_DIFFUSE_LIGHT) {  // material.zig:119-125
-            acc = acc + thr * texture_value<FEAT>(L, m.texture, h.outward, h.p);
+            acc = acc + thr * texture_value<FEAT>(L, m.texture, h.uv, h.p);
             return false;
         }
         // RTW_MAT_ISOTROPIC (material.zig:139-143)
         sc.d = ruv;
-        att = texture_value<FEAT>(L, m.texture, h.outward, h.p);
+        att = texture_value<FEAT>(L, m.texture, h.uv, h.p);
         return true;
     }
     return false;
@@ -640,7 +909,7 @@ __device__ f3 sample_radiance(const float4* __restrict__ nodes, const rtw_launch
     for (uint32_t depth = L.max_depth; depth > 0; depth--) {
         cnt.rays++;
         float t;
-        const int hit = traverse<FEAT>(nodes, L, r, t, cnt);
+        const int hit = traverse<FEAT>(nodes, L, r, t, cnt, rng.s);
         if (hit < 0) {
             acc = acc + thr * background(L, r);
             break;

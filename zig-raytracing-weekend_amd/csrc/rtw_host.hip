@@ -138,7 +138,8 @@ int rtw_camera_init(const rtw_camera_params* p, rtw_camera* c) {
 int rtw_scene_create(const rtw_scene_desc* d, int device, rtw_ctx** out) {
     if (!d || !out) return fail(RTW_E_INVALID, "null scene desc");
     *out = nullptr;
-    if (d->n_spheres == 0 || !d->spheres) return fail(RTW_E_INVALID, "scene has no spheres");
+    if ((d->n_spheres && !d->spheres) || (d->objects ? d->n_objects : d->n_spheres) == 0)
+        return fail(RTW_E_INVALID, "scene has no objects");
     if (d->n_materials == 0 || !d->materials) return fail(RTW_E_INVALID, "scene has no materials");
     for (uint32_t i = 0; i < d->n_spheres; i++)
         if (d->spheres[i].material >= d->n_materials) return fail(RTW_E_INVALID, "sphere material index out of range");
@@ -165,20 +166,31 @@ int rtw_scene_create(const rtw_scene_desc* d, int device, rtw_ctx** out) {
 
     rtw_ctx* ctx = new rtw_ctx();
     ctx->device = device;
-    std::vector<float> cvec;
+    rtw_geometry geom;
     uint32_t depth = 0, draws = 0;
-    int rc = rtw_build_bvh(*d, ctx->nodes_host, cvec, &depth, &draws, &ctx->box_pad, &ctx->extent);
+    int rc = rtw_build_bvh(*d, ctx->nodes_host, geom, &depth, &draws, &ctx->box_pad, &ctx->extent);
     if (rc != RTW_OK) {
         delete ctx;
-        return fail(rc, "BVH build failed (unknown bvh_mode?)");
+        return fail(rc, "BVH build failed (bad object graph or bvh_mode)");
     }
+    if ((geom.feat & RTW_F_GEOM) && ctx->nodes_host.size() >= (1u << RTW_HIT_NODE_BITS)) {
+        delete ctx;
+        return fail(RTW_E_INVALID, "scenes with instances are limited to 2^24 BVH nodes");
+    }
+    const std::vector<float>& cvec = geom.cvec;
 
-    // Blob layout (each section 256-B aligned): nodes | cvec | materials | textures | images-info | perlin | image bytes
+    // Blob layout (each section 256-B aligned): nodes | cvec | spheres | quads | members | instances | media |
+    // materials | textures | images-info | perlin | image bytes
     auto align = [](size_t x) { return (x + 255) & ~size_t(255); };
     const size_t n_nodes = ctx->nodes_host.size();
     size_t off = 0;
     const size_t o_nodes = off; off = align(off + n_nodes * sizeof(rtw_node));
     const size_t o_cvec = off; off = align(off + cvec.size() * sizeof(float) + 16);
+    const size_t o_sph = off; off = align(off + geom.spheres.size() * sizeof(rtw_dev_sphere) + 16);
+    const size_t o_quad = off; off = align(off + geom.quads.size() * sizeof(rtw_dev_quad) + 16);
+    const size_t o_memb = off; off = align(off + geom.members.size() * sizeof(uint32_t) + 16);
+    const size_t o_inst = off; off = align(off + geom.insts.size() * sizeof(rtw_dev_instance) + 16);
+    const size_t o_med = off; off = align(off + geom.media.size() * sizeof(rtw_dev_medium) + 16);
     const size_t o_mats = off; off = align(off + d->n_materials * sizeof(rtw_dev_material));
     const size_t o_texs = off; off = align(off + (d->n_textures + 1) * sizeof(rtw_dev_texture));
     const size_t o_imgi = off; off = align(off + (d->n_images + 1) * sizeof(rtw_dev_image));
@@ -197,7 +209,15 @@ int rtw_scene_create(const rtw_scene_desc* d, int device, rtw_ctx** out) {
 
     std::vector<uint8_t> blob(off, 0);
     std::memcpy(blob.data() + o_nodes, ctx->nodes_host.data(), n_nodes * sizeof(rtw_node));
-    if (!cvec.empty()) std::memcpy(blob.data() + o_cvec, cvec.data(), cvec.size() * sizeof(float));
+    auto put = [&](size_t o, const void* src, size_t nb) {
+        if (nb) std::memcpy(blob.data() + o, src, nb);
+    };
+    put(o_cvec, cvec.data(), cvec.size() * sizeof(float));
+    put(o_sph, geom.spheres.data(), geom.spheres.size() * sizeof(rtw_dev_sphere));
+    put(o_quad, geom.quads.data(), geom.quads.size() * sizeof(rtw_dev_quad));
+    put(o_memb, geom.members.data(), geom.members.size() * sizeof(uint32_t));
+    put(o_inst, geom.insts.data(), geom.insts.size() * sizeof(rtw_dev_instance));
+    put(o_med, geom.media.data(), geom.media.size() * sizeof(rtw_dev_medium));
     for (uint32_t i = 0; i < d->n_materials; i++) {
         rtw_dev_material m{};
         m.kind = d->materials[i].kind;
@@ -254,6 +274,11 @@ int rtw_scene_create(const rtw_scene_desc* d, int device, rtw_ctx** out) {
     rtw_launch& L = ctx->base;
     L.nodes = reinterpret_cast<const float4*>(dev + o_nodes);
     L.cvec = reinterpret_cast<const float4*>(dev + o_cvec);
+    L.sph = reinterpret_cast<const rtw_dev_sphere*>(dev + o_sph);
+    L.quads = reinterpret_cast<const rtw_dev_quad*>(dev + o_quad);
+    L.members = reinterpret_cast<const uint32_t*>(dev + o_memb);
+    L.insts = reinterpret_cast<const rtw_dev_instance*>(dev + o_inst);
+    L.media = reinterpret_cast<const rtw_dev_medium*>(dev + o_med);
     L.mats = reinterpret_cast<const rtw_dev_material*>(dev + o_mats);
     L.texs = reinterpret_cast<const rtw_dev_texture*>(dev + o_texs);
     L.img_info = reinterpret_cast<const rtw_dev_image*>(dev + o_imgi);
@@ -261,7 +286,7 @@ int rtw_scene_create(const rtw_scene_desc* d, int device, rtw_ctx** out) {
     L.images = dev + o_imgs;
     L.n_nodes = (uint32_t)n_nodes;
     L.n_perlin = d->n_perlins;
-    ctx->feat = scene_features(d);
+    ctx->feat = scene_features(d) | geom.feat;
     L.feat = ctx->feat;
     L.work_counter = ctx->d_work;
     if (const char* kv = std::getenv("RTW_KERNEL"))
@@ -315,8 +340,8 @@ int rtw_scene_create(const rtw_scene_desc* d, int device, rtw_ctx** out) {
     ctx->grid = rtw_persistent_grid(ctx->feat, (uint32_t)n_nodes, (int)L.waves, L.use_lds != 0);
 
     ctx->stats.n_nodes = (uint32_t)n_nodes;
-    ctx->stats.n_leaves = d->n_spheres;
-    ctx->stats.n_inner = (uint32_t)n_nodes - d->n_spheres;
+    ctx->stats.n_leaves = d->objects ? d->n_objects : d->n_spheres;
+    ctx->stats.n_inner = (uint32_t)n_nodes - ctx->stats.n_leaves;
     ctx->stats.depth = depth;
     ctx->stats.device_bytes = off;
     ctx->stats.axis_draws = draws;
@@ -339,11 +364,12 @@ void rtw_scene_destroy(rtw_ctx* ctx) {
 }
 
 int rtw_scene_flatten(const rtw_scene_desc* d, void* out, uint32_t cap, uint32_t* n_out, uint32_t* depth_out) {
-    if (!d || d->n_spheres == 0 || !d->spheres) return fail(RTW_E_INVALID, "scene has no spheres");
+    if (!d || (d->n_spheres && !d->spheres) || (d->objects ? d->n_objects : d->n_spheres) == 0)
+        return fail(RTW_E_INVALID, "scene has no objects");
     std::vector<rtw_node> nodes;
-    std::vector<float> cvec;
+    rtw_geometry geom;
     uint32_t depth = 0, draws = 0;
-    int rc = rtw_build_bvh(*d, nodes, cvec, &depth, &draws);
+    int rc = rtw_build_bvh(*d, nodes, geom, &depth, &draws);
     if (rc != RTW_OK) return fail(rc, "BVH build failed");
     const uint32_t n = (uint32_t)nodes.size();
     if (n_out) *n_out = n;

@@ -17,6 +17,11 @@ struct rtw_launch {
     // scene (device pointers)
     const float4* nodes;
     const float4* cvec;          // per-sphere center_vec (moving spheres)
+    const rtw_dev_sphere* sph;   // every sphere (instance members)
+    const rtw_dev_quad* quads;
+    const rtw_dev_instance* insts;
+    const uint32_t* members;
+    const rtw_dev_medium* media;
     const rtw_dev_material* mats;
     const rtw_dev_texture* texs;
     const uint8_t* images;
@@ -70,7 +75,10 @@ struct rtw_launch {
 #define RTW_F_NOISE 4u
 #define RTW_F_MOVING 8u
 #define RTW_F_LIGHT 16u
-#define RTW_F_ALL 31u
+#define RTW_F_GEOM 32u      // quads / instances (non-sphere BVH leaves)
+#define RTW_F_MEDIUM 64u    // ConstantMedium leaves
+#define RTW_F_SPHERES 31u   // every sphere-scene feature
+#define RTW_F_ALL 127u
 
 // max nodes staged in LDS by the persistent kernel (48 KiB)
 #define RTW_LDS_NODES 1536
@@ -120,9 +128,21 @@ struct rtw_timer {
 #define RTW_TIME_END(T) \
     if (T) (T)->end();
 
-// box_pad/extent (out, may be null): SAH trees pad every inner box by
-// extent * 2^-19 so the FMA slab test (rtw_kernels.hip box_next) stays conservative.
-int rtw_build_bvh(const rtw_scene_desc& desc, std::vector<rtw_node>& nodes, std::vector<float>& cvec,
+// Host copies of the device geometry arrays besides the nodes (rtw_layout.h records).
+struct rtw_geometry {
+    std::vector<float> cvec;                 // float4 per sphere: center_vec (moving spheres)
+    std::vector<rtw_dev_sphere> spheres;     // every sphere
+    std::vector<rtw_dev_quad> quads;
+    std::vector<rtw_dev_instance> insts;
+    std::vector<uint32_t> members;           // RTW_REF
+    std::vector<rtw_dev_medium> media;
+    uint32_t feat = 0;                       // RTW_F_GEOM | RTW_F_MEDIUM as present
+};
+
+// Validates the object graph, derives the geometry records and builds the BVH
+// over world_objects.  box_pad/extent (out, may be null): SAH trees pad every
+// inner box by extent * 2^-19 so the FMA slab test (box_next) stays conservative.
+int rtw_build_bvh(const rtw_scene_desc& desc, std::vector<rtw_node>& nodes, rtw_geometry& geom,
                   uint32_t* depth, uint32_t* axis_draws, float* box_pad = nullptr, float* extent = nullptr);
 
 // One scene on one device (the opaque rtw_ctx of include/rtw_gpu.h).

@@ -249,7 +249,7 @@ __global__ __launch_bounds__(256, WAVES) void render_persistent_v1(rtw_launch L)
                         if (st == ST_TRAV && pend >= 0) {
                             float4 A, B;
                             load_node(nodes, (uint32_t)pend, A, B);
-                            leaf_test<FEAT>(L, ray, rt, A, B, (uint32_t)pend, closest, hit, cnt);
+                            leaf_test<FEAT>(L, ray, rt, A, B, (uint32_t)pend, closest, hit, cnt, rng.s);
                             pend = -1;
                             if (ti >= n_nodes) st = ST_SHADE;
                         }
@@ -258,7 +258,7 @@ __global__ __launch_bounds__(256, WAVES) void render_persistent_v1(rtw_launch L)
 #pragma unroll
                     for (int u = 0; u < RTW_STEPS; u++) {
                         if (st == ST_TRAV) {
-                            ti = trav_step<FEAT>(nodes, L, ray, rt, ti, closest, hit, cnt);
+                            ti = trav_step<FEAT>(nodes, L, ray, rt, ti, closest, hit, cnt, rng.s);
                             if (ti >= n_nodes) st = ST_SHADE;
                         }
                     }
@@ -391,7 +391,7 @@ __global__ void debug_sample_kernel(rtw_launch L, uint32_t pixel, uint32_t sampl
     for (uint32_t depth = L.max_depth; depth > 0; depth--, bounce++) {
         debug_filter_check(L, r, out);
         float t;
-        const int hit = traverse<RTW_F_ALL>(L.nodes, L, r, t, cnt);
+        const int hit = traverse<RTW_F_ALL>(L.nodes, L, r, t, cnt, rng.s);
         // brute-force exact closest over all leaves
         {
             const RayTrav rt = ray_trav(r, L.fast_box != 0);
@@ -439,23 +439,19 @@ int occupancy_v1(size_t lds_bytes) {
     return b < 1 ? 1 : b;
 }
 
-// waves-per-SIMD launch-bound variants (RTW_WAVES): 1 = compiler's choice, 6, 8
 uint32_t pick_feat(uint32_t f) {
     if ((f & ~RTW_F_CHECKER) == 0) return f ? RTW_F_CHECKER : 0u;
     return RTW_F_ALL;
 }
 
 
+// (launch-bound variants forcing 6 or 8 waves/SIMD spilled and were slower: removed)
 template <uint32_t FEAT, bool LDS>
-void launch_waves(const rtw_launch& L, hipStream_t st, int grid, int waves) {
-    if (waves >= 8) launch_v1<FEAT, LDS, 8>(L, st, grid);
-    else if (waves >= 6) launch_v1<FEAT, LDS, 6>(L, st, grid);
-    else launch_v1<FEAT, LDS, 1>(L, st, grid);
+void launch_waves(const rtw_launch& L, hipStream_t st, int grid, int) {
+    launch_v1<FEAT, LDS, 1>(L, st, grid);
 }
 template <uint32_t FEAT, bool LDS>
-int occ_waves(size_t lds, int waves) {
-    if (waves >= 8) return occupancy_v1<FEAT, LDS, 8>(lds);
-    if (waves >= 6) return occupancy_v1<FEAT, LDS, 6>(lds);
+int occ_waves(size_t lds, int) {
     return occupancy_v1<FEAT, LDS, 1>(lds);
 }
 

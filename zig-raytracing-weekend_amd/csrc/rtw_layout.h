@@ -26,6 +26,52 @@ struct rtw_node {
 };
 static_assert(sizeof(rtw_node) == 32, "node must be 32 bytes");
 
+// Leaf b.w: bit 0 = moving sphere, bits 8..15 = object kind (RTW_OBJ_*).  Non-sphere
+// leaves: a = (0, 0, 0, bits(skip | LEAF_BIT)), b = (0, bits(mat), bits(index), bits(kind << 8)).
+#define RTW_LEAF_KIND(bw) (((bw) >> 8) & 0xFFu)
+// object reference inside the device arrays: kind in the top 4 bits
+#define RTW_REF(kind, idx) (((uint32_t)(kind) << 28) | (uint32_t)(idx))
+#define RTW_REF_KIND(r) ((r) >> 28)
+#define RTW_REF_INDEX(r) ((r) & 0x0FFFFFFFu)
+// hit id of a closest hit: leaf node | instance member << 24
+#define RTW_HIT_NODE_BITS 24
+
+// 32 B: every sphere (instance members read these; world-object spheres are inlined in their leaf)
+struct rtw_dev_sphere {
+    float c1[3];
+    float radius;
+    uint32_t mat, moving, _p0, _p1;
+};
+static_assert(sizeof(rtw_dev_sphere) == 32, "sphere record must be 32 bytes");
+
+// 80 B: Quad.init derived fields (objects.zig:201-210)
+struct rtw_dev_quad {
+    float q[3];
+    float d;
+    float n[3];
+    uint32_t mat;
+    float u[4];
+    float v[4];
+    float w[4];
+};
+static_assert(sizeof(rtw_dev_quad) == 80, "quad record must be 80 bytes");
+
+// 64 B: members[first .. first+count) (RTW_REF), xf[k] = {bits(kind), a, b, c}:
+// translate (a, b, c) = offset; rotate_y a = sin, b = cos.  xf[0] innermost.
+struct rtw_dev_instance {
+    uint32_t first, count, n_xf, _p;
+    float xf[3][4];
+};
+static_assert(sizeof(rtw_dev_instance) == 64, "instance record must be 64 bytes");
+
+// 16 B: ConstantMedium
+struct rtw_dev_medium {
+    uint32_t boundary;       // RTW_REF
+    float neg_inv_density;
+    uint32_t mat;
+    uint32_t _p;
+};
+
 // 32 B: {kind, texture, fuzz, ir} {albedo.xyz, 0}
 struct rtw_dev_material {
     uint32_t kind;

@@ -84,3 +84,13 @@ RTW_HD float rtw_rng_float(rtw_rng& r) {
 
 // rtweekend.zig:18-20
 RTW_HD float rtw_rng_range(rtw_rng& r, float mn, float mx) { return mn + (mx - mn) * rtw_rng_float(r); }
+
+// ConstantMedium.hit's one draw (objects.zig:484), keyed instead of sequential so
+// it does not depend on the order the BVH visits leaves: a float from the stream
+// started at mix64(path_state ^ K * (medium + 1)), path_state = the path's RNG
+// state at the traversal.
+RTW_HD float rtw_medium_u(uint64_t path_state, uint32_t medium) {
+    rtw_rng r;
+    r.s = rtw_mix64(path_state ^ (0xD1B54A32D192ED03ull * (uint64_t)(medium + 1)));
+    return rtw_rng_float(r);
+}

@@ -92,6 +92,13 @@ __device__ __forceinline__ void wf_push(const rtw_wf& W, uint32_t it, bool push,
     }
 }
 
+// the path's RNG state keys ConstantMedium draws (only read in scenes with media)
+template <uint32_t FEAT>
+__device__ __forceinline__ uint64_t wf_mkey(const rtw_wf& W, uint32_t p) {
+    if constexpr ((FEAT & RTW_F_MEDIUM) != 0) return W.rng[p];
+    return 0;
+}
+
 __device__ __forceinline__ Ray wf_load_ray(const rtw_wf& W, uint32_t p, uint32_t& depth) {
     const float4 o = W.ray_o[p], d = W.ray_d[p];
     Ray r;
@@ -177,6 +184,7 @@ __global__ __launch_bounds__(256) void wf_trace(rtw_launch L, rtw_wf W, uint32_t
         const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
         const bool fast = L.fast_box != 0;
         uint32_t cursor = 0, p = 0, ti = 0;
+        uint64_t mkey = 0;
         bool active = false, exhausted = false;
         Ray r;
         r.o = r.d = mk(0, 0, 0);
@@ -199,6 +207,7 @@ __global__ __launch_bounds__(256) void wf_trace(rtw_launch L, rtw_wf W, uint32_t
                     r = wf_load_ray(W, q, depth);
                     if (depth) {
                         p = q;
+                        mkey = wf_mkey<FEAT>(W, q);
                         rt = ray_trav(r, fast);
                         ti = 0;
                         closest = kInf;
@@ -213,7 +222,7 @@ __global__ __launch_bounds__(256) void wf_trace(rtw_launch L, rtw_wf W, uint32_t
                 continue;
             }
             if (active) {
-                ti = trav_step<FEAT>(L.nodes, L, r, rt, ti, closest, hit, cnt);
+                ti = trav_step<FEAT>(L.nodes, L, r, rt, ti, closest, hit, cnt, mkey);
                 if (ti >= L.n_nodes) {
                     W.hit[p] = make_float2(closest, __int_as_float(hit));
                     active = false;
@@ -230,7 +239,7 @@ __global__ __launch_bounds__(256) void wf_trace(rtw_launch L, rtw_wf W, uint32_t
             const Ray r = wf_load_ray(W, p, depth);
             if (depth) {
                 float t;
-                const int h = traverse<FEAT>(L.nodes, L, r, t, cnt);
+                const int h = traverse<FEAT>(L.nodes, L, r, t, cnt, wf_mkey<FEAT>(W, p));
                 W.hit[p] = make_float2(t, __int_as_float(h));
                 cnt.rays++;
             }
@@ -312,7 +321,7 @@ __global__ __launch_bounds__(256) void wf_tail(rtw_launch L, rtw_wf W, uint32_t 
             cnt.rays++;
             cnt.tail_rays++;
             float t;
-            const int hit = traverse<FEAT>(L.nodes, L, r, t, cnt);
+            const int hit = traverse<FEAT>(L.nodes, L, r, t, cnt, rng.s);
             bool done = true;
             if (hit < 0) {
                 acc = acc + thr * background(L, r);
@@ -410,7 +419,7 @@ void wf_run(const rtw_launch& L, const rtw_wf& W, hipStream_t st, int n_cu, rtw_
 
 uint32_t wf_pick_feat(uint32_t f) {
     if ((f & ~RTW_F_CHECKER) == 0) return f ? RTW_F_CHECKER : 0u;
-    return RTW_F_ALL;
+    return (f & (RTW_F_GEOM | RTW_F_MEDIUM)) ? RTW_F_ALL : RTW_F_SPHERES;
 }
 
 }  // namespace
@@ -420,13 +429,15 @@ void rtw_wavefront_batch(const rtw_launch& L, const rtw_wf& W, void* stream, int
     switch (wf_pick_feat(L.feat)) {
     case 0u: wf_run<0u>(L, W, st, n_cu, T); break;
     case RTW_F_CHECKER: wf_run<RTW_F_CHECKER>(L, W, st, n_cu, T); break;
+    case RTW_F_SPHERES: wf_run<RTW_F_SPHERES>(L, W, st, n_cu, T); break;
     default: wf_run<RTW_F_ALL>(L, W, st, n_cu, T); break;
     }
 }
 
 uint32_t rtw_wavefront_max_waves(int n_cu) {
     uint32_t m = 0;
-    for (uint32_t g : {wf_grids<0u>(n_cu).shade, wf_grids<RTW_F_CHECKER>(n_cu).shade, wf_grids<RTW_F_ALL>(n_cu).shade})
+    for (uint32_t g : {wf_grids<0u>(n_cu).shade, wf_grids<RTW_F_CHECKER>(n_cu).shade,
+                       wf_grids<RTW_F_SPHERES>(n_cu).shade, wf_grids<RTW_F_ALL>(n_cu).shade})
         m = g > m ? g : m;
     return 4 * m;
 }

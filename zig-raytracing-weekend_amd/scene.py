@@ -7,6 +7,9 @@ Reference types (all by value in Zig) and their mirrors here:
 * ``Material`` union (src/material.zig:11-30): ``Lambertian``, ``Metal``,
   ``Dielectric``, ``DiffuseLight``, ``Isotropic``
 * ``Sphere`` (src/objects.zig:68-149): ``Sphere.init`` / ``Sphere.initMoving``
+* ``Quad`` (src/objects.zig:193-262), ``HittableList`` (:264-290), ``Translate``
+  (:292-331), ``RotateY`` (:333-443), ``ConstantMedium`` (:445-508) and
+  ``createBox`` (:510-532)
 * ``BVHTree`` (src/bvh.zig:17-104): ``BVHTree.init(objects, start, end)`` --
   flattens the objects to the C-ABI records (include/rtw_gpu.h) and hands them
   to ``rtw_scene_create``, which builds the reference-topology BVH natively
@@ -199,6 +202,89 @@ class Sphere:
         return Sphere(_v3(center1), f32(radius), mat, True, _v3(center2))
 
 
+@dataclass(eq=False)
+class Quad:
+    """Quad.init (objects.zig:201-210); the library derives normal, d, w and the box."""
+    q: np.ndarray
+    u: np.ndarray
+    v: np.ndarray
+    mat: Material
+
+    @staticmethod
+    def init(q, u, v, mat: Material) -> "Quad":
+        return Quad(_v3(q), _v3(u), _v3(v), mat)
+
+
+@dataclass(eq=False)
+class HittableList:
+    """objects.zig:264-290 (members: Spheres / Quads)."""
+    objects: list = field(default_factory=list)
+
+    @staticmethod
+    def init() -> "HittableList":
+        return HittableList([])
+
+    def add(self, obj) -> None:
+        self.objects.append(obj)
+
+
+@dataclass(eq=False)
+class Translate:
+    """objects.zig:292-331."""
+    object: object
+    offset: np.ndarray
+
+    @staticmethod
+    def init(obj, offset) -> "Translate":
+        return Translate(obj, _v3(offset))
+
+
+@dataclass(eq=False)
+class RotateY:
+    """objects.zig:333-443 (sin/cos of degreesToRadians(angle), computed by the library)."""
+    object: object
+    angle: np.float32
+
+    @staticmethod
+    def init(obj, angle) -> "RotateY":
+        return RotateY(obj, f32(angle))
+
+
+@dataclass(eq=False)
+class ConstantMedium:
+    """objects.zig:445-508: boundary + density + Isotropic phase function."""
+    boundary: object
+    density: np.float32
+    phase: Material
+
+    @staticmethod
+    def initFromColor(boundary, density, color) -> "ConstantMedium":
+        return ConstantMedium(boundary, f32(density), Isotropic.init(SolidColor.init(color)))
+
+    @staticmethod
+    def initFromTexture(boundary, density, texture: Texture) -> "ConstantMedium":
+        return ConstantMedium(boundary, f32(density), Isotropic.init(texture))
+
+
+def createBox(a, b, mat: Material) -> HittableList:
+    """objects.zig:510-532: the six sides of the box with opposite vertices a, b."""
+    a, b = _v3(a), _v3(b)
+    mn = np.minimum(a, b)
+    mx = np.maximum(a, b)
+    z = np.float32(0)
+    dx = np.array([mx[0] - mn[0], z, z], np.float32)
+    dy = np.array([z, mx[1] - mn[1], z], np.float32)
+    dz = np.array([z, z, mx[2] - mn[2]], np.float32)
+    sides = HittableList.init()
+    sides.add(Quad.init([mn[0], mn[1], mn[2]], dx, dy, mat))
+    sides.add(Quad.init([mx[0], mn[1], mx[2]], -dz, dy, mat))
+    sides.add(Quad.init([mx[0], mn[1], mn[2]], -dx, dy, mat))
+    sides.add(Quad.init([mn[0], mn[1], mn[2]], dz, dy, mat))
+    sides.add(Quad.init([mn[0], mx[1], mx[2]], dx, -dz, mat))
+    sides.add(Quad.init([mn[0], mn[1], mn[2]], dx, dz, mat))
+    return sides
+
+
 @dataclass
 class SceneArrays:
     """The neutral scene description handed across the C ABI."""
@@ -210,6 +296,11 @@ class SceneArrays:
     bvh_seed: int = 0
     bvh_mode: int = _abi.RTW_BVH_SAH   # or _abi.RTW_BVH_REFERENCE (bvh.zig topology, same closest hits)
     order_dir: tuple = (0.0, 0.0, 0.0)
+    quads: np.ndarray = field(default_factory=lambda: np.zeros(0, _abi.QUAD_DT))
+    members: np.ndarray = field(default_factory=lambda: np.zeros(0, _abi.OBJECT_DT))
+    instances: np.ndarray = field(default_factory=lambda: np.zeros(0, _abi.INSTANCE_DT))
+    media: np.ndarray = field(default_factory=lambda: np.zeros(0, _abi.MEDIUM_DT))
+    objects: Optional[np.ndarray] = None   # world_objects order; None = every sphere in order
 
     def desc(self):
         """Build an RtwSceneDesc (keeps the ctypes image array alive on self)."""
@@ -229,13 +320,25 @@ class SceneArrays:
         d.bvh_seed = self.bvh_seed
         d.bvh_mode = self.bvh_mode
         d.order_dir[:] = list(self.order_dir)
+        d.quads, d.n_quads = _abi.ptr(self.quads), len(self.quads)
+        d.members, d.n_members = _abi.ptr(self.members), len(self.members)
+        d.instances, d.n_instances = _abi.ptr(self.instances), len(self.instances)
+        d.media, d.n_media = _abi.ptr(self.media), len(self.media)
+        if self.objects is not None:
+            d.objects, d.n_objects = _abi.ptr(self.objects), len(self.objects)
         return d
 
 
-def flatten(objects: Sequence[Sphere], bvh_seed: int = 0, bvh_mode: Optional[int] = None) -> SceneArrays:
-    """Objects -> C-ABI records.  bvh_mode: RTW_BVH_SAH (default, fastest) or
-    RTW_BVH_REFERENCE (the reference's random-axis median tree, seeded by bvh_seed)."""
-    sp = np.zeros(len(objects), _abi.SPHERE_DT)
+def flatten(objects: Sequence, bvh_seed: int = 0, bvh_mode: Optional[int] = None) -> SceneArrays:
+    """world_objects -> C-ABI records.  bvh_mode: RTW_BVH_SAH (default, fastest) or
+    RTW_BVH_REFERENCE (the reference's random-axis median tree, seeded by bvh_seed).
+
+    Every primitive gets its own material record (and textured materials their own
+    texture record), in object order; Perlin tables and images are shared by identity.
+    Translate/RotateY chains over a HittableList (or one primitive) become an
+    instance; a ConstantMedium's boundary is a sphere, quad or instance record that
+    is not itself a world object."""
+    spheres, quads, members, instances, media, objs = [], [], [], [], [], []
     mats, texs, perlins, images = [], [], [], []
 
     def tex_index(t: Texture) -> int:
@@ -263,8 +366,7 @@ def flatten(objects: Sequence[Sphere], bvh_seed: int = 0, bvh_mode: Optional[int
         texs.append(rec)
         return len(texs) - 1
 
-    for i, s in enumerate(objects):
-        m = s.mat
+    def mat_index(m: Material) -> int:
         rec = np.zeros((), _abi.MATERIAL_DT)
         rec["kind"] = m.kind
         if m.texture is not None:
@@ -273,19 +375,81 @@ def flatten(objects: Sequence[Sphere], bvh_seed: int = 0, bvh_mode: Optional[int
         rec["fuzz"] = m.fuzz
         rec["ir"] = m.ir
         mats.append(rec)
-        sp[i]["center1"] = s.center1
-        sp[i]["radius"] = s.radius
-        if s.is_moving:
-            sp[i]["center2"] = s.center2
-            sp[i]["is_moving"] = 1
-        sp[i]["material"] = len(mats) - 1
+        return len(mats) - 1
+
+    def prim(o) -> tuple:
+        if isinstance(o, Sphere):
+            rec = np.zeros((), _abi.SPHERE_DT)
+            rec["center1"] = o.center1
+            rec["radius"] = o.radius
+            if o.is_moving:
+                rec["center2"] = o.center2
+                rec["is_moving"] = 1
+            rec["material"] = mat_index(o.mat)
+            spheres.append(rec)
+            return (_abi.RTW_OBJ_SPHERE, len(spheres) - 1)
+        if isinstance(o, Quad):
+            rec = np.zeros((), _abi.QUAD_DT)
+            rec["q"], rec["u"], rec["v"] = o.q, o.u, o.v
+            rec["material"] = mat_index(o.mat)
+            quads.append(rec)
+            return (_abi.RTW_OBJ_QUAD, len(quads) - 1)
+        raise TypeError(f"not a primitive: {type(o).__name__}")
+
+    def hittable(o) -> tuple:
+        if isinstance(o, (Sphere, Quad)):
+            return prim(o)
+        if isinstance(o, (Translate, RotateY, HittableList)):
+            xfs = []
+            while isinstance(o, (Translate, RotateY)):   # outermost first
+                if isinstance(o, Translate):
+                    xfs.append((_abi.RTW_XF_TRANSLATE, o.offset))
+                else:
+                    xfs.append((_abi.RTW_XF_ROTATE_Y, np.array([o.angle, 0, 0], np.float32)))
+                o = o.object
+            if len(xfs) > _abi.RTW_MAX_XF:
+                raise ValueError(f"at most {_abi.RTW_MAX_XF} transforms per instance")
+            inner = o.objects if isinstance(o, HittableList) else [o]
+            rec = np.zeros((), _abi.INSTANCE_DT)
+            rec["first"] = len(members)
+            refs = [prim(m) for m in inner]
+            for k, i in refs:
+                members.append(np.array((k, i), _abi.OBJECT_DT))
+            rec["count"] = len(refs)
+            rec["n_xf"] = len(xfs)
+            rec["flags"] = _abi.RTW_INST_LIST if isinstance(o, HittableList) else 0
+            for j, (k, v) in enumerate(reversed(xfs)):    # xf[0] = innermost
+                rec["xf"][j]["kind"] = k
+                rec["xf"][j]["v"] = v
+            instances.append(rec)
+            return (_abi.RTW_OBJ_INSTANCE, len(instances) - 1)
+        if isinstance(o, ConstantMedium):
+            rec = np.zeros((), _abi.MEDIUM_DT)
+            k, i = hittable(o.boundary)
+            rec["boundary"]["kind"], rec["boundary"]["index"] = k, i
+            rec["density"] = o.density
+            rec["material"] = mat_index(o.phase)
+            media.append(rec)
+            return (_abi.RTW_OBJ_MEDIUM, len(media) - 1)
+        raise TypeError(f"unsupported hittable: {type(o).__name__}")
+
+    for o in objects:
+        objs.append(hittable(o))
     pl = np.zeros(len(perlins), _abi.PERLIN_DT)
     for i, p in enumerate(perlins):
         pl[i]["ranvec"] = p.ranvec
         pl[i]["perm_x"], pl[i]["perm_y"], pl[i]["perm_z"] = p.perm_x, p.perm_y, p.perm_z
-    return SceneArrays(sp, np.array(mats, _abi.MATERIAL_DT).reshape(-1),
-                       np.array(texs, _abi.TEXTURE_DT).reshape(-1), pl, images, bvh_seed,
-                       _abi.RTW_BVH_SAH if bvh_mode is None else bvh_mode)
+
+    def arr(lst, dt):
+        return np.array(lst, dt).reshape(-1) if lst else np.zeros(0, dt)
+
+    only_spheres = all(k == _abi.RTW_OBJ_SPHERE and i == n for n, (k, i) in enumerate(objs)) and \
+        len(objs) == len(spheres)
+    return SceneArrays(arr(spheres, _abi.SPHERE_DT), arr(mats, _abi.MATERIAL_DT), arr(texs, _abi.TEXTURE_DT), pl,
+                       images, bvh_seed, _abi.RTW_BVH_SAH if bvh_mode is None else bvh_mode,
+                       quads=arr(quads, _abi.QUAD_DT), members=arr(members, _abi.OBJECT_DT),
+                       instances=arr(instances, _abi.INSTANCE_DT), media=arr(media, _abi.MEDIUM_DT),
+                       objects=None if only_spheres else arr(objs, _abi.OBJECT_DT))
 
 
 def flatten_bvh(arrays: SceneArrays) -> np.ndarray:
@@ -343,7 +507,7 @@ class BVHTree:
     """bvh.zig:17-41 -- ``BVHTree.init(objects, start, end)`` returns a World."""
 
     @staticmethod
-    def init(objects: Sequence[Sphere], start: int = 0, end: Optional[int] = None, seed: int = 0,
+    def init(objects: Sequence, start: int = 0, end: Optional[int] = None, seed: int = 0,
              device: int = 0, bvh_mode: Optional[int] = None) -> World:
         end = len(objects) if end is None else end
         return World(flatten(list(objects[start:end]), bvh_seed=seed, bvh_mode=bvh_mode), device)

@@ -13,8 +13,8 @@ from typing import List, Optional, Sequence
 import numpy as np
 
 from .rng import DOMAIN_SCENE, Stream, f32
-from .scene import (CheckerTexture, Dielectric, Image, ImageTexture, Lambertian, Metal, NoiseTexture, Perlin,
-                    SolidColor, Sphere)
+from .scene import (CheckerTexture, ConstantMedium, Dielectric, DiffuseLight, Image, ImageTexture, Lambertian,
+                    Metal, NoiseTexture, Perlin, Quad, RotateY, SolidColor, Sphere, Translate, createBox)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 
@@ -142,3 +142,74 @@ def earth_perlin_world(seed: int = 0, images: Optional[Sequence[Image]] = None) 
         Sphere.init([0, 2, 2.5], 2, noise),
         Sphere.init([0, 2, -2.5], 2, Lambertian.init(ImageTexture.init(images, 0))),
     ]
+
+
+def quads_world() -> list:
+    """quadsWorld (src/main.zig:127-144): five coloured quads."""
+    left_red = Lambertian.init(SolidColor.init([1, 0.2, 0.2]))
+    back_green = Lambertian.init(SolidColor.init([0.2, 1.0, 0.2]))
+    right_blue = Lambertian.init(SolidColor.init([0.2, 0.2, 1.0]))
+    upper_orange = Lambertian.init(SolidColor.init([1.0, 0.5, 0]))
+    lower_teal = Lambertian.init(SolidColor.init([0.2, 0.8, 0.8]))
+    return [
+        Quad.init([-3, -2, 5], [0, 0, -4], [0, 4, 0], left_red),
+        Quad.init([-2, -2, 0], [4, 0, 0], [0, 4, 0], back_green),
+        Quad.init([3, -2, 1], [0, 0, 4], [0, 4, 0], right_blue),
+        Quad.init([-2, -3, 1], [4, 0, 0], [0, 0, 4], upper_orange),
+        Quad.init([-2, -3, 5], [4, 0, 0], [0, 0, -4], lower_teal),
+    ]
+
+
+def simple_light_world(seed: int = 0) -> list:
+    """simpleLightWorld (src/main.zig:146-166): Perlin spheres lit by a quad and a sphere light
+    (camera: camera.simple_light_camera)."""
+    mat = Lambertian.init(NoiseTexture.init(4, Perlin.init(seed, 0)))
+    difflight = DiffuseLight.init(SolidColor.init([4, 4, 4]))
+    return [
+        Sphere.init([0, -1000, 0], 1000, mat),
+        Sphere.init([0, 2, 0], 2, mat),
+        Quad.init([3, 1, -2], [2, 0, 0], [0, 2, 0], difflight),
+        Sphere.init([0, 7, 0], 2, difflight),
+    ]
+
+
+def _cornell_walls(light_q, light_u, light_v, light_color):
+    red = Lambertian.init(SolidColor.init([0.65, 0.05, 0.05]))
+    white = Lambertian.init(SolidColor.init([0.73, 0.73, 0.73]))
+    green = Lambertian.init(SolidColor.init([0.12, 0.45, 0.15]))
+    light = DiffuseLight.init(SolidColor.init(light_color))
+    walls = [
+        Quad.init([555, 0, 0], [0, 555, 0], [0, 0, 555], green),
+        Quad.init([0, 0, 0], [0, 555, 0], [0, 0, 555], red),
+        Quad.init(light_q, light_u, light_v, light),
+        Quad.init([0, 0, 0], [555, 0, 0], [0, 0, 555], white),
+        Quad.init([555, 555, 555], [-555, 0, 0], [0, 0, -555], white),
+        Quad.init([0, 0, 555], [555, 0, 0], [0, 555, 0], white),
+    ]
+    return walls, white
+
+
+def cornell_box() -> list:
+    """cornellBox (src/main.zig:168-205), HEAD's default scene (camera: camera.cornell_camera)."""
+    objs, white = _cornell_walls([343, 554, 332], [-130, 0, 0], [0, 0, -105], [15, 15, 15])
+    box1 = createBox([0, 0, 0], [165, 330, 165], white)
+    box1 = RotateY.init(box1, 15)
+    box1 = Translate.init(box1, [265, 0, 295])
+    objs.append(box1)
+    box2 = createBox([0, 0, 0], [165, 165, 165], white)
+    box2 = RotateY.init(box2, -18)
+    box2 = Translate.init(box2, [130, 0, 65])
+    objs.append(box2)
+    return objs
+
+
+def cornell_smoke() -> list:
+    """cornellBoxSmoke (src/main.zig:207-251): the two boxes as ConstantMedium (density 0.01),
+    black and white smoke (camera: camera.cornell_smoke_camera)."""
+    objs, white = _cornell_walls([113, 554, 127], [330, 0, 0], [0, 0, 305], [7, 7, 7])
+    box1 = Translate.init(RotateY.init(createBox([0, 0, 0], [165, 330, 165], white), 15), [265, 0, 295])
+    objs.append(ConstantMedium.initFromColor(box1, 0.01, [0, 0, 0]))
+    box2 = Translate.init(RotateY.init(createBox([0, 0, 0], [165, 165, 165], white), -18), [130, 0, 65])
+    objs.append(ConstantMedium.initFromColor(box2, 0.01, [1, 1, 1]))
+    return objs
+
