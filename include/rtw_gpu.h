@@ -293,6 +293,28 @@ uint32_t rtw_shard_rows(uint32_t height, uint32_t rows_per_block, uint32_t n_sha
 /* SharedStateImageWriter texel update: u8(256*clamp(sqrt(rgb/w),0,0.999)), alpha 255
  * (src/camera.zig:58-65, src/color.zig:43-62). Host, n pixels. */
 int rtw_texture_from_accum(const float* accum, uint32_t n, uint8_t* rgba_out);
+/* The same texel update on the device (d_accum float4[n] -> d_rgba u8x4[n], HBM), enqueued on
+ * `stream` (NULL = the context's default device stream of device 0's current context). */
+int rtw_texture_from_accum_device(const float* d_accum, uint32_t n, uint8_t* d_rgba, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Output formats (the reference's README TODO "Output selector"
+ * and main.zig:47 "save to file").  Host-only, over the float4 accumulator.
+ * ------------------------------------------------------------------------- */
+enum rtw_ppm_style {
+    RTW_PPM_WRITECOLOR = 0,    /* color.zig:64-69 writeColor: round(256 * toGamma(c)), "r g b\n" per pixel
+                                  (the format of the reference's image2.ppm; values reach 256) */
+    RTW_PPM_STDOUT = 1         /* stdout.zig:5-18 printPpmToStdout: floor(255.999 * toGamma(c)), "r g b\t"
+                                  (the format of image.ppm) */
+};
+/* P3 PPM "P3\n<w> <h>\n255\n" + pixels row-major from the top row.  Writes at most cap
+ * bytes; *len = bytes of the whole encoding (call with out = NULL to size the buffer).
+ * Returns RTW_E_INVALID if out != NULL and cap < *len.  NaN components print "nan". */
+int rtw_encode_ppm(const float* accum, uint32_t width, uint32_t height, uint32_t style, char* out, size_t cap,
+                   size_t* len);
+/* 8-bit RGBA PNG (zlib stored blocks, no filtering) of u8x4 texels, e.g. the
+ * SharedStateImageWriter texture_buffer (rtw_texture_from_accum).  Same sizing contract. */
+int rtw_encode_png(const uint8_t* rgba, uint32_t width, uint32_t height, uint8_t* out, size_t cap, size_t* len);
 
 /* Host-only: build + flatten the BVH exactly as rtw_scene_create does, without
  * touching a device (nodes_out may be NULL to query the count). */

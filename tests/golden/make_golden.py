@@ -74,6 +74,12 @@ def main():
                         image_rows=img1[:30].astype(np.int16),
                         image2_mean=img2.reshape(-1, 3).mean(0), image_mean=img1.reshape(-1, 3).mean(0))
 
+    # the first 400 bytes of the reference's two PPM files: header + pixel text format (data)
+    import json
+    heads = {n: open(os.path.join(REF, n), "rb").read(400).decode("ascii") for n in ("image2.ppm", "image.ppm")}
+    with open(os.path.join(HERE, "ppm_heads.json"), "w") as f:
+        json.dump(heads, f, indent=1)
+
     b_sp, b_mt, b_tx = O.gen_book1(0, 0)
     h_sp, h_mt, h_tx = O.gen_book1(0, 1)
     perlin = O.gen_perlin(0, 0)

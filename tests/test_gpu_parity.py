@@ -343,3 +343,19 @@ def test_fast_reject_is_exact(rtw, scene, monkeypatch):
         outs.append(render_rows(rtw, w, cam, 0, cam.derived.image_height, 0, 4, 5))
         w.close()
     assert np.array_equal(outs[0], outs[1])
+
+
+def test_texture_from_accum_device_matches_host(rtw):
+    """Device texel update (rtw_texture_from_accum_device) == host toGamma2 texels."""
+    import torch
+    rng = np.random.default_rng(1)
+    acc = np.concatenate([rng.random((5000, 3), np.float32) * 30, rng.integers(1, 64, (5000, 1)).astype(np.float32)], 1)
+    acc[:4, :3] = 0
+    acc[4:8, :3] = 1e7
+    host = np.zeros((5000, 4), np.uint8)
+    rtw.lib().rtw_texture_from_accum(acc.ctypes.data, 5000, host.ctypes.data)
+    d_acc = torch.from_numpy(acc).cuda()
+    d_out = torch.zeros((5000, 4), dtype=torch.uint8, device="cuda")
+    rtw._abi.check(rtw.lib().rtw_texture_from_accum_device(d_acc.data_ptr(), 5000, d_out.data_ptr(), None), "tex")
+    torch.cuda.synchronize()
+    assert np.array_equal(d_out.cpu().numpy(), host)

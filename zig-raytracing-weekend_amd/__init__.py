@@ -11,7 +11,7 @@ Host API (mirrors the reference's Zig API names):
            stress_world, earth_perlin_world
 The hot path runs in librtw_gpu.so (include/rtw_gpu.h) on gfx950.
 """
-from . import _abi, configs, distributed, rng, worlds  # noqa: F401
+from . import _abi, configs, distributed, output, rng, worlds  # noqa: F401
 from ._abi import RtwError, lib  # noqa: F401
 from .camera import (Camera, RayTraceState, SharedStateImageWriter, Task, book1_camera,  # noqa: F401
                      cornell_camera, cornell_smoke_camera, earth_perlin_camera, simple_light_camera, start_render)

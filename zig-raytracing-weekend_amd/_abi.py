@@ -19,6 +19,7 @@ RTW_MAT_LAMBERTIAN, RTW_MAT_METAL, RTW_MAT_DIELECTRIC, RTW_MAT_DIFFUSE_LIGHT, RT
 RTW_TEX_SOLID, RTW_TEX_CHECKER, RTW_TEX_IMAGE, RTW_TEX_NOISE = range(4)
 RTW_BG_CONSTANT, RTW_BG_GRADIENT = 0, 1
 RTW_BVH_REFERENCE, RTW_BVH_SAH = 0, 1
+RTW_PPM_WRITECOLOR, RTW_PPM_STDOUT = 0, 1
 RTW_RENDER_NO_SYNC = 1
 RTW_STAT_RAYS, RTW_STAT_NODES, RTW_STAT_LEAVES, RTW_STAT_SAMPLES, RTW_STAT_NAN, RTW_STAT_TAIL_RAYS = 0, 1, 2, 3, 4, 5
 RTW_STAT_COUNT = 8
@@ -122,6 +123,11 @@ SIGNATURES = {
                                          C.POINTER(RtwRenderOpts)]),
     "rtw_shard_rows": (C.c_uint32, [C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32]),
     "rtw_texture_from_accum": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p]),
+    "rtw_texture_from_accum_device": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p]),
+    "rtw_encode_ppm": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_void_p, C.c_size_t,
+                                 C.POINTER(C.c_size_t)]),
+    "rtw_encode_png": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p, C.c_size_t,
+                                 C.POINTER(C.c_size_t)]),
     "rtw_scene_flatten": (C.c_int, [C.POINTER(RtwSceneDesc), C.c_void_p, C.c_uint32, C.POINTER(C.c_uint32),
                                     C.POINTER(C.c_uint32)]),
     "rtw_scene_stats_get": (C.c_int, [C.c_void_p, C.POINTER(RtwSceneStats)]),

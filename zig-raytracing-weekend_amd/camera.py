@@ -56,6 +56,16 @@ class SharedStateImageWriter:
     def image(self) -> np.ndarray:
         return self.texture_buffer.reshape(self.height, self.width, 4)
 
+    def save_ppm(self, path: str, style: int = _abi.RTW_PPM_WRITECOLOR) -> None:
+        """P3 PPM of the accumulator (color.zig writeColor / stdout.zig formats)."""
+        from .output import write_ppm
+        write_ppm(path, self.buffer, self.width, self.height, style)
+
+    def save_png(self, path: str) -> None:
+        """RGBA8 PNG of the texture buffer (update_texture first)."""
+        from .output import write_png
+        write_png(path, self.texture_buffer, self.width, self.height)
+
 
 @dataclass
 class Camera:

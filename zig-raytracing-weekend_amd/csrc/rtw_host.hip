@@ -681,7 +681,7 @@ int rtw_texture_from_accum(const float* accum, uint32_t n, uint8_t* out) {
             float x = std::sqrt(px[k] * scale);
             if (x < 0.0f) x = 0.0f;
             if (x > 0.999f) x = 0.999f;
-            out[4 * (size_t)i + k] = (uint8_t)(256 * x);
+            out[4 * (size_t)i + k] = (x == x) ? (uint8_t)(256 * x) : 0;  // NaN (UB in the reference): 0
         }
         out[4 * (size_t)i + 3] = 255;
     }
