@@ -312,6 +312,28 @@ enum rtw_ppm_style {
  * Returns RTW_E_INVALID if out != NULL and cap < *len.  NaN components print "nan". */
 int rtw_encode_ppm(const float* accum, uint32_t width, uint32_t height, uint32_t style, char* out, size_t cap,
                    size_t* len);
+/* ---------------------------------------------------------------------------
+ * Progressive / resumable renders.  rtw_render* accumulate
+ * samples [spp_begin, spp_end) onto the buffer in sample order, so any split
+ * of [0, spp) into consecutive calls -- including across a checkpoint -- is
+ * bit-identical to one call.
+ * ------------------------------------------------------------------------- */
+/* countSamples (src/main.zig:470-477): f32 sum of accum[i][3] in index order -- the
+ * control panel's progress (vs spp * n) and POWER (= samples / elapsed ms, :495-503). */
+float rtw_count_samples(const float* accum, uint64_t n);
+/* FNV-1a 64 of the scene's device image (nodes + geometry + materials + textures); a
+ * checkpoint records it so a resume on a different scene or BVH is refused. */
+int rtw_scene_hash(rtw_ctx* ctx, uint64_t* out);
+/* Checkpoint file (little endian): "RTWCKPT1", u32 version 1, u32 spp_done, u64 seed,
+ * u64 scene_hash, rtw_camera, u64 n_pixels, float4[n_pixels] accumulator, u32 CRC-32 of
+ * everything before it.  read: cam/seed/hash/spp_done may be NULL; accum must hold
+ * cap_pixels float4 (n_pixels must equal cap_pixels) -- RTW_E_INVALID on any mismatch or
+ * corruption. */
+int rtw_checkpoint_write(const char* path, const rtw_camera* cam, uint64_t seed, uint64_t scene_hash,
+                         uint32_t spp_done, const float* accum);
+int rtw_checkpoint_read(const char* path, rtw_camera* cam, uint64_t* seed, uint64_t* scene_hash,
+                        uint32_t* spp_done, float* accum, uint64_t cap_pixels);
+
 /* 8-bit RGBA PNG (zlib stored blocks, no filtering) of u8x4 texels, e.g. the
  * SharedStateImageWriter texture_buffer (rtw_texture_from_accum).  Same sizing contract. */
 int rtw_encode_png(const uint8_t* rgba, uint32_t width, uint32_t height, uint8_t* out, size_t cap, size_t* len);

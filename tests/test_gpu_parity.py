@@ -359,3 +359,31 @@ def test_texture_from_accum_device_matches_host(rtw):
     rtw._abi.check(rtw.lib().rtw_texture_from_accum_device(d_acc.data_ptr(), 5000, d_out.data_ptr(), None), "tex")
     torch.cuda.synchronize()
     assert np.array_equal(d_out.cpu().numpy(), host)
+
+
+def test_progressive_and_resume_bit_identical(rtw, book1, tmp_path):
+    """progressive batches (the interactive UI loop) and a
+    checkpoint -> new process state -> resume are bit-identical to one render;
+    countSamples reaches spp * n; a checkpoint of another scene is refused."""
+    arr, world = book1
+    cam = rtw.book1_camera(image_width=160, aspect_ratio=1.5, spp=7).init()
+    one = rtw.RayTraceState(cam, rtw.SharedStateImageWriter(160, cam.derived.image_height), world, seed=5)
+    one.writer.buffer[:, 3] = 0
+    cam.render_range(one, 0, cam.size, 0, 7)
+    prog = rtw.RayTraceState(cam, rtw.SharedStateImageWriter(160, cam.derived.image_height), world, seed=5)
+    prog.writer.buffer[:, 3] = 0
+    seen = []
+    done = rtw.progressive_render(prog, 0, 2, lambda s, n: seen.append((s, n)) or s >= 4)
+    assert done == 4 and [s for s, _ in seen] == [2, 4] and seen[-1][1] == 4 * cam.size
+    prog.checkpoint(str(tmp_path / "c.ckpt"), done)
+    fresh = rtw.RayTraceState(cam, rtw.SharedStateImageWriter(160, cam.derived.image_height), world, seed=5)
+    start = fresh.resume(str(tmp_path / "c.ckpt"))
+    assert start == 4
+    assert rtw.progressive_render(fresh, start, 2) == 7
+    assert np.array_equal(fresh.writer.buffer, one.writer.buffer)
+    assert fresh.count_samples() == 7 * cam.size
+    other = rtw.World(rtw.flatten(rtw.worlds.two_spheres_world()))
+    bad = rtw.RayTraceState(cam, rtw.SharedStateImageWriter(160, cam.derived.image_height), other, seed=5)
+    with pytest.raises(rtw.RtwError):
+        bad.resume(str(tmp_path / "c.ckpt"))
+    other.close()

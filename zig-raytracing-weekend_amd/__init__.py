@@ -14,7 +14,8 @@ The hot path runs in librtw_gpu.so (include/rtw_gpu.h) on gfx950.
 from . import _abi, configs, distributed, output, rng, worlds  # noqa: F401
 from ._abi import RtwError, lib  # noqa: F401
 from .camera import (Camera, RayTraceState, SharedStateImageWriter, Task, book1_camera,  # noqa: F401
-                     cornell_camera, cornell_smoke_camera, earth_perlin_camera, simple_light_camera, start_render)
+                     cornell_camera, cornell_smoke_camera, earth_perlin_camera, progressive_render,
+                     simple_light_camera, start_render)
 from .scene import (BVHTree, CheckerTexture, ConstantMedium, Dielectric, DiffuseLight,  # noqa: F401
                     HittableList, Image, ImageTexture, Isotropic, Lambertian, Metal, NoiseTexture, Perlin, Quad,
                     RotateY, SceneArrays, SolidColor, Sphere, Translate, World, createBox, flatten)

@@ -128,6 +128,12 @@ SIGNATURES = {
                                  C.POINTER(C.c_size_t)]),
     "rtw_encode_png": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p, C.c_size_t,
                                  C.POINTER(C.c_size_t)]),
+    "rtw_count_samples": (C.c_float, [C.c_void_p, C.c_uint64]),
+    "rtw_scene_hash": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint64)]),
+    "rtw_checkpoint_write": (C.c_int, [C.c_char_p, C.POINTER(RtwCamera), C.c_uint64, C.c_uint64, C.c_uint32,
+                                       C.c_void_p]),
+    "rtw_checkpoint_read": (C.c_int, [C.c_char_p, C.POINTER(RtwCamera), C.POINTER(C.c_uint64),
+                                      C.POINTER(C.c_uint64), C.POINTER(C.c_uint32), C.c_void_p, C.c_uint64]),
     "rtw_scene_flatten": (C.c_int, [C.POINTER(RtwSceneDesc), C.c_void_p, C.c_uint32, C.POINTER(C.c_uint32),
                                     C.POINTER(C.c_uint32)]),
     "rtw_scene_stats_get": (C.c_int, [C.c_void_p, C.POINTER(RtwSceneStats)]),

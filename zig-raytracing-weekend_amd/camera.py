@@ -154,6 +154,59 @@ class RayTraceState:
         """RenderThread.stop (src/main.zig:58-60): polled between sample batches."""
         self.cancel.value = 1
 
+    def count_samples(self) -> float:
+        """countSamples (src/main.zig:470-477): f32 sum of buffer[i][3] (progress / POWER)."""
+        b = self.writer.buffer
+        return float(_abi.lib().rtw_count_samples(b.ctypes.data, b.shape[0]))
+
+    def samples_done(self) -> int:
+        """Samples per pixel already in the buffer (writeColor stores the count in .w)."""
+        return int(self.writer.buffer[:, 3].max()) if self.writer.buffer.size else 0
+
+    def checkpoint(self, path: str, spp_done: int) -> None:
+        """Write the accumulator + camera/seed/scene hash (rtw_checkpoint_write)."""
+        h = C.c_uint64()
+        _abi.check(_abi.lib().rtw_scene_hash(self.world.handle, C.byref(h)), "rtw_scene_hash")
+        b = self.writer.buffer
+        _abi.check(_abi.lib().rtw_checkpoint_write(path.encode(), C.byref(self.camera.derived), self.seed, h.value,
+                                                   spp_done, b.ctypes.data), "rtw_checkpoint_write")
+
+    def resume(self, path: str) -> int:
+        """Load a checkpoint into the writer; refuses another scene, camera or seed.
+        Returns the samples already done (render [done, spp) next)."""
+        cam = _abi.RtwCamera()
+        seed, h, done = C.c_uint64(), C.c_uint64(), C.c_uint32()
+        b = self.writer.buffer
+        _abi.check(_abi.lib().rtw_checkpoint_read(path.encode(), C.byref(cam), C.byref(seed), C.byref(h),
+                                                  C.byref(done), b.ctypes.data, b.shape[0]), "rtw_checkpoint_read")
+        mine = C.c_uint64()
+        _abi.check(_abi.lib().rtw_scene_hash(self.world.handle, C.byref(mine)), "rtw_scene_hash")
+        if h.value != mine.value or seed.value != self.seed or bytes(cam) != bytes(self.camera.derived):
+            raise _abi.RtwError(_abi.RTW_E_INVALID, "resume", "checkpoint is for another scene/camera/seed")
+        self.writer.update_texture()
+        return int(done.value)
+
+
+def progressive_render(state: RayTraceState, spp_begin: int = 0, batch: int = 1,
+                       on_batch: Optional[Callable[[int, float], bool]] = None) -> int:
+    """Interactive-style render: samples [spp_begin, spp) in batches of `batch` over the
+    whole image, refreshing the texture after each (what the UI shows) and calling
+    on_batch(samples_done_per_pixel, count_samples()) -- return True to stop (the
+    reference's Stop button, main.zig:58-60).  Consecutive batches are bit-identical to
+    one render.  Returns the samples per pixel done."""
+    cam = state.camera
+    if cam.derived is None:
+        cam.init()
+    s = spp_begin
+    spp = cam.samples_per_pixel
+    while s < spp and not state.cancel.value:
+        e = min(spp, s + batch)
+        cam.render_range(state, 0, cam.size, s, e)
+        s = e
+        if on_batch is not None and on_batch(s, state.count_samples()):
+            break
+    return s
+
 
 def start_render(state: RayTraceState, number_of_threads: int = 8) -> None:
     """startRender (src/main.zig:314-326): scrub, Camera.init, 8 Tasks of size/8.

@@ -270,6 +270,11 @@ int rtw_scene_create(const rtw_scene_desc* d, int device, rtw_ctx** out) {
         return code;
     }
     ctx->blob_bytes = off;
+    {   // FNV-1a 64 of the scene image (rtw_scene_hash)
+        uint64_t h = 0xCBF29CE484222325ull;
+        for (size_t i = 0; i < off; i++) h = (h ^ blob[i]) * 0x100000001B3ull;
+        ctx->scene_hash = h;
+    }
     uint8_t* dev = static_cast<uint8_t*>(ctx->d_blob);
     rtw_launch& L = ctx->base;
     L.nodes = reinterpret_cast<const float4*>(dev + o_nodes);
@@ -375,6 +380,12 @@ int rtw_scene_flatten(const rtw_scene_desc* d, void* out, uint32_t cap, uint32_t
     if (n_out) *n_out = n;
     if (depth_out) *depth_out = depth;
     if (out) std::memcpy(out, nodes.data(), sizeof(rtw_node) * (cap < n ? cap : n));
+    return RTW_OK;
+}
+
+int rtw_scene_hash(rtw_ctx* ctx, uint64_t* out) {
+    if (!ctx || !out) return fail(RTW_E_INVALID, "null ctx");
+    *out = ctx->scene_hash;
     return RTW_OK;
 }
 

@@ -168,6 +168,7 @@ struct rtw_ctx {
     uint32_t wf_iters = 6;         // RTW_WF_ITERS: wavefront bounces before the tail kernel
     int n_cu = 256;                // compute units of the device (wavefront grids)
     std::vector<hipEvent_t> ev_pool;  // recycled timing events
+    uint64_t scene_hash = 0;       // FNV-1a 64 of the uploaded scene image
     float box_pad = 0;             // absolute pad baked into the inner boxes (SAH trees), 0 = none
     float extent = 0;              // max |coordinate| over the scene's boxes
 };

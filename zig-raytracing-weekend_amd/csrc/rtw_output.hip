@@ -1,14 +1,18 @@
-// rtw_output.hip -- output formats over the float4 accumulator:
+// rtw_output.hip -- output formats and checkpoints over the float4 accumulator
+// (SURVEY §8f rows 3-4).  Output:
 // the two P3 PPM writers of the reference (color.zig:64-69 writeColor,
 // stdout.zig:5-18 printPpmToStdout), an RGBA8 PNG encoder for the
 // SharedStateImageWriter texture (the reference's "save to file" TODO,
 // main.zig:47), and the texel update of camera.zig:58-65 as a device kernel.
+// Progress/resume: countSamples (main.zig:470-477) and a CRC-checked checkpoint
+// file of the accumulator + the camera, seed, scene hash and samples done.
 #include <hip/hip_runtime.h>
 
 #include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <vector>
 
 #include "../../include/rtw_gpu.h"
 
@@ -37,14 +41,16 @@ inline int put_value(char* dst, float v) {
 }
 
 uint32_t crc_table[256];
-bool crc_ready = false;
-void crc_init() {
+void crc_fill() {
     for (uint32_t n = 0; n < 256; n++) {
         uint32_t c = n;
         for (int k = 0; k < 8; k++) c = (c & 1) ? 0xEDB88320u ^ (c >> 1) : c >> 1;
         crc_table[n] = c;
     }
-    crc_ready = true;
+}
+void crc_init() {
+    static const bool once = (crc_fill(), true);  // thread-safe one-time init
+    (void)once;
 }
 uint32_t crc32(const uint8_t* p, size_t n, uint32_t c = 0xFFFFFFFFu) {
     for (size_t i = 0; i < n; i++) c = crc_table[(c ^ p[i]) & 0xFF] ^ (c >> 8);
@@ -117,9 +123,86 @@ int rtw_encode_ppm(const float* accum, uint32_t width, uint32_t height, uint32_t
     return RTW_OK;
 }
 
+float rtw_count_samples(const float* accum, uint64_t n) {
+    float samples = 0;  // main.zig:471-476: f32, index order
+    if (!accum) return 0;
+    for (uint64_t i = 0; i < n; i++) samples += accum[4 * i + 3];
+    return samples;
+}
+
+int rtw_checkpoint_write(const char* path, const rtw_camera* cam, uint64_t seed, uint64_t scene_hash,
+                         uint32_t spp_done, const float* accum) {
+    if (!path || !cam || !accum) return RTW_E_INVALID;
+    crc_init();
+    FILE* f = std::fopen(path, "wb");
+    if (!f) return RTW_E_INVALID;
+    uint32_t crc = 0xFFFFFFFFu;
+    bool ok = true;
+    auto put = [&](const void* p, size_t n) {
+        crc = crc32(static_cast<const uint8_t*>(p), n, crc);
+        ok = ok && std::fwrite(p, 1, n, f) == n;
+    };
+    const uint32_t version = 1;
+    const uint64_t n_pix = cam->size;
+    put("RTWCKPT1", 8);
+    put(&version, 4);
+    put(&spp_done, 4);
+    put(&seed, 8);
+    put(&scene_hash, 8);
+    put(cam, sizeof *cam);
+    put(&n_pix, 8);
+    put(accum, n_pix * 16);
+    const uint32_t c = crc ^ 0xFFFFFFFFu;
+    ok = ok && std::fwrite(&c, 1, 4, f) == 4;
+    ok = (std::fclose(f) == 0) && ok;
+    return ok ? RTW_OK : RTW_E_INVALID;
+}
+
+int rtw_checkpoint_read(const char* path, rtw_camera* cam, uint64_t* seed, uint64_t* scene_hash,
+                        uint32_t* spp_done, float* accum, uint64_t cap_pixels) {
+    if (!path) return RTW_E_INVALID;
+    crc_init();
+    FILE* f = std::fopen(path, "rb");
+    if (!f) return RTW_E_INVALID;
+    uint32_t crc = 0xFFFFFFFFu;
+    bool ok = true;
+    auto get = [&](void* p, size_t n) {
+        ok = ok && std::fread(p, 1, n, f) == n;
+        if (ok) crc = crc32(static_cast<const uint8_t*>(p), n, crc);
+    };
+    char magic[8];
+    uint32_t version = 0, done = 0;
+    uint64_t sd = 0, hash = 0, n_pix = 0;
+    rtw_camera c{};
+    get(magic, 8);
+    get(&version, 4);
+    get(&done, 4);
+    get(&sd, 8);
+    get(&hash, 8);
+    get(&c, sizeof c);
+    get(&n_pix, 8);
+    ok = ok && std::memcmp(magic, "RTWCKPT1", 8) == 0 && version == 1 && n_pix == c.size &&
+         (!accum || n_pix == cap_pixels);
+    std::vector<float> tmp;
+    if (ok) {
+        tmp.resize(n_pix * 4);
+        get(tmp.data(), n_pix * 16);
+    }
+    uint32_t stored = 0;
+    ok = ok && std::fread(&stored, 1, 4, f) == 4 && stored == (crc ^ 0xFFFFFFFFu);
+    std::fclose(f);
+    if (!ok) return RTW_E_INVALID;
+    if (cam) *cam = c;
+    if (seed) *seed = sd;
+    if (scene_hash) *scene_hash = hash;
+    if (spp_done) *spp_done = done;
+    if (accum) std::memcpy(accum, tmp.data(), n_pix * 16);
+    return RTW_OK;
+}
+
 int rtw_encode_png(const uint8_t* rgba, uint32_t width, uint32_t height, uint8_t* out, size_t cap, size_t* len) {
     if (!rgba || !len || width == 0 || height == 0) return RTW_E_INVALID;
-    if (!crc_ready) crc_init();
+    crc_init();
     Sink s{out, out ? cap : 0};
     static const uint8_t sig[8] = {0x89, 'P', 'N', 'G', '\r', '\n', 0x1A, '\n'};
     s.put(sig, 8);
