@@ -35,7 +35,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--config", default="c2", choices=["c2", "c3", "c4", "c5"])
+    ap.add_argument("--config", default="c2",
+                    choices=["c1", "c2", "c3", "c4", "c5", "cornell", "cornell_smoke", "simple_light"])
     ap.add_argument("--spp", type=int, default=0, help="override spp (0 = config's)")
     ap.add_argument("--bvh", default="sah", choices=["sah", "reference"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -161,7 +162,8 @@ def main():
 
     if rank == 0:
         line = {
-            "metric": "Msamples/s (pixel·spp) on 1200×800 Book-1 random-spheres @500spp; 1→8 GPU",
+            "metric": ("Msamples/s (pixel·spp) on 1200×800 Book-1 random-spheres @500spp; 1→8 GPU"
+                       if args.config == "c2" else f"Msamples/s (pixel·spp) on {cfg.description}"),
             "value": round(value, 3),
             "unit": "Msamples/s",
             "n_gpus": world_size,
@@ -172,10 +174,9 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic: seeded Book-1 random-spheres scene (seed 0, %d spheres), counter-based RNG seed 0"
-                    % len(objs),
+            "data": "synthetic: seeded %s scene (%d world objects), counter-based RNG seed 0" % (args.config, len(objs)),
             "config": {"workload": cfg.description, "config_id": args.config, "width": W, "height": H,
-                       "spp": spp, "max_depth": cam.max_depth, "spheres": len(objs), "bvh_nodes": stats["n_nodes"],
+                       "spp": spp, "max_depth": cam.max_depth, "objects": len(objs), "bvh_nodes": stats["n_nodes"],
                        "bvh_depth": stats["depth"], "parallelism": f"row-interleaved tiles x{world_size}"
                        + (" + RCCL gather" if distributed else ""), "rows_per_block": ROWS_PER_BLOCK},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -229,7 +230,7 @@ def cpu_baseline(pkg, arr, cam, args):
     import numpy as np
     import oracle as O
 
-    ow = O.World(arr.spheres, arr.materials, arr.textures, arr.perlins, [im.rgba for im in arr.images])
+    ow = O.World.from_arrays(arr)
     d = cam.derived
     ocam = O.camera(aspect_ratio=cam.aspect_ratio, image_width=d.image_width, image_height=d.image_height,
                     samples_per_pixel=d.samples_per_pixel, max_depth=d.max_depth, background=tuple(d.background),

@@ -350,9 +350,9 @@ __device__ __forceinline__ bool quad_t(const rtw_dev_quad& q, const Ray& r, floa
 
 // world ray -> object space of an instance: the outermost transform first
 // (Translate.hit objects.zig:314-317, RotateY.hit :401-411)
-__device__ __forceinline__ Ray inst_to_object(const rtw_dev_instance& in, Ray r) {
-    for (int k = (int)in.n_xf - 1; k >= 0; k--) {
-        const float4 x = ldg4(in.xf[k]);
+__device__ __forceinline__ Ray inst_to_object(const rtw_dev_instance* __restrict__ in, Ray r) {
+    for (int k = (int)in->n_xf - 1; k >= 0; k--) {
+        const float4 x = ldg4(in->xf[k]);
         if (fbits(x.x) == RTW_XF_TRANSLATE) {
             r.o = r.o - mk(x.y, x.z, x.w);
         } else {
@@ -368,9 +368,9 @@ __device__ __forceinline__ Ray inst_to_object(const rtw_dev_instance& in, Ray r)
 }
 
 // object-space point/normal -> world: innermost transform first (RotateY.hit :419-435, Translate.hit :325-326)
-__device__ __forceinline__ void inst_to_world(const rtw_dev_instance& in, f3& p, f3& n) {
-    for (uint32_t k = 0; k < in.n_xf; k++) {
-        const float4 x = ldg4(in.xf[k]);
+__device__ __forceinline__ void inst_to_world(const rtw_dev_instance* __restrict__ in, f3& p, f3& n) {
+    for (uint32_t k = 0; k < in->n_xf; k++) {
+        const float4 x = ldg4(in->xf[k]);
         if (fbits(x.x) == RTW_XF_TRANSLATE) {
             p = p + mk(x.y, x.z, x.w);
         } else {
@@ -386,12 +386,13 @@ __device__ __forceinline__ void inst_to_world(const rtw_dev_instance& in, f3& p,
 
 // HittableList.hit over the members in object space (objects.zig:281-289)
 template <uint32_t FEAT>
-__device__ __forceinline__ bool list_t(const rtw_launch& L, const rtw_dev_instance& in, const Ray& ro, float tmin,
-                                       float tmax, float& t, uint32_t& sub) {
+__device__ __forceinline__ bool list_t(const rtw_launch& L, const rtw_dev_instance* __restrict__ in, const Ray& ro,
+                                       float tmin, float tmax, float& t, uint32_t& sub) {
     bool any = false;
     float closest = tmax;
-    for (uint32_t m = 0; m < in.count; m++) {
-        const uint32_t ref = L.members[in.first + m];
+    const uint32_t first = in->first, count = in->count;
+    for (uint32_t m = 0; m < count; m++) {
+        const uint32_t ref = L.members[first + m];
         const uint32_t idx = RTW_REF_INDEX(ref);
         float tt;
         bool h;
@@ -423,7 +424,7 @@ __device__ __forceinline__ bool boundary_t(const rtw_launch& L, uint32_t ref, co
     }
     case RTW_OBJ_QUAD: return quad_t(L.quads[idx], r, tmin, tmax, t);
     default: {
-        const rtw_dev_instance in = L.insts[idx];
+        const rtw_dev_instance* in = L.insts + idx;
         uint32_t sub;
         return list_t<FEAT>(L, in, inst_to_object(in, r), tmin, tmax, t, sub);
     }
@@ -453,7 +454,7 @@ __device__ __forceinline__ bool medium_t(const rtw_launch& L, uint32_t idx, cons
 // A non-sphere leaf tested with (0.001, closest): updates closest / hit
 // (hit = node | member << 24 for an instance's list member)
 template <uint32_t FEAT>
-__device__ __noinline__ void object_leaf(const rtw_launch& L, const Ray& r, uint32_t kind, uint32_t idx, uint32_t node,
+__device__ __forceinline__ void object_leaf(const rtw_launch& L, const Ray& r, uint32_t kind, uint32_t idx, uint32_t node,
                                          float& closest, int& hit, uint64_t mkey) {
     float t;
     uint32_t sub = 0;
@@ -461,7 +462,7 @@ __device__ __noinline__ void object_leaf(const rtw_launch& L, const Ray& r, uint
     if (kind == RTW_OBJ_QUAD) {
         h = quad_t(L.quads[idx], r, kTmin, closest, t);
     } else if (kind == RTW_OBJ_INSTANCE) {
-        const rtw_dev_instance in = L.insts[idx];
+        const rtw_dev_instance* in = L.insts + idx;
         h = list_t<FEAT>(L, in, inst_to_object(in, r), kTmin, closest, t, sub);
     } else if constexpr ((FEAT & RTW_F_MEDIUM) != 0) {
         h = medium_t<FEAT>(L, idx, r, kTmin, closest, mkey, t);
@@ -638,7 +639,7 @@ __device__ __forceinline__ void quad_prep(const rtw_dev_quad& q, const Ray& r, f
 }
 
 template <uint32_t FEAT>
-__device__ __noinline__ HitPrep object_prep(const rtw_launch& L, const Ray& r, uint32_t kind, uint32_t idx,
+__device__ __forceinline__ HitPrep object_prep(const rtw_launch& L, const Ray& r, uint32_t kind, uint32_t idx,
                                             uint32_t sub, float t) {
     HitPrep h;
     if (kind == RTW_OBJ_QUAD) {
@@ -648,9 +649,9 @@ __device__ __noinline__ HitPrep object_prep(const rtw_launch& L, const Ray& r, u
         return h;
     }
     if (kind == RTW_OBJ_INSTANCE) {
-        const rtw_dev_instance in = L.insts[idx];
+        const rtw_dev_instance* in = L.insts + idx;
         const Ray ro = inst_to_object(in, r);
-        const uint32_t ref = L.members[in.first + sub];
+        const uint32_t ref = L.members[in->first + sub];
         const uint32_t mi = RTW_REF_INDEX(ref);
         uint32_t mat;
         if (RTW_REF_KIND(ref) == RTW_OBJ_SPHERE) {  // Sphere.hit record (objects.zig:138-147)
