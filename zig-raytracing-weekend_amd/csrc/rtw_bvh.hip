@@ -406,27 +406,85 @@ public:
         for (int k = 0; k < 3; k++) dir_[k] = d.order_dir[k];
         if (dir_[0] == 0 && dir_[1] == 0 && dir_[2] == 0) dir_[1] = -1;
     }
-    void build() {
+    // orders = 1: one pre-order with children front-to-back along order_dir;
+    // orders = 8: one pre-order per ray-direction octant (bit k set = negative
+    // component k), children ordered front-to-back along that octant's diagonal,
+    // concatenated.  The walk of a ray uses the array of its own octant, so the
+    // child nearer along the ray is visited first and shrinks `closest` early.
+    void build(uint32_t orders) {
         nodes_.clear();
-        nodes_.reserve(2 * objs_.size());
+        tree_.clear();
+        tree_.reserve(2 * objs_.size());
         depth_ = 0;
-        emit(0, idx_.size(), 1);
+        const int root = build_tree(0, idx_.size(), 1);
+        nodes_.reserve(orders * tree_.size());
+        for (uint32_t o = 0; o < orders; o++) {
+            float dir[3];
+            for (int k = 0; k < 3; k++) dir[k] = orders == 1 ? dir_[k] : ((o >> k) & 1 ? -1.0f : 1.0f);
+            base_ = (uint32_t)nodes_.size();
+            emit_tree(root, dir);
+        }
     }
     uint32_t depth() const { return depth_; }
 
 private:
+    struct TNode {
+        Box box;
+        int left = -1, right = -1;
+        uint32_t obj = 0;  // leaf: index into objs_
+    };
+
+    int build_tree(size_t a, size_t b, uint32_t level) {
+        depth_ = std::max(depth_, level);
+        const int me = (int)tree_.size();
+        tree_.push_back(TNode{});
+        if (b - a == 1) {
+            tree_[me].obj = idx_[a];
+            tree_[me].box = objs_[idx_[a]].box;
+            return me;
+        }
+        const size_t mid = split(a, b);
+        const int l = build_tree(a, mid, level + 1);
+        const int r = build_tree(mid, b, level + 1);
+        tree_[me].left = l;
+        tree_[me].right = r;
+        tree_[me].box = box_union(tree_[l].box, tree_[r].box);
+        return me;
+    }
+
+    // pre-order with skip links (relative to the array start base_)
+    void emit_tree(int t, const float dir[3]) {
+        const TNode& n = tree_[t];
+        if (n.left < 0) {
+            nodes_.push_back(geo_.leaf(objs_[n.obj], (uint32_t)nodes_.size() + 1 - base_));
+            return;
+        }
+        const Box& lb = tree_[n.left].box;
+        const Box& rb = tree_[n.right].box;
+        float pl = 0, pr = 0;
+        for (int k = 0; k < 3; k++) {
+            pl += dir[k] * (lb.mn[k] + lb.mx[k]);
+            pr += dir[k] * (rb.mn[k] + rb.mx[k]);
+        }
+        const size_t me = nodes_.size();
+        nodes_.push_back(rtw_node{});
+        if (pr < pl) {  // right child is nearer along dir: walk it first
+            emit_tree(n.right, dir);
+            emit_tree(n.left, dir);
+        } else {
+            emit_tree(n.left, dir);
+            emit_tree(n.right, dir);
+        }
+        rtw_node& o = nodes_[me];
+        const uint32_t skip = (uint32_t)nodes_.size() - base_;
+        for (int i = 0; i < 3; i++) { o.a[i] = n.box.mn[i]; o.b[i] = n.box.mx[i]; }
+        std::memcpy(&o.a[3], &skip, 4);
+        o.b[3] = 0.0f;
+    }
+
     static float area(const Box& b) {
         const float dx = b.mx[0] - b.mn[0], dy = b.mx[1] - b.mn[1], dz = b.mx[2] - b.mn[2];
         return 2.0f * (dx * dy + dy * dz + dz * dx);
-    }
-    Box bounds(size_t a, size_t b) const {
-        Box r = objs_[idx_[a]].box;
-        for (size_t i = a + 1; i < b; i++) r = box_union(r, objs_[idx_[i]].box);
-        return r;
-    }
-    Box emit_leaf(uint32_t oi) {
-        nodes_.push_back(geo_.leaf(objs_[oi], (uint32_t)nodes_.size() + 1));
-        return objs_[oi].box;
     }
     // returns split position (index) after partitioning idx_[a, b)
     size_t split(size_t a, size_t b) {
@@ -491,39 +549,11 @@ private:
         }
         return mid;
     }
-    Box emit(size_t a, size_t b, uint32_t level) {
-        depth_ = std::max(depth_, level);
-        if (b - a == 1) return emit_leaf(idx_[a]);
-        const size_t mid = split(a, b);
-        // front-to-back child order along dir_
-        const Box lb0 = bounds(a, mid), rb0 = bounds(mid, b);
-        float pl = 0, pr = 0;
-        for (int k = 0; k < 3; k++) {
-            pl += dir_[k] * (lb0.mn[k] + lb0.mx[k]);
-            pr += dir_[k] * (rb0.mn[k] + rb0.mx[k]);
-        }
-        const size_t me = nodes_.size();
-        nodes_.push_back(rtw_node{});
-        Box l, r;
-        if (pr < pl) {  // right child is nearer along dir_: emit it first
-            l = emit(mid, b, level + 1);
-            r = emit(a, mid, level + 1);
-        } else {
-            l = emit(a, mid, level + 1);
-            r = emit(mid, b, level + 1);
-        }
-        Box bb = box_union(l, r);
-        rtw_node& n = nodes_[me];
-        uint32_t skip = (uint32_t)nodes_.size();
-        for (int i = 0; i < 3; i++) { n.a[i] = bb.mn[i]; n.b[i] = bb.mx[i]; }
-        std::memcpy(&n.a[3], &skip, 4);
-        n.b[3] = 0.0f;
-        return bb;
-    }
-
     const Geometry& geo_;
     std::vector<rtw_node>& nodes_;
     std::vector<Obj> objs_;
+    std::vector<TNode> tree_;
+    uint32_t base_ = 0;
     std::vector<std::array<float, 3>> cent_;
     std::vector<uint32_t> idx_;
     float dir_[3];
@@ -533,14 +563,14 @@ private:
 }  // namespace
 
 int rtw_build_bvh(const rtw_scene_desc& desc, std::vector<rtw_node>& nodes, rtw_geometry& geom,
-                  uint32_t* depth, uint32_t* axis_draws, float* box_pad, float* extent) {
+                  uint32_t* depth, uint32_t* axis_draws, float* box_pad, float* extent, uint32_t orders) {
     if (box_pad) *box_pad = 0;
     if (extent) *extent = 0;
     Geometry geo(desc, geom);
     if (int rc = geo.build()) return rc;
     if (desc.bvh_mode == RTW_BVH_SAH) {
         SahBuilder b(desc, geo, nodes);
-        b.build();
+        b.build(orders);
         if (depth) *depth = b.depth();
         if (axis_draws) *axis_draws = 0;
         // Pad the inner boxes for the FMA slab test: its t error for a plane P and

@@ -593,10 +593,20 @@ __device__ __forceinline__ uint32_t trav_step(const float4* __restrict__ nodes, 
 }
 
 // World hit for one ray (whole walk).  Returns leaf node index or -1.
-// mkey: the path's RNG state (keys ConstantMedium draws; unused without media)
+// The node array a ray walks: SAH scenes keep 8 copies, children ordered
+// front-to-back for each ray-direction octant (rtw_bvh.hip SahBuilder::build).
+__device__ __forceinline__ const float4* order_base(const float4* nodes, const rtw_launch& L, const Ray& r) {
+    if (L.n_orders <= 1) return nodes;
+    const uint32_t oct = (r.d.x < 0 ? 1u : 0u) | (r.d.y < 0 ? 2u : 0u) | (r.d.z < 0 ? 4u : 0u);
+    return nodes + (size_t)oct * 2u * L.n_nodes;
+}
+
+// mkey: the path's RNG state (keys ConstantMedium draws; unused without media).
+// `nodes` is the base of the node arrays (the octant copy is picked here).
 template <uint32_t FEAT>
 __device__ __forceinline__ int traverse(const float4* __restrict__ nodes, const rtw_launch& L, const Ray& r,
                                         float& t_out, Counters& cnt, uint64_t mkey = 0) {
+    nodes = order_base(nodes, L, r);
     const RayTrav rt = ray_trav(r, L.fast_box != 0);
     float closest = kInf;
     int hit = -1;
@@ -689,6 +699,7 @@ __device__ __forceinline__ HitPrep object_prep(const rtw_launch& L, const Ray& r
 template <uint32_t FEAT>
 __device__ __forceinline__ HitPrep hit_prep(const float4* __restrict__ nodes, const rtw_launch& L, const Ray& r,
                                             int hit, float t) {
+    nodes = order_base(nodes, L, r);
     if constexpr ((FEAT & RTW_F_GEOM) != 0) {
         const uint32_t node = (uint32_t)hit & ((1u << RTW_HIT_NODE_BITS) - 1u);
         const float4 B = nodes[2 * node + 1];

@@ -168,7 +168,10 @@ int rtw_scene_create(const rtw_scene_desc* d, int device, rtw_ctx** out) {
     ctx->device = device;
     rtw_geometry geom;
     uint32_t depth = 0, draws = 0;
-    int rc = rtw_build_bvh(*d, ctx->nodes_host, geom, &depth, &draws, &ctx->box_pad, &ctx->extent);
+    // SAH trees: 8 octant-ordered copies of the node array (RTW_ORDERS=1: one, ordered along order_dir)
+    uint32_t orders = d->bvh_mode == RTW_BVH_SAH ? 8u : 1u;
+    if (const char* o = std::getenv("RTW_ORDERS")) orders = (d->bvh_mode == RTW_BVH_SAH && std::atoi(o) == 8) ? 8u : 1u;
+    int rc = rtw_build_bvh(*d, ctx->nodes_host, geom, &depth, &draws, &ctx->box_pad, &ctx->extent, orders);
     if (rc != RTW_OK) {
         delete ctx;
         return fail(rc, "BVH build failed (bad object graph or bvh_mode)");
@@ -182,9 +185,9 @@ int rtw_scene_create(const rtw_scene_desc* d, int device, rtw_ctx** out) {
     // Blob layout (each section 256-B aligned): nodes | cvec | spheres | quads | members | instances | media |
     // materials | textures | images-info | perlin | image bytes
     auto align = [](size_t x) { return (x + 255) & ~size_t(255); };
-    const size_t n_nodes = ctx->nodes_host.size();
+    const size_t n_nodes = ctx->nodes_host.size() / orders;  // per ordering
     size_t off = 0;
-    const size_t o_nodes = off; off = align(off + n_nodes * sizeof(rtw_node));
+    const size_t o_nodes = off; off = align(off + ctx->nodes_host.size() * sizeof(rtw_node));
     const size_t o_cvec = off; off = align(off + cvec.size() * sizeof(float) + 16);
     const size_t o_sph = off; off = align(off + geom.spheres.size() * sizeof(rtw_dev_sphere) + 16);
     const size_t o_quad = off; off = align(off + geom.quads.size() * sizeof(rtw_dev_quad) + 16);
@@ -208,7 +211,7 @@ int rtw_scene_create(const rtw_scene_desc* d, int device, rtw_ctx** out) {
     off = align(off + img_bytes + 16);
 
     std::vector<uint8_t> blob(off, 0);
-    std::memcpy(blob.data() + o_nodes, ctx->nodes_host.data(), n_nodes * sizeof(rtw_node));
+    std::memcpy(blob.data() + o_nodes, ctx->nodes_host.data(), ctx->nodes_host.size() * sizeof(rtw_node));
     auto put = [&](size_t o, const void* src, size_t nb) {
         if (nb) std::memcpy(blob.data() + o, src, nb);
     };
@@ -290,6 +293,7 @@ int rtw_scene_create(const rtw_scene_desc* d, int device, rtw_ctx** out) {
     L.perlin = reinterpret_cast<const float4*>(dev + o_perl);
     L.images = dev + o_imgs;
     L.n_nodes = (uint32_t)n_nodes;
+    L.n_orders = orders;
     L.n_perlin = d->n_perlins;
     ctx->feat = scene_features(d) | geom.feat;
     L.feat = ctx->feat;
@@ -323,8 +327,8 @@ int rtw_scene_create(const rtw_scene_desc* d, int device, rtw_ctx** out) {
     if (const char* fr = std::getenv("RTW_FAST_REJECT")) L.fast_reject = (uint32_t)std::atoi(fr);
     if (const char* to = std::getenv("RTW_TILE_ORDER")) L.tile_order = (uint32_t)std::atoi(to);
     if (const char* wv = std::getenv("RTW_WAVES")) L.waves = (uint32_t)std::atoi(wv);
-    L.use_lds = 1;
-    if (const char* ul = std::getenv("RTW_LDS")) L.use_lds = (uint32_t)std::atoi(ul);
+    L.use_lds = orders == 1 ? 1 : 0;  // the octant copies do not fit the megakernel's LDS stage
+    if (const char* ul = std::getenv("RTW_LDS")) L.use_lds = orders == 1 ? (uint32_t)std::atoi(ul) : 0;
     // SAH trees: FMA slab test on the padded boxes + leaf postponement (both only
     // enlarge the set of visited nodes; reference trees keep the exact aabb.zig walk)
     const bool sah = ctx->box_pad > 0;
@@ -397,7 +401,7 @@ int rtw_scene_stats_get(rtw_ctx* ctx, rtw_scene_stats* out) {
 
 int rtw_scene_nodes(rtw_ctx* ctx, void* out, uint32_t cap, uint32_t* n_out) {
     if (!ctx) return fail(RTW_E_INVALID, "null ctx");
-    const uint32_t n = (uint32_t)ctx->nodes_host.size();
+    const uint32_t n = ctx->stats.n_nodes;  // the first ordering
     if (n_out) *n_out = n;
     if (out) std::memcpy(out, ctx->nodes_host.data(), sizeof(rtw_node) * (cap < n ? cap : n));
     return RTW_OK;

@@ -62,6 +62,7 @@ struct rtw_launch {
     uint32_t postpone;           // 1 = postpone leaf tests until leaf_min/64 of the walking lanes hold one
     uint32_t leaf_min;           // postponement threshold in 1/64ths of the walking lanes
     uint32_t refill_min;         // wavefront trace: refill idle lanes once >= refill_min are idle (0 = off)
+    uint32_t n_orders;           // 1, or 8 octant-ordered copies of the node array (SAH trees)
 };
 
 #define RTW_TILE_W 16
@@ -142,8 +143,11 @@ struct rtw_geometry {
 // Validates the object graph, derives the geometry records and builds the BVH
 // over world_objects.  box_pad/extent (out, may be null): SAH trees pad every
 // inner box by extent * 2^-19 so the FMA slab test (box_next) stays conservative.
+// SAH trees: `orders` (1 or 8) pre-order arrays, one per ray-direction octant when 8
+// (concatenated; node indices and skip links are relative to each array).
 int rtw_build_bvh(const rtw_scene_desc& desc, std::vector<rtw_node>& nodes, rtw_geometry& geom,
-                  uint32_t* depth, uint32_t* axis_draws, float* box_pad = nullptr, float* extent = nullptr);
+                  uint32_t* depth, uint32_t* axis_draws, float* box_pad = nullptr, float* extent = nullptr,
+                  uint32_t orders = 1);
 
 // One scene on one device (the opaque rtw_ctx of include/rtw_gpu.h).
 struct rtw_ctx {

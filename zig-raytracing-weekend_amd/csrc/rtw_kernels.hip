@@ -112,6 +112,7 @@ __global__ __launch_bounds__(256, WAVES) void render_persistent_v1(rtw_launch L)
     float closest = kInf;
     int hit = -1;
     int pend = -1;  // parked leaf (leaf postponement), -1 = none
+    const float4* nb = nodes;  // this lane's node array (octant copy, order_base)
     Counters cnt;
     uint32_t samples_done = 0;
 #if defined(RTW_STAMPS)
@@ -203,6 +204,7 @@ __global__ __launch_bounds__(256, WAVES) void render_persistent_v1(rtw_launch L)
                     hit = -2;
                 } else {
                     rt = ray_trav(ray, L.fast_box != 0);
+                    nb = order_base(nodes, L, ray);
                     ti = 0;
                     closest = kInf;
                     hit = -1;
@@ -232,7 +234,7 @@ __global__ __launch_bounds__(256, WAVES) void render_persistent_v1(rtw_launch L)
                     // larger `closest` (superset of visits, same closest hit).
                     if (st == ST_TRAV && pend < 0) {
                         float4 A, B;
-                        load_node(nodes, ti, A, B);
+                        load_node(nb, ti, A, B);
                         const uint32_t w = fbits(A.w);
                         if (w & RTW_LEAF_BIT) {
                             pend = (int)ti;
@@ -248,7 +250,7 @@ __global__ __launch_bounds__(256, WAVES) void render_persistent_v1(rtw_launch L)
                     if (n_park && (n_park == n_walk || n_park * 64u >= n_walk * L.leaf_min)) {
                         if (st == ST_TRAV && pend >= 0) {
                             float4 A, B;
-                            load_node(nodes, (uint32_t)pend, A, B);
+                            load_node(nb, (uint32_t)pend, A, B);
                             leaf_test<FEAT>(L, ray, rt, A, B, (uint32_t)pend, closest, hit, cnt, rng.s);
                             pend = -1;
                             if (ti >= n_nodes) st = ST_SHADE;
@@ -258,7 +260,7 @@ __global__ __launch_bounds__(256, WAVES) void render_persistent_v1(rtw_launch L)
 #pragma unroll
                     for (int u = 0; u < RTW_STEPS; u++) {
                         if (st == ST_TRAV) {
-                            ti = trav_step<FEAT>(nodes, L, ray, rt, ti, closest, hit, cnt, rng.s);
+                            ti = trav_step<FEAT>(nb, L, ray, rt, ti, closest, hit, cnt, rng.s);
                             if (ti >= n_nodes) st = ST_SHADE;
                         }
                     }
@@ -298,6 +300,7 @@ __global__ __launch_bounds__(256, WAVES) void render_persistent_v1(rtw_launch L)
                         ray = sc;
                         depth--;
                         rt = ray_trav(ray, L.fast_box != 0);
+                        nb = order_base(nodes, L, ray);
                         ti = 0;
                         closest = kInf;
                         hit = -1;

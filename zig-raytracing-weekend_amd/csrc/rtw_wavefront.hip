@@ -185,6 +185,7 @@ __global__ __launch_bounds__(256) void wf_trace(rtw_launch L, rtw_wf W, uint32_t
         const bool fast = L.fast_box != 0;
         uint32_t cursor = 0, p = 0, ti = 0;
         uint64_t mkey = 0;
+        const float4* nb = L.nodes;
         bool active = false, exhausted = false;
         Ray r;
         r.o = r.d = mk(0, 0, 0);
@@ -208,6 +209,7 @@ __global__ __launch_bounds__(256) void wf_trace(rtw_launch L, rtw_wf W, uint32_t
                     if (depth) {
                         p = q;
                         mkey = wf_mkey<FEAT>(W, q);
+                        nb = order_base(L.nodes, L, r);
                         rt = ray_trav(r, fast);
                         ti = 0;
                         closest = kInf;
@@ -222,7 +224,7 @@ __global__ __launch_bounds__(256) void wf_trace(rtw_launch L, rtw_wf W, uint32_t
                 continue;
             }
             if (active) {
-                ti = trav_step<FEAT>(L.nodes, L, r, rt, ti, closest, hit, cnt, mkey);
+                ti = trav_step<FEAT>(nb, L, r, rt, ti, closest, hit, cnt, mkey);
                 if (ti >= L.n_nodes) {
                     W.hit[p] = make_float2(closest, __int_as_float(hit));
                     active = false;
