@@ -475,6 +475,8 @@ int run_wavefront(rtw_ctx* ctx, rtw_launch L, hipStream_t stream, rtw_timer* T) 
     auto stripe_cap = [&](uint64_t paths) {
         return ((paths + 63) / 64 / RTW_WF_STRIPES + 1 + max_waves / RTW_WF_STRIPES) * 64;
     };
+    // slots per set: every path (iteration 0: slot = path id) or every stripe's capacity
+    auto slots = [&](uint64_t paths) { return std::max<uint64_t>(paths, stripe_cap(paths) * RTW_WF_STRIPES); };
     if (ctx->wf_cap < need) {
         if (ctx->d_wf) {
             HIP_TRY(hipStreamSynchronize(stream));
@@ -482,22 +484,32 @@ int run_wavefront(rtw_ctx* ctx, rtw_launch L, hipStream_t stream, rtw_timer* T) 
         }
         ctx->d_wf = nullptr;
         ctx->wf_cap = 0;
-        const size_t bytes = need * RTW_WF_PATH_BYTES + 2 * stripe_cap(need) * RTW_WF_STRIPES * 4 +
-                             2 * RTW_WF_STRIPES * RTW_WF_LEN_STRIDE * 4 + 256;
+        const uint64_t Q = slots(need);
+        const size_t bytes = 2 * Q * (4 * 16 + 8 + 4) + Q * 8 + need * 16 +
+                             2 * RTW_WF_STRIPES * RTW_WF_LEN_STRIDE * 4 + 16 * 256;
         HIP_TRY(hipMalloc(&ctx->d_wf, bytes));
         ctx->wf_cap = need;
     }
-    const uint64_t P = ctx->wf_cap, qcap = stripe_cap(P) * RTW_WF_STRIPES;
-    W.ray_o = (float4*)ctx->d_wf;
-    W.ray_d = W.ray_o + P;
-    W.thr = W.ray_d + P;
-    W.ls = W.thr + P;
-    W.rng = (uint64_t*)(W.ls + P);
-    W.hit = (float2*)(W.rng + P);
-    W.queue[0] = (uint32_t*)(W.hit + P);
-    W.queue[1] = W.queue[0] + qcap;
-    W.len[0] = W.queue[1] + qcap;
-    W.len[1] = W.len[0] + RTW_WF_STRIPES * RTW_WF_LEN_STRIDE;
+    const uint64_t P = ctx->wf_cap, Q = slots(P);
+    char* cur = static_cast<char*>(ctx->d_wf);
+    auto take = [&](size_t nb) {
+        char* p = cur;
+        cur += (nb + 255) & ~size_t(255);
+        return p;
+    };
+    for (int k = 0; k < 2; k++) {
+        rtw_wf_set& S = W.set[k];
+        S.ray_o = reinterpret_cast<float4*>(take(Q * 16));
+        S.ray_d = reinterpret_cast<float4*>(take(Q * 16));
+        S.thr = reinterpret_cast<float4*>(take(Q * 16));
+        S.acc = reinterpret_cast<float4*>(take(Q * 16));
+        S.rng = reinterpret_cast<uint64_t*>(take(Q * 8));
+        S.pid = reinterpret_cast<uint32_t*>(take(Q * 4));
+    }
+    W.hit = reinterpret_cast<float2*>(take(Q * 8));
+    W.ls = reinterpret_cast<float4*>(take(P * 16));
+    W.len[0] = reinterpret_cast<uint32_t*>(take(RTW_WF_STRIPES * RTW_WF_LEN_STRIDE * 4));
+    W.len[1] = reinterpret_cast<uint32_t*>(take(RTW_WF_STRIPES * RTW_WF_LEN_STRIDE * 4));
     W.n_pix = (uint32_t)n_pix;
     W.iters = ctx->wf_iters;
     const uint32_t s_end = L.s1;

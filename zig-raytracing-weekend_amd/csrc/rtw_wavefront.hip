@@ -40,67 +40,70 @@ __device__ __forceinline__ bool wf_pixel(const rtw_launch& L, const rtw_wf& W, u
 __device__ __forceinline__ uint32_t wf_wave() { return blockIdx.x * 4u + (threadIdx.x >> 6); }
 __device__ __forceinline__ uint32_t wf_nwaves() { return gridDim.x * 4u; }
 
-// The paths of iteration `it` handed to this wave, 64 at a time:
-//   for (WfIter e(W, it); e.more(); e.next()) { uint32_t p; if (e.get(W, p)) ... }
+// The slots of iteration `it` handed to this wave, 64 at a time:
+//   for (WfIter e(W, it); e.more(); e.next()) { uint32_t slot; if (e.get(W, slot)) ... }
 // (wave-uniform loop; get() is per lane)
 struct WfIter {
-    uint32_t it, j, step, n, base;
-    const uint32_t* q;
+    uint32_t it, j, step, n, base, off;
     __device__ WfIter(const rtw_wf& W, uint32_t it_) : it(it_) {
         const uint32_t w = wf_wave(), nw = wf_nwaves();
         if (it == 0) {
             j = w;
             step = nw;
             n = (W.n_paths + 63u) >> 6;  // chunks
-            q = nullptr;
-            base = 0;
+            base = W.n_paths;
+            off = 0;
         } else {
             const uint32_t s = w % RTW_WF_STRIPES;
             j = w / RTW_WF_STRIPES;
             step = nw / RTW_WF_STRIPES;
-            n = (W.len[it & 1u][s * RTW_WF_LEN_STRIDE] + 63u) >> 6;
-            q = W.queue[it & 1u] + (size_t)s * W.stripe_cap;
-            base = W.len[it & 1u][s * RTW_WF_LEN_STRIDE];  // entries in the stripe
+            base = W.len[it & 1u][s * RTW_WF_LEN_STRIDE];  // slots used in the stripe
+            n = (base + 63u) >> 6;
+            off = s * W.stripe_cap;
         }
     }
     __device__ bool more() const { return j < n; }
     __device__ void next() { j += step; }
-    __device__ bool get(const rtw_wf& W, uint32_t& p) const {
+    __device__ bool get(const rtw_wf&, uint32_t& slot) const {
         const uint32_t k = (j << 6) | __lane_id();
-        if (it == 0) {
-            p = k;
-            return p < W.n_paths;
-        }
-        if (k >= base) return false;
-        p = q[k];
-        return true;
+        slot = off + k;
+        return k < base;
     }
 };
 
-// wave-aggregated append of `p` (where push) to this wave's output stripe
-__device__ __forceinline__ void wf_push(const rtw_wf& W, uint32_t it, bool push, uint32_t p) {
+// m-th slot of this wave's list at iteration it (the WfIter order); false past the
+// end or for padding.  `end` is set when m is past the list.
+__device__ __forceinline__ bool wf_nth(const rtw_wf& W, uint32_t it, uint32_t m, uint32_t& slot, bool& end) {
+    const uint32_t w = wf_wave(), nw = wf_nwaves();
+    if (it == 0) {
+        const uint32_t chunk = w + (m >> 6) * nw;
+        slot = (chunk << 6) | (m & 63u);
+        end = chunk >= ((W.n_paths + 63u) >> 6);
+        return slot < W.n_paths;
+    }
+    const uint32_t s = w % RTW_WF_STRIPES, R = nw / RTW_WF_STRIPES;
+    const uint32_t k = ((((m >> 6) * R) + w / RTW_WF_STRIPES) << 6) | (m & 63u);
+    const uint32_t n = W.len[it & 1u][s * RTW_WF_LEN_STRIDE];
+    end = (k & ~63u) >= n;
+    slot = s * W.stripe_cap + k;
+    return k < n;
+}
+
+// wave-aggregated slot allocation in this wave's output stripe of set[(it+1)&1]
+__device__ __forceinline__ uint32_t wf_push(const rtw_wf& W, uint32_t it, bool push) {
     const uint64_t m = __ballot(push);
-    if (!m) return;
+    if (!m) return 0;
     const uint32_t s = wf_wave() % RTW_WF_STRIPES, lane = __lane_id();
     uint32_t* len = &W.len[(it + 1u) & 1u][s * RTW_WF_LEN_STRIDE];
     uint32_t base = 0;
     if (lane == 0) base = atomicAdd(len, (uint32_t)__popcll(m));
     base = __shfl(base, 0);
-    if (push) {
-        const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-        W.queue[(it + 1u) & 1u][(size_t)s * W.stripe_cap + base + (uint32_t)__popcll(m & lt)] = p;
-    }
+    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    return s * W.stripe_cap + base + (uint32_t)__popcll(m & lt);
 }
 
-// the path's RNG state keys ConstantMedium draws (only read in scenes with media)
-template <uint32_t FEAT>
-__device__ __forceinline__ uint64_t wf_mkey(const rtw_wf& W, uint32_t p) {
-    if constexpr ((FEAT & RTW_F_MEDIUM) != 0) return W.rng[p];
-    return 0;
-}
-
-__device__ __forceinline__ Ray wf_load_ray(const rtw_wf& W, uint32_t p, uint32_t& depth) {
-    const float4 o = W.ray_o[p], d = W.ray_d[p];
+__device__ __forceinline__ Ray wf_load_ray(const rtw_wf_set& S, uint32_t slot, uint32_t& depth) {
+    const float4 o = S.ray_o[slot], d = S.ray_d[slot];
     Ray r;
     r.o = mk(o.x, o.y, o.z);
     r.time = o.w;
@@ -109,23 +112,30 @@ __device__ __forceinline__ Ray wf_load_ray(const rtw_wf& W, uint32_t p, uint32_t
     return r;
 }
 
-__device__ __forceinline__ void wf_store_ray(const rtw_wf& W, uint32_t p, const Ray& r, uint32_t depth) {
-    W.ray_o[p] = make_float4(r.o.x, r.o.y, r.o.z, r.time);
-    W.ray_d[p] = make_float4(r.d.x, r.d.y, r.d.z, __uint_as_float(depth));
+__device__ __forceinline__ void wf_store_ray(const rtw_wf_set& S, uint32_t slot, const Ray& r, uint32_t depth) {
+    S.ray_o[slot] = make_float4(r.o.x, r.o.y, r.o.z, r.time);
+    S.ray_d[slot] = make_float4(r.d.x, r.d.y, r.d.z, __uint_as_float(depth));
 }
 
-// throughput and radiance of path p: implicit (1, 0) on its first bounce; the
-// radiance is only ever non-zero before the path ends in scenes with emitters
+// the path's RNG state keys ConstantMedium draws (only read in scenes with media)
 template <uint32_t FEAT>
-__device__ __forceinline__ void wf_load_state(const rtw_launch& L, const rtw_wf& W, uint32_t p, uint32_t depth,
+__device__ __forceinline__ uint64_t wf_mkey(const rtw_wf_set& S, uint32_t slot) {
+    if constexpr ((FEAT & RTW_F_MEDIUM) != 0) return S.rng[slot];
+    return 0;
+}
+
+// throughput and radiance: implicit (1, 0) on the first bounce; the radiance is
+// only non-zero before the path ends in scenes with emitters
+template <uint32_t FEAT>
+__device__ __forceinline__ void wf_load_state(const rtw_launch& L, const rtw_wf_set& S, uint32_t slot, uint32_t depth,
                                               f3& thr, f3& acc) {
     thr = mk(1, 1, 1);
     acc = mk(0, 0, 0);
     if (depth != L.max_depth) {
-        const float4 t4 = W.thr[p];
+        const float4 t4 = S.thr[slot];
         thr = mk(t4.x, t4.y, t4.z);
         if constexpr ((FEAT & RTW_F_LIGHT) != 0) {
-            const float4 l4 = W.ls[p];
+            const float4 l4 = S.acc[slot];
             acc = mk(l4.x, l4.y, l4.z);
         }
     }
@@ -137,45 +147,27 @@ __global__ __launch_bounds__(256) void wf_gen(rtw_launch L, rtw_wf W) {
     if (p >= W.n_paths) return;
     const uint32_t s_local = p / W.n_pix, q = p - s_local * W.n_pix;
     uint32_t pixel, out_idx, x, y;
-    // thr = 1 and radiance = 0 are implicit while depth == max_depth (not stored)
+    const rtw_wf_set& S = W.set[0];  // iteration 0: slot = path id
     if (wf_pixel(L, W, q, pixel, out_idx, x, y) && L.max_depth > 0) {
         const uint32_t s = L.s0 + s_local;
         rtw_rng rng;
         rng.s = rtw_mix64(L.key0 ^ (((uint64_t)pixel << 32) | (uint64_t)s));
         const Ray r = get_ray(L, x + L.pixel_offset, y + L.pixel_offset, rng);  // camera.zig:100-101
-        wf_store_ray(W, p, r, L.max_depth);
-        W.rng[p] = rng.s;
+        wf_store_ray(S, p, r, L.max_depth);
+        S.rng[p] = rng.s;
     } else {
-        W.ray_d[p] = make_float4(0, 0, 0, 0);  // depth 0: no path (padding / outside the range)
+        S.ray_d[p] = make_float4(0, 0, 0, 0);  // depth 0: no path (padding / outside the range)
         W.ls[p] = make_float4(0, 0, 0, 0);     // rayColor(r, 0) = 0
     }
 }
 
-// m-th path of this wave's list at iteration it (see WfIter); false past the end
-// or for padding.  `end` (wave-uniform) is set when m is past the list.
-__device__ __forceinline__ bool wf_nth(const rtw_wf& W, uint32_t it, uint32_t m, uint32_t& p, bool& end) {
-    const uint32_t w = wf_wave(), nw = wf_nwaves();
-    if (it == 0) {
-        const uint32_t chunk = w + (m >> 6) * nw;
-        p = (chunk << 6) | (m & 63u);
-        end = chunk >= ((W.n_paths + 63u) >> 6);
-        return p < W.n_paths;
-    }
-    const uint32_t s = w % RTW_WF_STRIPES, R = nw / RTW_WF_STRIPES;
-    const uint32_t k = ((((m >> 6) * R) + w / RTW_WF_STRIPES) << 6) | (m & 63u);
-    const uint32_t n = W.len[it & 1u][s * RTW_WF_LEN_STRIDE];
-    end = (k & ~63u) >= n;
-    if (k >= n) return false;
-    p = W.queue[it & 1u][(size_t)s * W.stripe_cap + k];
-    return true;
-}
-
-// trace: closest hit per queued ray (no shading state in registers)
+// trace: closest hit per ray of the input set (no shading state in registers)
 template <uint32_t FEAT>
 __global__ __launch_bounds__(256) void wf_trace(rtw_launch L, rtw_wf W, uint32_t it) {
     // the stripes shade(it) appends to start empty (they were iteration it-1's input)
     if (blockIdx.x == 0) W.len[(it + 1u) & 1u][threadIdx.x * RTW_WF_LEN_STRIDE] = 0;
     static_assert(RTW_WF_STRIPES == 256, "one block zeroes the stripe counters");
+    const rtw_wf_set& S = W.set[it & 1u];
     Counters cnt;
     if (L.refill_min) {
         // per-lane refill: a lane whose walk is done takes the wave's next ray
@@ -183,7 +175,7 @@ __global__ __launch_bounds__(256) void wf_trace(rtw_launch L, rtw_wf W, uint32_t
         const uint32_t lane = __lane_id();
         const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
         const bool fast = L.fast_box != 0;
-        uint32_t cursor = 0, p = 0, ti = 0;
+        uint32_t cursor = 0, slot = 0, ti = 0;
         uint64_t mkey = 0;
         const float4* nb = L.nodes;
         bool active = false, exhausted = false;
@@ -205,10 +197,10 @@ __global__ __launch_bounds__(256) void wf_trace(rtw_launch L, rtw_wf W, uint32_t
                 exhausted = __ballot(end && !active) == idle;  // every idle lane ran past the list
                 if (!active && ok) {
                     uint32_t depth;
-                    r = wf_load_ray(W, q, depth);
+                    r = wf_load_ray(S, q, depth);
                     if (depth) {
-                        p = q;
-                        mkey = wf_mkey<FEAT>(W, q);
+                        slot = q;
+                        mkey = wf_mkey<FEAT>(S, q);
                         nb = order_base(L.nodes, L, r);
                         rt = ray_trav(r, fast);
                         ti = 0;
@@ -226,7 +218,7 @@ __global__ __launch_bounds__(256) void wf_trace(rtw_launch L, rtw_wf W, uint32_t
             if (active) {
                 ti = trav_step<FEAT>(nb, L, r, rt, ti, closest, hit, cnt, mkey);
                 if (ti >= L.n_nodes) {
-                    W.hit[p] = make_float2(closest, __int_as_float(hit));
+                    W.hit[slot] = make_float2(closest, __int_as_float(hit));
                     active = false;
                 }
             }
@@ -235,14 +227,14 @@ __global__ __launch_bounds__(256) void wf_trace(rtw_launch L, rtw_wf W, uint32_t
         return;
     }
     for (WfIter e(W, it); e.more(); e.next()) {
-        uint32_t p;
-        if (e.get(W, p)) {
+        uint32_t slot;
+        if (e.get(W, slot)) {
             uint32_t depth;
-            const Ray r = wf_load_ray(W, p, depth);
+            const Ray r = wf_load_ray(S, slot, depth);
             if (depth) {
                 float t;
-                const int h = traverse<FEAT>(L.nodes, L, r, t, cnt, wf_mkey<FEAT>(W, p));
-                W.hit[p] = make_float2(t, __int_as_float(h));
+                const int h = traverse<FEAT>(L.nodes, L, r, t, cnt, wf_mkey<FEAT>(S, slot));
+                W.hit[slot] = make_float2(t, __int_as_float(h));
                 cnt.rays++;
             }
         }
@@ -250,40 +242,47 @@ __global__ __launch_bounds__(256) void wf_trace(rtw_launch L, rtw_wf W, uint32_t
     flush_counters(L, cnt, 0);
 }
 
-// shade: emission / background and Material.scatter; survivors -> next queue
+// shade: emission / background and Material.scatter; a surviving path's state
+// moves to its slot in the other set; an ending path stores its radiance by id
 template <uint32_t FEAT>
 __global__ __launch_bounds__(256) void wf_shade(rtw_launch L, rtw_wf W, uint32_t it) {
+    const rtw_wf_set& S = W.set[it & 1u];
+    const rtw_wf_set& O = W.set[(it + 1u) & 1u];
     for (WfIter e(W, it); e.more(); e.next()) {
         bool push = false;
-        uint32_t p = 0;
-        if (e.get(W, p)) {
-            uint32_t depth;
-            const Ray r = wf_load_ray(W, p, depth);
+        uint32_t slot = 0, pid = 0, depth = 0;
+        f3 thr = mk(0, 0, 0), acc = mk(0, 0, 0);
+        rtw_rng rng;
+        rng.s = 0;
+        Ray sc;
+        if (e.get(W, slot)) {
+            const Ray r = wf_load_ray(S, slot, depth);
             if (depth) {
-                const float2 h = W.hit[p];
+                pid = it == 0 ? slot : S.pid[slot];
+                const float2 h = W.hit[slot];
                 const int hit = __float_as_int(h.y);
-                f3 thr, acc;
-                wf_load_state<FEAT>(L, W, p, depth, thr, acc);
+                wf_load_state<FEAT>(L, S, slot, depth, thr, acc);
                 if (hit < 0) {
                     acc = acc + thr * background(L, r);
                 } else {
-                    rtw_rng rng;
-                    rng.s = W.rng[p];
+                    rng.s = S.rng[slot];
                     f3 att;
-                    Ray sc;
                     if (shade<FEAT>(L.nodes, L, r, hit, h.x, rng, thr, acc, att, sc) && depth > 1) {
-                        wf_store_ray(W, p, sc, depth - 1);
                         thr = thr * att;
-                        W.thr[p] = make_float4(thr.x, thr.y, thr.z, 0);
-                        W.rng[p] = rng.s;
                         push = true;
                     }
                 }
-                // without emitters the radiance stays 0 until the path ends
-                if (!push || (FEAT & RTW_F_LIGHT) != 0) W.ls[p] = make_float4(acc.x, acc.y, acc.z, 0);
+                if (!push) W.ls[pid] = make_float4(acc.x, acc.y, acc.z, 0);
             }
         }
-        wf_push(W, it, push, p);
+        const uint32_t out = wf_push(W, it, push);
+        if (push) {
+            wf_store_ray(O, out, sc, depth - 1);
+            O.thr[out] = make_float4(thr.x, thr.y, thr.z, 0);
+            O.rng[out] = rng.s;
+            O.pid[out] = pid;
+            if constexpr ((FEAT & RTW_F_LIGHT) != 0) O.acc[out] = make_float4(acc.x, acc.y, acc.z, 0);
+        }
     }
 }
 
@@ -291,34 +290,37 @@ __global__ __launch_bounds__(256) void wf_shade(rtw_launch L, rtw_wf W, uint32_t
 // completion; a lane whose path ends takes the wave's next path at once
 template <uint32_t FEAT>
 __global__ __launch_bounds__(256) void wf_tail(rtw_launch L, rtw_wf W, uint32_t it) {
-    const uint32_t w = wf_wave(), lane = __lane_id();
-    const uint32_t s = w % RTW_WF_STRIPES, r0 = w / RTW_WF_STRIPES, R = wf_nwaves() / RTW_WF_STRIPES;
-    const uint32_t n = W.len[it & 1u][s * RTW_WF_LEN_STRIDE];
-    const uint32_t* q = W.queue[it & 1u] + (size_t)s * W.stripe_cap;
+    const uint32_t lane = __lane_id();
     const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    const rtw_wf_set& S = W.set[it & 1u];
     Counters cnt;
-    uint32_t cursor = 0, p = 0, depth = 0;
-    bool active = false;
+    uint32_t cursor = 0, pid = 0, depth = 0;
+    bool active = false, exhausted = false;
     Ray r;
     f3 thr = mk(0, 0, 0), acc = mk(0, 0, 0);
     rtw_rng rng;
     rng.s = 0;
     for (;;) {
         const uint64_t need = __ballot(!active);
-        if (need) {
-            // m-th path of this wave = stripe entry ((m / 64) * R + r0) * 64 + m % 64
+        if (need && !exhausted) {
             const uint32_t m = cursor + (uint32_t)__popcll(need & lt);
             cursor += (uint32_t)__popcll(need);
-            const uint32_t k = (((m >> 6) * R + r0) << 6) | (m & 63u);
-            if (!active && k < n) {
-                p = q[k];
-                r = wf_load_ray(W, p, depth);
-                wf_load_state<FEAT>(L, W, p, depth, thr, acc);
-                rng.s = W.rng[p];
-                active = true;
+            bool end = false;
+            uint32_t slot = 0;
+            const bool ok = wf_nth(W, it, m, slot, end);
+            exhausted = __ballot(end && !active) == need;
+            if (!active && ok) {
+                r = wf_load_ray(S, slot, depth);
+                wf_load_state<FEAT>(L, S, slot, depth, thr, acc);
+                rng.s = S.rng[slot];
+                pid = it == 0 ? slot : S.pid[slot];
+                active = depth != 0;
             }
         }
-        if (!__ballot(active)) break;
+        if (!__ballot(active)) {
+            if (exhausted) break;
+            continue;
+        }
         if (active) {  // one more iteration of rayColor
             cnt.rays++;
             cnt.tail_rays++;
@@ -338,7 +340,7 @@ __global__ __launch_bounds__(256) void wf_tail(rtw_launch L, rtw_wf W, uint32_t 
                 }
             }
             if (done) {
-                W.ls[p] = make_float4(acc.x, acc.y, acc.z, 0);
+                W.ls[pid] = make_float4(acc.x, acc.y, acc.z, 0);
                 active = false;
             }
         }
