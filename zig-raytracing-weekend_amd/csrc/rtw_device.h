@@ -617,6 +617,55 @@ __device__ __forceinline__ int traverse(const float4* __restrict__ nodes, const 
     return hit;
 }
 
+// traverse() with leaf postponement (Aila & Laine 2009 "while-while"): a lane
+// that reaches a leaf parks it and the wave keeps stepping inner nodes for the
+// others until leaf_min/64 of the walking lanes hold one; then every parked leaf
+// is tested in one pass, so a wave step runs either the box or the sphere code,
+// not both.  Leaves are tested in walk order per lane; boxes passed meanwhile
+// saw a larger `closest` (a superset of visits, the same closest hit).
+// Must be called by the whole wave (ballots); `walking` = this lane has a ray.
+template <uint32_t FEAT>
+__device__ __forceinline__ int traverse_postponed(const float4* __restrict__ nodes, const rtw_launch& L, const Ray& r,
+                                                  bool walking, float& t_out, Counters& cnt, uint64_t mkey = 0) {
+    nodes = order_base(nodes, L, r);
+    const RayTrav rt = ray_trav(r, L.fast_box != 0);
+    float closest = kInf;
+    int hit = -1, pend = -1;
+    uint32_t i = 0;
+    const uint32_t n = L.n_nodes;
+    bool active = walking;
+    for (;;) {
+        if (active && pend < 0 && i < n) {
+            float4 A, B;
+            load_node(nodes, i, A, B);
+            const uint32_t w = fbits(A.w);
+            if (w & RTW_LEAF_BIT) {
+                pend = (int)i;
+                i = w & RTW_SKIP_MASK;
+            } else {
+                cnt.nodes++;
+                i = box_next(r, rt, A, B, i, closest, L.fast_box != 0);
+            }
+        }
+        if (active && pend < 0 && i >= n) active = false;
+        const uint64_t walk = __ballot(active);
+        if (!walk) break;
+        const uint32_t n_walk = (uint32_t)__popcll(walk);
+        const uint32_t n_park = (uint32_t)__popcll(__ballot(active && pend >= 0));
+        if (n_park && (n_park == n_walk || n_park * 64u >= n_walk * L.leaf_min)) {
+            if (active && pend >= 0) {
+                float4 A, B;
+                load_node(nodes, (uint32_t)pend, A, B);
+                leaf_test<FEAT>(L, r, rt, A, B, (uint32_t)pend, closest, hit, cnt, mkey);
+                pend = -1;
+                if (i >= n) active = false;
+            }
+        }
+    }
+    t_out = closest;
+    return hit;
+}
+
 __device__ __forceinline__ f3 background(const rtw_launch& L, const Ray& r) {
     if (L.bg_mode == RTW_BG_GRADIENT) {  // camera.zig:204-206
         f3 ud = unit_vector(r.d);

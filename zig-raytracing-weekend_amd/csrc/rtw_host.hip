@@ -168,8 +168,11 @@ int rtw_scene_create(const rtw_scene_desc* d, int device, rtw_ctx** out) {
     ctx->device = device;
     rtw_geometry geom;
     uint32_t depth = 0, draws = 0;
-    // SAH trees: 8 octant-ordered copies of the node array (RTW_ORDERS=1: one, ordered along order_dir)
-    uint32_t orders = d->bvh_mode == RTW_BVH_SAH ? 8u : 1u;
+    // SAH trees of sphere scenes: 8 octant-ordered copies of the node array (RTW_ORDERS=1: one, ordered
+    // along order_dir).  Scenes with quads/instances/media keep one order: their leaf tests are costly, and
+    // lanes walking different orders stop executing them together (Cornell: -31 % with 8 orders).
+    const bool objects = d->n_quads || d->n_instances || d->n_media;
+    uint32_t orders = (d->bvh_mode == RTW_BVH_SAH && !objects) ? 8u : 1u;
     if (const char* o = std::getenv("RTW_ORDERS")) orders = (d->bvh_mode == RTW_BVH_SAH && std::atoi(o) == 8) ? 8u : 1u;
     int rc = rtw_build_bvh(*d, ctx->nodes_host, geom, &depth, &draws, &ctx->box_pad, &ctx->extent, orders);
     if (rc != RTW_OK) {
@@ -333,7 +336,7 @@ int rtw_scene_create(const rtw_scene_desc* d, int device, rtw_ctx** out) {
     // enlarge the set of visited nodes; reference trees keep the exact aabb.zig walk)
     const bool sah = ctx->box_pad > 0;
     L.fast_box = sah ? 1 : 0;
-    L.postpone = sah ? 1 : 0;
+    L.postpone = 0;  // measured: no gain in v1; wavefront trace: see RTW_POSTPONE A/B
     L.leaf_min = 32;
     L.refill_min = 0;
     if (const char* rm = std::getenv("RTW_REFILL_MIN")) {

@@ -226,6 +226,24 @@ __global__ __launch_bounds__(256) void wf_trace(rtw_launch L, rtw_wf W, uint32_t
         flush_counters(L, cnt, 0);
         return;
     }
+    if (L.postpone) {
+        for (WfIter e(W, it); e.more(); e.next()) {
+            uint32_t slot, depth = 0;
+            Ray r;
+            r.o = r.d = mk(0, 0, 0);
+            r.time = 0;
+            if (e.get(W, slot)) r = wf_load_ray(S, slot, depth);
+            float t;
+            const int h = traverse_postponed<FEAT>(L.nodes, L, r, depth != 0, t, cnt,
+                                                   depth ? wf_mkey<FEAT>(S, slot) : 0);
+            if (depth) {
+                W.hit[slot] = make_float2(t, __int_as_float(h));
+                cnt.rays++;
+            }
+        }
+        flush_counters(L, cnt, 0);
+        return;
+    }
     for (WfIter e(W, it); e.more(); e.next()) {
         uint32_t slot;
         if (e.get(W, slot)) {
