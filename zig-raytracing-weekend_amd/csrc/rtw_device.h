@@ -593,12 +593,21 @@ __device__ __forceinline__ uint32_t trav_step(const float4* __restrict__ nodes, 
 }
 
 // World hit for one ray (whole walk).  Returns leaf node index or -1.
-// The node array a ray walks: SAH scenes keep 8 copies, children ordered
-// front-to-back for each ray-direction octant (rtw_bvh.hip SahBuilder::build).
-__device__ __forceinline__ const float4* order_base(const float4* nodes, const rtw_launch& L, const Ray& r) {
-    if (L.n_orders <= 1) return nodes;
-    const uint32_t oct = (r.d.x < 0 ? 1u : 0u) | (r.d.y < 0 ? 2u : 0u) | (r.d.z < 0 ? 4u : 0u);
+// The node array a ray walks: SAH sphere scenes keep 8 copies, children ordered
+// front-to-back for each ray-direction octant (rtw_bvh.hip SahBuilder::build);
+// each lane walks its own octant's copy (a per-wave majority octant measured
+// slower: more node visits and no gain in coherence).  The copy is recorded in
+// the hit id (bits 24..26; such scenes have no instance members there) so
+// shading finds the leaf.
+__device__ __forceinline__ uint32_t order_of(const rtw_launch& L, const Ray& r) {
+    if (L.n_orders <= 1) return 0;
+    return (r.d.x < 0 ? 1u : 0u) | (r.d.y < 0 ? 2u : 0u) | (r.d.z < 0 ? 4u : 0u);
+}
+__device__ __forceinline__ const float4* order_base(const float4* nodes, const rtw_launch& L, uint32_t oct) {
     return nodes + (size_t)oct * 2u * L.n_nodes;
+}
+__device__ __forceinline__ int hit_with_order(int hit, uint32_t oct) {
+    return hit < 0 ? hit : (int)((uint32_t)hit | (oct << RTW_HIT_NODE_BITS));
 }
 
 // mkey: the path's RNG state (keys ConstantMedium draws; unused without media).
@@ -606,7 +615,8 @@ __device__ __forceinline__ const float4* order_base(const float4* nodes, const r
 template <uint32_t FEAT>
 __device__ __forceinline__ int traverse(const float4* __restrict__ nodes, const rtw_launch& L, const Ray& r,
                                         float& t_out, Counters& cnt, uint64_t mkey = 0) {
-    nodes = order_base(nodes, L, r);
+    const uint32_t oct = order_of(L, r);
+    nodes = order_base(nodes, L, oct);
     const RayTrav rt = ray_trav(r, L.fast_box != 0);
     float closest = kInf;
     int hit = -1;
@@ -614,7 +624,7 @@ __device__ __forceinline__ int traverse(const float4* __restrict__ nodes, const 
     const uint32_t n = L.n_nodes;
     while (i < n) i = trav_step<FEAT>(nodes, L, r, rt, i, closest, hit, cnt, mkey);
     t_out = closest;
-    return hit;
+    return hit_with_order(hit, oct);
 }
 
 // traverse() with leaf postponement (Aila & Laine 2009 "while-while"): a lane
@@ -627,7 +637,8 @@ __device__ __forceinline__ int traverse(const float4* __restrict__ nodes, const 
 template <uint32_t FEAT>
 __device__ __forceinline__ int traverse_postponed(const float4* __restrict__ nodes, const rtw_launch& L, const Ray& r,
                                                   bool walking, float& t_out, Counters& cnt, uint64_t mkey = 0) {
-    nodes = order_base(nodes, L, r);
+    const uint32_t oct = order_of(L, r);
+    nodes = order_base(nodes, L, oct);
     const RayTrav rt = ray_trav(r, L.fast_box != 0);
     float closest = kInf;
     int hit = -1, pend = -1;
@@ -663,7 +674,7 @@ __device__ __forceinline__ int traverse_postponed(const float4* __restrict__ nod
         }
     }
     t_out = closest;
-    return hit;
+    return hit_with_order(hit, oct);
 }
 
 __device__ __forceinline__ f3 background(const rtw_launch& L, const Ray& r) {
@@ -748,7 +759,10 @@ __device__ __forceinline__ HitPrep object_prep(const rtw_launch& L, const Ray& r
 template <uint32_t FEAT>
 __device__ __forceinline__ HitPrep hit_prep(const float4* __restrict__ nodes, const rtw_launch& L, const Ray& r,
                                             int hit, float t) {
-    nodes = order_base(nodes, L, r);
+    if (L.n_orders > 1) {  // sphere scenes only: the octant copy the walk used
+        nodes = order_base(nodes, L, (uint32_t)hit >> RTW_HIT_NODE_BITS);
+        hit &= (1 << RTW_HIT_NODE_BITS) - 1;
+    }
     if constexpr ((FEAT & RTW_F_GEOM) != 0) {
         const uint32_t node = (uint32_t)hit & ((1u << RTW_HIT_NODE_BITS) - 1u);
         const float4 B = nodes[2 * node + 1];

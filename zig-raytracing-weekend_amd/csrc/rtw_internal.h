@@ -62,7 +62,7 @@ struct rtw_launch {
     uint32_t postpone;           // 1 = postpone leaf tests until leaf_min/64 of the walking lanes hold one
     uint32_t leaf_min;           // postponement threshold in 1/64ths of the walking lanes
     uint32_t refill_min;         // wavefront trace: refill idle lanes once >= refill_min are idle (0 = off)
-    uint32_t n_orders;           // 1, or 8 octant-ordered copies of the node array (SAH trees)
+    uint32_t n_orders;           // 1, or 8 octant-ordered copies of the node array (SAH sphere scenes)
 };
 
 #define RTW_TILE_W 16

@@ -113,6 +113,7 @@ __global__ __launch_bounds__(256, WAVES) void render_persistent_v1(rtw_launch L)
     int hit = -1;
     int pend = -1;  // parked leaf (leaf postponement), -1 = none
     const float4* nb = nodes;  // this lane's node array (octant copy, order_base)
+    uint32_t oct = 0;
     Counters cnt;
     uint32_t samples_done = 0;
 #if defined(RTW_STAMPS)
@@ -204,7 +205,8 @@ __global__ __launch_bounds__(256, WAVES) void render_persistent_v1(rtw_launch L)
                     hit = -2;
                 } else {
                     rt = ray_trav(ray, L.fast_box != 0);
-                    nb = order_base(nodes, L, ray);
+                    oct = order_of(L, ray);
+                    nb = order_base(nodes, L, oct);
                     ti = 0;
                     closest = kInf;
                     hit = -1;
@@ -282,7 +284,7 @@ __global__ __launch_bounds__(256, WAVES) void render_persistent_v1(rtw_launch L)
             HitPrep hp;
             bool need_uv = false;
             if (shading && hit >= 0) {
-                hp = hit_prep<FEAT>(nodes, L, ray, hit, closest);
+                hp = hit_prep<FEAT>(nodes, L, ray, hit_with_order(hit, oct), closest);
                 need_uv = needs_unit_vector<FEAT>(hp.m.kind);
             }
             float ruv3[3] = {0.0f, 0.0f, 0.0f};
@@ -300,7 +302,8 @@ __global__ __launch_bounds__(256, WAVES) void render_persistent_v1(rtw_launch L)
                         ray = sc;
                         depth--;
                         rt = ray_trav(ray, L.fast_box != 0);
-                        nb = order_base(nodes, L, ray);
+                        oct = order_of(L, ray);
+                    nb = order_base(nodes, L, oct);
                         ti = 0;
                         closest = kInf;
                         hit = -1;

@@ -178,6 +178,7 @@ __global__ __launch_bounds__(256) void wf_trace(rtw_launch L, rtw_wf W, uint32_t
         uint32_t cursor = 0, slot = 0, ti = 0;
         uint64_t mkey = 0;
         const float4* nb = L.nodes;
+        uint32_t oct = 0;
         bool active = false, exhausted = false;
         Ray r;
         r.o = r.d = mk(0, 0, 0);
@@ -201,7 +202,8 @@ __global__ __launch_bounds__(256) void wf_trace(rtw_launch L, rtw_wf W, uint32_t
                     if (depth) {
                         slot = q;
                         mkey = wf_mkey<FEAT>(S, q);
-                        nb = order_base(L.nodes, L, r);
+                        oct = order_of(L, r);
+                        nb = order_base(L.nodes, L, oct);
                         rt = ray_trav(r, fast);
                         ti = 0;
                         closest = kInf;
@@ -218,7 +220,7 @@ __global__ __launch_bounds__(256) void wf_trace(rtw_launch L, rtw_wf W, uint32_t
             if (active) {
                 ti = trav_step<FEAT>(nb, L, r, rt, ti, closest, hit, cnt, mkey);
                 if (ti >= L.n_nodes) {
-                    W.hit[slot] = make_float2(closest, __int_as_float(hit));
+                    W.hit[slot] = make_float2(closest, __int_as_float(hit_with_order(hit, oct)));
                     active = false;
                 }
             }
