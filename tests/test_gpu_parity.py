@@ -315,10 +315,12 @@ def test_v1_knobs_invariant(rtw, book1, knob, monkeypatch):
 
 
 @pytest.mark.parametrize("knob", [("RTW_WF_ITERS", "1"), ("RTW_WF_ITERS", "50"), ("RTW_WF_PATHS", "4096"),
-                                  ("RTW_REFILL_MIN", "16"), ("RTW_FASTBOX", "0")])
+                                  ("RTW_REFILL_MIN", "16"), ("RTW_FASTBOX", "0"), ("RTW_WF_LDS", "0"),
+                                  ("RTW_SAH_LEAF", "4")])
 def test_wavefront_knobs_invariant(rtw, book1, knob, monkeypatch):
     """Wavefront knobs (bounces before the tail kernel, batch size -> many batches,
-    per-lane refill in trace, FMA vs reference slab test) never change a pixel."""
+    per-lane refill in trace, FMA vs reference slab test, LDS-staged nodes, SAH
+    leaf runs of up to 4 spheres) never change a pixel."""
     arr, world = book1
     cam = rtw.book1_camera(image_width=300, aspect_ratio=1.5, spp=5).init()
     ref = render_rows(rtw, world, cam, 0, 200, 0, 5, 4)

@@ -17,6 +17,7 @@
 #include <algorithm>
 #include <array>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -405,6 +406,8 @@ public:
         for (size_t i = 0; i < n; i++) idx_[i] = (uint32_t)i;
         for (int k = 0; k < 3; k++) dir_[k] = d.order_dir[k];
         if (dir_[0] == 0 && dir_[1] == 0 && dir_[2] == 0) dir_[1] = -1;
+        if (const char* e = std::getenv("RTW_SAH_LEAF")) max_leaf_ = (size_t)std::max(1, std::atoi(e));
+        if (const char* e = std::getenv("RTW_SAH_CI")) ci_ = (float)std::atof(e);
     }
     // orders = 1: one pre-order with children front-to-back along order_dir;
     // orders = 8: one pre-order per ray-direction octant (bit k set = negative
@@ -431,24 +434,30 @@ private:
     struct TNode {
         Box box;
         int left = -1, right = -1;
-        uint32_t obj = 0;  // leaf: index into objs_
+        uint32_t first = 0, count = 0;  // leaf: idx_[first, first + count)
     };
 
     int build_tree(size_t a, size_t b, uint32_t level) {
         depth_ = std::max(depth_, level);
         const int me = (int)tree_.size();
         tree_.push_back(TNode{});
-        if (b - a == 1) {
-            tree_[me].obj = idx_[a];
-            tree_[me].box = objs_[idx_[a]].box;
-            return me;
-        }
-        const size_t mid = split(a, b);
+        Box box = objs_[idx_[a]].box;
+        for (size_t i = a + 1; i < b; i++) box = box_union(box, objs_[idx_[i]].box);
+        tree_[me].box = box;
+        tree_[me].first = (uint32_t)a;
+        tree_[me].count = (uint32_t)(b - a);
+        if (b - a == 1) return me;
+        float sc;
+        const size_t mid = split(a, b, &sc);
+        // SAH termination: a leaf of up to max_leaf_ objects is a run of leaf records
+        // the walk tests one after the other with no box (cost n * ci_); a split costs
+        // one box test per child plus the area-weighted tests below it
+        if (b - a <= max_leaf_ && (float)(b - a) * ci_ <= 2.0f + ci_ * sc / area(box)) return me;
+        tree_[me].count = 0;
         const int l = build_tree(a, mid, level + 1);
         const int r = build_tree(mid, b, level + 1);
         tree_[me].left = l;
         tree_[me].right = r;
-        tree_[me].box = box_union(tree_[l].box, tree_[r].box);
         return me;
     }
 
@@ -456,7 +465,8 @@ private:
     void emit_tree(int t, const float dir[3]) {
         const TNode& n = tree_[t];
         if (n.left < 0) {
-            nodes_.push_back(geo_.leaf(objs_[n.obj], (uint32_t)nodes_.size() + 1 - base_));
+            for (uint32_t i = 0; i < n.count; i++)
+                nodes_.push_back(geo_.leaf(objs_[idx_[n.first + i]], (uint32_t)nodes_.size() + 1 - base_));
             return;
         }
         const Box& lb = tree_[n.left].box;
@@ -487,7 +497,8 @@ private:
         return 2.0f * (dx * dy + dy * dz + dz * dx);
     }
     // returns split position (index) after partitioning idx_[a, b)
-    size_t split(size_t a, size_t b) {
+    // binned SAH split of idx_[a, b); *cost = sum over the two sides of area x count
+    size_t split(size_t a, size_t b, float* cost) {
         const size_t n = b - a;
         float cmn[3] = {1e30f, 1e30f, 1e30f}, cmx[3] = {-1e30f, -1e30f, -1e30f};
         for (size_t i = a; i < b; i++)
@@ -547,6 +558,7 @@ private:
             mid = (size_t)(it - idx_.begin());
             if (mid == a || mid == b) mid = a + n / 2;
         }
+        *cost = best_axis < 0 ? 1e38f : best;
         return mid;
     }
     const Geometry& geo_;
@@ -558,6 +570,8 @@ private:
     std::vector<uint32_t> idx_;
     float dir_[3];
     uint32_t depth_ = 0;
+    size_t max_leaf_ = 1;  // objects per leaf run
+    float ci_ = 2.0f;      // cost of one leaf test relative to one box test
 };
 
 }  // namespace

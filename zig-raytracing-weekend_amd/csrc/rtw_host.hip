@@ -332,6 +332,10 @@ int rtw_scene_create(const rtw_scene_desc* d, int device, rtw_ctx** out) {
     if (const char* wv = std::getenv("RTW_WAVES")) L.waves = (uint32_t)std::atoi(wv);
     L.use_lds = orders == 1 ? 1 : 0;  // the octant copies do not fit the megakernel's LDS stage
     if (const char* ul = std::getenv("RTW_LDS")) L.use_lds = orders == 1 ? (uint32_t)std::atoi(ul) : 0;
+    // wavefront trace: node array staged in LDS when one ordering fits (object scenes,
+    // reference trees; +2 % on Cornell); the 8 octant copies of SAH sphere trees do not
+    L.wf_lds = 1;
+    if (const char* wl = std::getenv("RTW_WF_LDS")) L.wf_lds = (uint32_t)std::atoi(wl);
     // SAH trees: FMA slab test on the padded boxes + leaf postponement (both only
     // enlarge the set of visited nodes; reference trees keep the exact aabb.zig walk)
     const bool sah = ctx->box_pad > 0;

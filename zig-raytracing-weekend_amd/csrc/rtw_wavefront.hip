@@ -21,6 +21,8 @@
 #include "rtw_device.h"
 #include "rtw_wavefront.h"
 
+#include <cstdlib>
+
 namespace {
 
 // logical pixel q of the batch -> image pixel / output slot (false = padding)
@@ -162,13 +164,35 @@ __global__ __launch_bounds__(256) void wf_gen(rtw_launch L, rtw_wf W) {
 }
 
 // trace: closest hit per ray of the input set (no shading state in registers)
-template <uint32_t FEAT>
+template <uint32_t FEAT, bool LDS>
 __global__ __launch_bounds__(256) void wf_trace(rtw_launch L, rtw_wf W, uint32_t it) {
     // the stripes shade(it) appends to start empty (they were iteration it-1's input)
     if (blockIdx.x == 0) W.len[(it + 1u) & 1u][threadIdx.x * RTW_WF_LEN_STRIDE] = 0;
     static_assert(RTW_WF_STRIPES == 256, "one block zeroes the stripe counters");
     const rtw_wf_set& S = W.set[it & 1u];
     Counters cnt;
+    if constexpr (LDS) {
+        // the node array(s) staged in LDS: the walk's loads become ds_read_b128
+        extern __shared__ float4 wf_lds_nodes[];
+        const uint32_t n4 = 2u * L.n_nodes * L.n_orders;
+        for (uint32_t k = threadIdx.x; k < n4; k += 256u) wf_lds_nodes[k] = L.nodes[k];
+        __syncthreads();
+        for (WfIter e(W, it); e.more(); e.next()) {
+            uint32_t slot;
+            if (e.get(W, slot)) {
+                uint32_t depth;
+                const Ray r = wf_load_ray(S, slot, depth);
+                if (depth) {
+                    float t;
+                    const int h = traverse<FEAT>(wf_lds_nodes, L, r, t, cnt, wf_mkey<FEAT>(S, slot));
+                    W.hit[slot] = make_float2(t, __int_as_float(h));
+                    cnt.rays++;
+                }
+            }
+        }
+        flush_counters(L, cnt, 0);
+        return;
+    }
     if (L.refill_min) {
         // per-lane refill: a lane whose walk is done takes the wave's next ray
         // once refill_min lanes are idle (the refill stalls the wave on the loads)
@@ -394,9 +418,9 @@ __global__ __launch_bounds__(256) void wf_reduce(rtw_launch L, rtw_wf W) {
 
 // resident blocks of `kernel`, rounded down to whole stripes of waves
 template <typename K>
-uint32_t wf_grid(K kernel, int n_cu) {
+uint32_t wf_grid(K kernel, int n_cu, size_t lds = 0) {
     int b = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kernel, 256, 0) != hipSuccess || b < 1) b = 1;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kernel, 256, lds) != hipSuccess || b < 1) b = 1;
     uint32_t g = (uint32_t)(b * n_cu);
     g -= g % (RTW_WF_STRIPES / 4);
     return g ? g : RTW_WF_STRIPES / 4;
@@ -406,9 +430,20 @@ template <uint32_t FEAT>
 struct WfGrids {
     uint32_t trace, shade, tail;
     explicit WfGrids(int n_cu)
-        : trace(wf_grid(wf_trace<FEAT>, n_cu)), shade(wf_grid(wf_shade<FEAT>, n_cu)),
+        : trace(wf_grid(wf_trace<FEAT, false>, n_cu)), shade(wf_grid(wf_shade<FEAT>, n_cu)),
           tail(wf_grid(wf_tail<FEAT>, n_cu)) {}
 };
+
+// largest LDS stage of the wavefront trace (bytes); larger trees read L1/L2
+#define RTW_WF_LDS_MAX (64u * 1024u)
+
+template <uint32_t FEAT>
+uint32_t wf_lds_grid(int n_cu, size_t lds) {
+    static uint32_t cache[RTW_WF_LDS_MAX / 512 + 1] = {0};
+    uint32_t& g = cache[lds / 512];
+    if (!g) g = wf_grid(wf_trace<FEAT, true>, n_cu, lds);
+    return g;
+}
 
 template <uint32_t FEAT>
 const WfGrids<FEAT>& wf_grids(int n_cu) {
@@ -423,9 +458,21 @@ void wf_run(const rtw_launch& L, const rtw_wf& W, hipStream_t st, int n_cu, rtw_
     hipLaunchKernelGGL(wf_gen<FEAT>, dim3((W.n_paths + 255u) / 256u), dim3(256), 0, st, L, W);
     RTW_TIME_END(T)
     const uint32_t iters = L.max_depth < W.iters ? L.max_depth : W.iters;
+    const size_t lds_need = (size_t)L.n_nodes * L.n_orders * 32u;
+    const size_t lds = (L.wf_lds && !L.refill_min && !L.postpone && lds_need <= RTW_WF_LDS_MAX)
+                           ? (lds_need + 511u) / 512u * 512u : 0;
+    const uint32_t lds_grid = lds ? wf_lds_grid<FEAT>(n_cu, lds) : 0;
+    const char* op = std::getenv("RTW_TRACE_OCC_PAD");
+    const size_t occ_pad = op ? (size_t)std::atoi(op) : 0;
+    const uint32_t pad_grid = occ_pad ? wf_grid(wf_trace<FEAT, false>, n_cu, occ_pad) : 0;
     for (uint32_t it = 0; it < iters; it++) {
         RTW_TIME_BEGIN(T, RTW_K_TRACE)
-        hipLaunchKernelGGL(wf_trace<FEAT>, dim3(g.trace), dim3(256), 0, st, L, W, it);
+        if (lds)
+            hipLaunchKernelGGL((wf_trace<FEAT, true>), dim3(lds_grid), dim3(256), lds, st, L, W, it);
+        else if (occ_pad)  // DIAGNOSTIC: occupancy sweep (dynamic LDS limits resident blocks)
+            hipLaunchKernelGGL((wf_trace<FEAT, false>), dim3(pad_grid), dim3(256), occ_pad, st, L, W, it);
+        else
+            hipLaunchKernelGGL((wf_trace<FEAT, false>), dim3(g.trace), dim3(256), 0, st, L, W, it);
         RTW_TIME_END(T)
         RTW_TIME_BEGIN(T, RTW_K_SHADE)
         hipLaunchKernelGGL(wf_shade<FEAT>, dim3(g.shade), dim3(256), 0, st, L, W, it);
