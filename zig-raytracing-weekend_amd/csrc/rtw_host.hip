@@ -303,6 +303,16 @@ int rtw_scene_create(const rtw_scene_desc* d, int device, rtw_ctx** out) {
     L.work_counter = ctx->d_work;
     if (const char* kv = std::getenv("RTW_KERNEL"))
         ctx->variant = (std::strcmp(kv, "v0") == 0) ? 0 : (std::strcmp(kv, "v1") == 0) ? 1 : 2;
+    {
+        // wavefront batch capacity: up to 2^29 paths (BASELINE config 2 = 480M samples in one
+        // batch: one drain of long paths per render instead of one per 64M), within ~35 % of
+        // the device's memory (RTW_WF_PATH_BYTES per path)
+        size_t free_b = 0, total_b = 0;
+        uint64_t cap = 1ull << 29;
+        if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && total_b)
+            cap = std::min<uint64_t>(cap, (uint64_t)(0.35 * (double)total_b) / RTW_WF_PATH_BYTES);
+        ctx->wf_max_paths = std::max<uint64_t>(cap, 1u << 20);
+    }
     if (const char* wp = std::getenv("RTW_WF_PATHS")) {
         long long v = std::atoll(wp);
         if (v >= 4096) ctx->wf_max_paths = (uint64_t)v;
@@ -448,9 +458,11 @@ rtw_launch make_launch(const rtw_ctx* ctx, const rtw_camera* c, uint64_t seed) {
     return L;
 }
 
-uint32_t auto_batch(uint64_t pixels, uint32_t spp) {
-    // ~64M samples per launch: long enough to amortise the launch, short enough to poll cancel
-    uint64_t b = pixels ? (64ull << 20) / pixels : spp;
+uint32_t auto_batch(const rtw_ctx* ctx, uint64_t pixels, uint32_t spp) {
+    // ~64M samples per launch (the wavefront: its batch capacity): long enough to
+    // amortise the launches, short enough to poll cancel
+    const uint64_t target = ctx->variant == 2 ? ctx->wf_max_paths : (64ull << 20);
+    uint64_t b = pixels ? target / pixels : spp;
     if (b < 1) b = 1;
     if (b > spp) b = spp;
     return (uint32_t)b;
@@ -614,7 +626,7 @@ int rtw_render(rtw_ctx* ctx, const rtw_camera* cam, uint32_t pix_begin, uint32_t
     L.n_shards = 0;
     L.counters = nullptr;
     set_tiles(L);
-    const uint32_t batch = auto_batch(pix_end - pix_begin, spp_end - spp_begin);
+    const uint32_t batch = auto_batch(ctx, pix_end - pix_begin, spp_end - spp_begin);
     int rc = run_batches(ctx, L, spp_begin, spp_end, batch, ctx->stream, true, cancel, progress, user,
                          pix_end - pix_begin);
     // copy back whatever was rendered (also on cancel: completed batches are valid)
@@ -642,7 +654,7 @@ int rtw_render_device(rtw_ctx* ctx, const rtw_camera* cam, uint32_t pix_begin, u
     L.n_shards = 0;
     L.counters = opts ? reinterpret_cast<unsigned long long*>(opts->counters) : nullptr;
     set_tiles(L);
-    uint32_t batch = opts && opts->spp_batch ? opts->spp_batch : auto_batch(pix_end - pix_begin, spp_end - spp_begin);
+    uint32_t batch = opts && opts->spp_batch ? opts->spp_batch : auto_batch(ctx, pix_end - pix_begin, spp_end - spp_begin);
     rtw_timer T;
     T.stream = s;
     T.pool.swap(ctx->ev_pool);
@@ -691,7 +703,7 @@ int rtw_render_rows_device(rtw_ctx* ctx, const rtw_camera* cam, uint32_t rpb, ui
     L.pix_end = cam->size;
     L.counters = opts ? reinterpret_cast<unsigned long long*>(opts->counters) : nullptr;
     set_tiles(L);
-    uint32_t batch = opts && opts->spp_batch ? opts->spp_batch : auto_batch((uint64_t)rows * cam->image_width, spp_end - spp_begin);
+    uint32_t batch = opts && opts->spp_batch ? opts->spp_batch : auto_batch(ctx, (uint64_t)rows * cam->image_width, spp_end - spp_begin);
     rtw_timer T;
     T.stream = s;
     T.pool.swap(ctx->ev_pool);

@@ -169,8 +169,8 @@ struct rtw_ctx {
     uint32_t shade_min = 48;       // RTW_SHADE_MIN (tuned on C2: 8..64 -> 48 best)
     void* d_wf = nullptr;          // wavefront path state (rtw_wavefront.h), wf_cap paths
     uint64_t wf_cap = 0;
-    uint64_t wf_max_paths = 1u << 26;  // RTW_WF_PATHS: paths per wavefront batch (x ~90 B)
-    uint32_t wf_iters = 6;         // RTW_WF_ITERS: wavefront bounces before the tail kernel
+    uint64_t wf_max_paths = 1u << 26;  // RTW_WF_PATHS: paths per wavefront batch (x RTW_WF_PATH_BYTES); set at scene creation
+    uint32_t wf_iters = 9;         // RTW_WF_ITERS: wavefront bounces before the tail kernel
     int n_cu = 256;                // compute units of the device (wavefront grids)
     std::vector<hipEvent_t> ev_pool;  // recycled timing events
     uint64_t scene_hash = 0;       // FNV-1a 64 of the uploaded scene image
