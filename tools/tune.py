@@ -35,6 +35,7 @@ for st in [s for _ in range(rounds) for s in settings]:
     prev_keys = list(st.keys())
     world = pkg.World(arr)
     cnt = torch.zeros(8, dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()  # the render runs on `stream`: the zeroing must be done
     copts = pkg._abi.RtwRenderOpts(spp, 0, cnt.data_ptr())
     pkg._abi.check(pkg.lib().rtw_render_device(world.handle, C.byref(cam.derived), 0, cam.size, 0, 2, 0,
                                                acc.data_ptr(), C.c_void_p(stream.cuda_stream), C.byref(copts)), "count")

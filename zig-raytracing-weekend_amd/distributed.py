@@ -74,7 +74,10 @@ class ShardedRender:
         """Enqueue this rank's rows x samples [spp_begin, spp_end) on `stream`.
         timing: optional _abi.RtwKernelTiming filled with per-kernel device time
         (the call then synchronises the stream)."""
+        import torch
         self.tile.zero_()
+        if stream is not None and stream != torch.cuda.current_stream(self.tile.device):
+            stream.wait_stream(torch.cuda.current_stream(self.tile.device))  # the zeroing precedes the render
         flags = 0 if sync else _abi.RTW_RENDER_NO_SYNC
         opts = _abi.RtwRenderOpts(spp_batch, flags, counters, C.pointer(timing) if timing is not None else None)
         rc = _abi.lib().rtw_render_rows_device(self.world.handle, C.byref(self.cam.derived), self.rpb,
