@@ -316,11 +316,11 @@ def test_v1_knobs_invariant(rtw, book1, knob, monkeypatch):
 
 @pytest.mark.parametrize("knob", [("RTW_WF_ITERS", "1"), ("RTW_WF_ITERS", "50"), ("RTW_WF_PATHS", "4096"),
                                   ("RTW_REFILL_MIN", "16"), ("RTW_FASTBOX", "0"), ("RTW_WF_LDS", "0"),
-                                  ("RTW_SAH_LEAF", "4")])
+                                  ("RTW_SAH_LEAF", "4"), ("RTW_COMPACT", "0")])
 def test_wavefront_knobs_invariant(rtw, book1, knob, monkeypatch):
     """Wavefront knobs (bounces before the tail kernel, batch size -> many batches,
     per-lane refill in trace, FMA vs reference slab test, LDS-staged nodes, SAH
-    leaf runs of up to 4 spheres) never change a pixel."""
+    leaf runs of up to 4 spheres, 16-B fp16-box nodes vs 32-B nodes) never change a pixel."""
     arr, world = book1
     cam = rtw.book1_camera(image_width=300, aspect_ratio=1.5, spp=5).init()
     ref = render_rows(rtw, world, cam, 0, 200, 0, 5, 4)
@@ -329,6 +329,24 @@ def test_wavefront_knobs_invariant(rtw, book1, knob, monkeypatch):
     got = render_rows(rtw, w2, cam, 0, 200, 0, 5, 4)
     w2.close()
     assert np.array_equal(ref, got)
+
+
+@pytest.mark.parametrize("n,seed", [(20000, 3), (100000, 0)])
+def test_compact_nodes_are_exact(rtw, n, seed, monkeypatch):
+    """The 16-B node walk (fp16 inner boxes rounded outward, leaves with radius^2)
+    visits a superset of the 32-B walk's boxes: identical images on dense stress
+    worlds (small spheres far from the origin: the coarsest fp16 boxes), at the
+    BASELINE config-4 camera."""
+    arr = rtw.flatten(rtw.worlds.stress_world(n, seed), bvh_mode=rtw._abi.RTW_BVH_SAH)
+    cam = rtw.book1_camera(image_width=480, aspect_ratio=16 / 9, spp=4).init()
+    outs = []
+    for c in ("0", "1"):
+        monkeypatch.setenv("RTW_COMPACT", c)
+        w = rtw.World(arr)
+        outs.append(render_rows(rtw, w, cam, 0, cam.derived.image_height, 0, 4, 6))
+        w.close()
+    assert np.isfinite(outs[1]).all()
+    assert np.array_equal(outs[0], outs[1])
 
 
 @pytest.mark.parametrize("scene", ["book1", "stress"])

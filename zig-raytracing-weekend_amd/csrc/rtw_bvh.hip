@@ -620,3 +620,76 @@ int rtw_build_bvh(const rtw_scene_desc& desc, std::vector<rtw_node>& nodes, rtw_
     if (axis_draws) *axis_draws = b.axis_draws();
     return RTW_OK;
 }
+
+// ---------------------------------------------------------------------------
+// Compact 16-B nodes for the wavefront walk of static sphere SAH trees: one
+// dwordx4 per step instead of two (the walk is bound by the vector-memory
+// gather rate, not by arithmetic).  Same indices and skip links as the 32-B
+// array (hit ids and shading keep using it):
+//   inner: x = minx | miny << 16, y = minz | maxx << 16, z = maxy | maxz << 16
+//          (fp16, min rounded down and max up: a superset of the padded box,
+//          read by v_fma_mix_f32 at no conversion cost), w = skip
+//   leaf:  center.xyz (fp32), w = bits(radius * radius) | RTW_LEAF_BIT (the
+//          reference's `radius * radius`, objects.zig:126, evaluated once here
+//          with the same fp32 rounding); a leaf's successor is always i + 1
+namespace {
+
+uint16_t h_bits(_Float16 h) {
+    uint16_t b;
+    std::memcpy(&b, &h, 2);
+    return b;
+}
+float h_val(uint16_t b) {
+    _Float16 h;
+    std::memcpy(&h, &b, 2);
+    return (float)h;
+}
+// one fp16 ulp toward -inf / +inf (finite inputs)
+uint16_t h_prev(uint16_t b) { return (b & 0x8000) ? (uint16_t)(b + 1) : (b == 0 ? (uint16_t)0x8001 : (uint16_t)(b - 1)); }
+uint16_t h_next(uint16_t b) { return (b & 0x8000) ? (b == 0x8000 ? (uint16_t)0x0001 : (uint16_t)(b - 1)) : (uint16_t)(b + 1); }
+bool h_subnormal(uint16_t b) { return (b & 0x7C00) == 0 && (b & 0x03FF) != 0; }
+// largest fp16 <= x that is zero or normal (a subnormal could be flushed by the hardware)
+uint16_t h_down(float x) {
+    uint16_t b = h_bits((_Float16)x);
+    if (h_val(b) > x) b = h_prev(b);
+    if (h_subnormal(b)) b = (b & 0x8000) ? (uint16_t)0x8400 : (uint16_t)0x0000;
+    return b;
+}
+uint16_t h_up(float x) {
+    uint16_t b = h_bits((_Float16)x);
+    if (h_val(b) < x) b = h_next(b);
+    if (h_subnormal(b)) b = (b & 0x8000) ? (uint16_t)0x8000 : (uint16_t)0x0400;
+    return b;
+}
+
+}  // namespace
+
+bool rtw_compact_nodes(const std::vector<rtw_node>& nodes, std::vector<rtw_cnode>& out) {
+    out.resize(nodes.size());
+    for (size_t i = 0; i < nodes.size(); i++) {
+        const rtw_node& n = nodes[i];
+        rtw_cnode& c = out[i];
+        uint32_t w;
+        std::memcpy(&w, &n.a[3], 4);
+        if (w & RTW_LEAF_BIT) {
+            const float rr = n.b[0] * n.b[0];
+            uint32_t rb;
+            std::memcpy(&rb, &rr, 4);
+            if (!(rr >= 0) || !std::isfinite(rr) || (rb & RTW_LEAF_BIT)) return false;
+            std::memcpy(&c.v[0], &n.a[0], 12);
+            c.v[3] = rb | RTW_LEAF_BIT;
+            continue;
+        }
+        uint16_t h[6];
+        for (int k = 0; k < 3; k++) {
+            if (!(std::fabs(n.a[k]) <= 60000.0f) || !(std::fabs(n.b[k]) <= 60000.0f)) return false;
+            h[k] = h_down(n.a[k]);
+            h[3 + k] = h_up(n.b[k]);
+        }
+        c.v[0] = (uint32_t)h[0] | ((uint32_t)h[1] << 16);
+        c.v[1] = (uint32_t)h[2] | ((uint32_t)h[3] << 16);
+        c.v[2] = (uint32_t)h[4] | ((uint32_t)h[5] << 16);
+        c.v[3] = w;
+    }
+    return true;
+}

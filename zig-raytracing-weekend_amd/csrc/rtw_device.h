@@ -484,27 +484,13 @@ __device__ __forceinline__ void load_node(const float4* __restrict__ nodes, uint
 
 // Leaf: Sphere.hit (objects.zig:116-136) on the open interval (0.001, closest),
 // no box test (bvh.zig:123-125).  Updates closest/hit.
-template <uint32_t FEAT>
-__device__ __forceinline__ void leaf_test(const rtw_launch& L, const Ray& r, const RayTrav& rt, float4 A, float4 B,
-                                          uint32_t i, float& closest, int& hit, Counters& cnt, uint64_t mkey = 0) {
-    cnt.leaves++;
-    if constexpr ((FEAT & RTW_F_GEOM) != 0) {
-        const uint32_t kind = RTW_LEAF_KIND(fbits(B.w));
-        if (kind != RTW_OBJ_SPHERE) {
-            object_leaf<FEAT>(L, r, kind, fbits(B.z), i, closest, hit, mkey);
-            return;
-        }
-    }
-    f3 center = mk(A.x, A.y, A.z);
-    if constexpr ((FEAT & RTW_F_MOVING) != 0) {
-        if (fbits(B.w)) {  // Sphere.getCenter (objects.zig:94-98)
-            const float4 cv = L.cvec[fbits(B.z)];
-            center = center + splat(r.time) * mk(cv.x, cv.y, cv.z);
-        }
-    }
+// Sphere.hit (objects.zig:116-136) of a sphere at `center` with rr = radius * radius
+// (the reference's product, evaluated by the caller or on the host) on (0.001, closest).
+__device__ __forceinline__ void sphere_leaf(const rtw_launch& L, const Ray& r, const RayTrav& rt, f3 center, float rr,
+                                            uint32_t i, float& closest, int& hit) {
     const f3 oc = r.o - center;
     const float half_b = dot(oc, r.d);
-    const float c = length_squared(oc) - B.x * B.x;
+    const float c = length_squared(oc) - rr;
     const float disc = half_b * half_b - rt.a * c;
     bool exact = disc >= 0;
 #if !defined(RTW_ABLATE_MATH)
@@ -540,6 +526,27 @@ __device__ __forceinline__ void leaf_test(const rtw_launch& L, const Ray& r, con
             hit = (int)i;
         }
     }
+}
+
+template <uint32_t FEAT>
+__device__ __forceinline__ void leaf_test(const rtw_launch& L, const Ray& r, const RayTrav& rt, float4 A, float4 B,
+                                          uint32_t i, float& closest, int& hit, Counters& cnt, uint64_t mkey = 0) {
+    cnt.leaves++;
+    if constexpr ((FEAT & RTW_F_GEOM) != 0) {
+        const uint32_t kind = RTW_LEAF_KIND(fbits(B.w));
+        if (kind != RTW_OBJ_SPHERE) {
+            object_leaf<FEAT>(L, r, kind, fbits(B.z), i, closest, hit, mkey);
+            return;
+        }
+    }
+    f3 center = mk(A.x, A.y, A.z);
+    if constexpr ((FEAT & RTW_F_MOVING) != 0) {
+        if (fbits(B.w)) {  // Sphere.getCenter (objects.zig:94-98)
+            const float4 cv = L.cvec[fbits(B.z)];
+            center = center + splat(r.time) * mk(cv.x, cv.y, cv.z);
+        }
+    }
+    sphere_leaf(L, r, rt, center, B.x * B.x, i, closest, hit);
 }
 
 // Inner node: Aabb.hit (aabb.zig:82-114) with [0.001, closest]; returns the next
@@ -610,11 +617,57 @@ __device__ __forceinline__ int hit_with_order(int hit, uint32_t oct) {
     return hit < 0 ? hit : (int)((uint32_t)hit | (oct << RTW_HIT_NODE_BITS));
 }
 
+// The walk over the compact 16-B nodes (rtw_bvh.hip rtw_compact_nodes; static
+// sphere SAH trees, FMA slab test): one load per step.  Inner boxes are fp16,
+// rounded outward, consumed by v_fma_mix_f32 (exact f16->f32, one rounding:
+// the same t = fma(P, inv, -o*inv) as box_next's fast test on a superset box);
+// leaves carry center and radius^2.  Same visits-superset argument: same hit.
+__device__ __forceinline__ float h_lo(uint32_t w) { return (float)__builtin_bit_cast(_Float16, (unsigned short)(w & 0xFFFFu)); }
+__device__ __forceinline__ float h_hi(uint32_t w) { return (float)__builtin_bit_cast(_Float16, (unsigned short)(w >> 16)); }
+
+__device__ __forceinline__ int traverse_compact(const rtw_launch& L, const Ray& r, float& t_out, Counters& cnt) {
+    const uint32_t oct = order_of(L, r);
+    const uint4* __restrict__ cn = L.cnodes + (size_t)oct * L.n_nodes;
+    const RayTrav rt = ray_trav(r, true);
+    float closest = kInf;
+    int hit = -1;
+    uint32_t i = 0;
+    const uint32_t n = L.n_nodes;
+    while (i < n) {
+        const uint4 c = cn[i];
+        asm volatile("" ::"v"(c.x), "v"(c.y), "v"(c.z), "v"(c.w));
+        if (c.w & RTW_LEAF_BIT) {
+            cnt.leaves++;
+            sphere_leaf(L, r, rt, mk(__uint_as_float(c.x), __uint_as_float(c.y), __uint_as_float(c.z)),
+                        __uint_as_float(c.w & ~RTW_LEAF_BIT), i, closest, hit);
+            i++;
+        } else {
+            cnt.nodes++;
+            const float t0x = __builtin_fmaf(h_lo(c.x), rt.inv.x, rt.oinv.x);
+            const float t1x = __builtin_fmaf(h_hi(c.y), rt.inv.x, rt.oinv.x);
+            const float t0y = __builtin_fmaf(h_hi(c.x), rt.inv.y, rt.oinv.y);
+            const float t1y = __builtin_fmaf(h_lo(c.z), rt.inv.y, rt.oinv.y);
+            const float t0z = __builtin_fmaf(h_lo(c.y), rt.inv.z, rt.oinv.z);
+            const float t1z = __builtin_fmaf(h_hi(c.z), rt.inv.z, rt.oinv.z);
+            const float lo = __builtin_fmaxf(__builtin_fmaxf(kTmin, __builtin_fminf(t0x, t1x)),
+                                             __builtin_fmaxf(__builtin_fminf(t0y, t1y), __builtin_fminf(t0z, t1z)));
+            const float hi = __builtin_fminf(__builtin_fminf(closest, __builtin_fmaxf(t0x, t1x)),
+                                             __builtin_fminf(__builtin_fmaxf(t0y, t1y), __builtin_fmaxf(t0z, t1z)));
+            i = (hi <= lo) ? c.w : i + 1;
+        }
+    }
+    t_out = closest;
+    return hit_with_order(hit, oct);
+}
+
 // mkey: the path's RNG state (keys ConstantMedium draws; unused without media).
 // `nodes` is the base of the node arrays (the octant copy is picked here).
 template <uint32_t FEAT>
 __device__ __forceinline__ int traverse(const float4* __restrict__ nodes, const rtw_launch& L, const Ray& r,
                                         float& t_out, Counters& cnt, uint64_t mkey = 0) {
+    if constexpr ((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING)) == 0) {
+        if (L.cnodes && L.fast_box) return traverse_compact(L, r, t_out, cnt);
+    }
     const uint32_t oct = order_of(L, r);
     nodes = order_base(nodes, L, oct);
     const RayTrav rt = ray_trav(r, L.fast_box != 0);

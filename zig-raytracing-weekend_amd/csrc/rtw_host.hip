@@ -184,6 +184,14 @@ int rtw_scene_create(const rtw_scene_desc* d, int device, rtw_ctx** out) {
         return fail(RTW_E_INVALID, "scenes with instances are limited to 2^24 BVH nodes");
     }
     const std::vector<float>& cvec = geom.cvec;
+    // compact 16-B walk for static sphere SAH trees (rtw_compact_nodes); RTW_COMPACT=0 disables
+    std::vector<rtw_cnode> cnodes;
+    {
+        bool want = d->bvh_mode == RTW_BVH_SAH && !objects && ctx->box_pad > 0;
+        for (uint32_t i = 0; want && i < d->n_spheres; i++) want = !d->spheres[i].is_moving;
+        if (const char* c = std::getenv("RTW_COMPACT")) want = want && std::atoi(c) != 0;
+        if (want && !rtw_compact_nodes(ctx->nodes_host, cnodes)) cnodes.clear();
+    }
 
     // Blob layout (each section 256-B aligned): nodes | cvec | spheres | quads | members | instances | media |
     // materials | textures | images-info | perlin | image bytes
@@ -191,6 +199,7 @@ int rtw_scene_create(const rtw_scene_desc* d, int device, rtw_ctx** out) {
     const size_t n_nodes = ctx->nodes_host.size() / orders;  // per ordering
     size_t off = 0;
     const size_t o_nodes = off; off = align(off + ctx->nodes_host.size() * sizeof(rtw_node));
+    const size_t o_cnod = off; off = align(off + cnodes.size() * sizeof(rtw_cnode));
     const size_t o_cvec = off; off = align(off + cvec.size() * sizeof(float) + 16);
     const size_t o_sph = off; off = align(off + geom.spheres.size() * sizeof(rtw_dev_sphere) + 16);
     const size_t o_quad = off; off = align(off + geom.quads.size() * sizeof(rtw_dev_quad) + 16);
@@ -218,6 +227,7 @@ int rtw_scene_create(const rtw_scene_desc* d, int device, rtw_ctx** out) {
     auto put = [&](size_t o, const void* src, size_t nb) {
         if (nb) std::memcpy(blob.data() + o, src, nb);
     };
+    put(o_cnod, cnodes.data(), cnodes.size() * sizeof(rtw_cnode));
     put(o_cvec, cvec.data(), cvec.size() * sizeof(float));
     put(o_sph, geom.spheres.data(), geom.spheres.size() * sizeof(rtw_dev_sphere));
     put(o_quad, geom.quads.data(), geom.quads.size() * sizeof(rtw_dev_quad));
@@ -284,6 +294,7 @@ int rtw_scene_create(const rtw_scene_desc* d, int device, rtw_ctx** out) {
     uint8_t* dev = static_cast<uint8_t*>(ctx->d_blob);
     rtw_launch& L = ctx->base;
     L.nodes = reinterpret_cast<const float4*>(dev + o_nodes);
+    L.cnodes = cnodes.empty() ? nullptr : reinterpret_cast<const uint4*>(dev + o_cnod);
     L.cvec = reinterpret_cast<const float4*>(dev + o_cvec);
     L.sph = reinterpret_cast<const rtw_dev_sphere*>(dev + o_sph);
     L.quads = reinterpret_cast<const rtw_dev_quad*>(dev + o_quad);

@@ -16,6 +16,7 @@ struct rtw_scene_desc;
 struct rtw_launch {
     // scene (device pointers)
     const float4* nodes;
+    const uint4* cnodes;         // compact 16-B copy of `nodes` (static sphere SAH trees) or null
     const float4* cvec;          // per-sphere center_vec (moving spheres)
     const rtw_dev_sphere* sph;   // every sphere (instance members)
     const rtw_dev_quad* quads;
@@ -146,6 +147,13 @@ struct rtw_geometry {
 // inner box by extent * 2^-19 so the FMA slab test (box_next) stays conservative.
 // SAH trees: `orders` (1 or 8) pre-order arrays, one per ray-direction octant when 8
 // (concatenated; node indices and skip links are relative to each array).
+// 16-B node of the compact walk (rtw_bvh.hip rtw_compact_nodes)
+struct rtw_cnode {
+    uint32_t v[4];
+};
+// false: the tree cannot be encoded (coordinates beyond fp16 range, non-finite radius)
+bool rtw_compact_nodes(const std::vector<rtw_node>& nodes, std::vector<rtw_cnode>& out);
+
 int rtw_build_bvh(const rtw_scene_desc& desc, std::vector<rtw_node>& nodes, rtw_geometry& geom,
                   uint32_t* depth, uint32_t* axis_draws, float* box_pad = nullptr, float* extent = nullptr,
                   uint32_t orders = 1);
