@@ -625,9 +625,11 @@ __device__ __forceinline__ int hit_with_order(int hit, uint32_t oct) {
 __device__ __forceinline__ float h_lo(uint32_t w) { return (float)__builtin_bit_cast(_Float16, (unsigned short)(w & 0xFFFFu)); }
 __device__ __forceinline__ float h_hi(uint32_t w) { return (float)__builtin_bit_cast(_Float16, (unsigned short)(w >> 16)); }
 
-__device__ __forceinline__ int traverse_compact(const rtw_launch& L, const Ray& r, float& t_out, Counters& cnt) {
+// `base`: L.cnodes, or their copy in LDS
+__device__ __forceinline__ int traverse_compact(const rtw_launch& L, const uint4* base, const Ray& r, float& t_out,
+                                                Counters& cnt) {
     const uint32_t oct = order_of(L, r);
-    const uint4* __restrict__ cn = L.cnodes + (size_t)oct * L.n_nodes;
+    const uint4* __restrict__ cn = base + (size_t)oct * L.n_nodes;
     const RayTrav rt = ray_trav(r, true);
     float closest = kInf;
     int hit = -1;
@@ -666,7 +668,7 @@ template <uint32_t FEAT>
 __device__ __forceinline__ int traverse(const float4* __restrict__ nodes, const rtw_launch& L, const Ray& r,
                                         float& t_out, Counters& cnt, uint64_t mkey = 0) {
     if constexpr ((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING)) == 0) {
-        if (L.cnodes && L.fast_box) return traverse_compact(L, r, t_out, cnt);
+        if (L.cnodes && L.fast_box) return traverse_compact(L, L.cnodes, r, t_out, cnt);
     }
     const uint32_t oct = order_of(L, r);
     nodes = order_base(nodes, L, oct);

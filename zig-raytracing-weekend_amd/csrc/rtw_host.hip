@@ -356,6 +356,9 @@ int rtw_scene_create(const rtw_scene_desc* d, int device, rtw_ctx** out) {
     // wavefront trace: node array staged in LDS when one ordering fits (object scenes,
     // reference trees; +2 % on Cornell); the 8 octant copies of SAH sphere trees do not
     L.wf_lds = 1;
+    // small static sphere SAH trees: the compact nodes of all 8 orders in LDS (C2: +1 %)
+    L.wf_clds = 1;
+    if (const char* cl = std::getenv("RTW_WF_CLDS")) L.wf_clds = (uint32_t)std::atoi(cl);
     if (const char* wl = std::getenv("RTW_WF_LDS")) L.wf_lds = (uint32_t)std::atoi(wl);
     // SAH trees: FMA slab test on the padded boxes + leaf postponement (both only
     // enlarge the set of visited nodes; reference trees keep the exact aabb.zig walk)

@@ -65,6 +65,7 @@ struct rtw_launch {
     uint32_t refill_min;         // wavefront trace: refill idle lanes once >= refill_min are idle (0 = off)
     uint32_t n_orders;           // 1, or 8 octant-ordered copies of the node array (SAH sphere scenes)
     uint32_t wf_lds;             // wavefront trace: stage the node array(s) in LDS when they fit
+    uint32_t wf_clds;            // wavefront trace: stage the compact nodes (all orders) in LDS when they fit
 };
 
 #define RTW_TILE_W 16

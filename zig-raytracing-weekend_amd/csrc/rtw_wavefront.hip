@@ -39,8 +39,8 @@ __device__ __forceinline__ bool wf_pixel(const rtw_launch& L, const rtw_wf& W, u
     return true;
 }
 
-__device__ __forceinline__ uint32_t wf_wave() { return blockIdx.x * 4u + (threadIdx.x >> 6); }
-__device__ __forceinline__ uint32_t wf_nwaves() { return gridDim.x * 4u; }
+__device__ __forceinline__ uint32_t wf_wave() { return blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); }
+__device__ __forceinline__ uint32_t wf_nwaves() { return gridDim.x * (blockDim.x >> 6); }
 
 // The slots of iteration `it` handed to this wave, 64 at a time:
 //   for (WfIter e(W, it); e.more(); e.next()) { uint32_t slot; if (e.get(W, slot)) ... }
@@ -286,6 +286,35 @@ __global__ __launch_bounds__(256) void wf_trace(rtw_launch L, rtw_wf W, uint32_t
     flush_counters(L, cnt, 0);
 }
 
+// trace over the compact nodes staged in LDS (all octant copies of a small tree,
+// e.g. BASELINE config 2: 8 x 969 x 16 B = 124 KB): 1024-thread blocks share one
+// copy (one block per CU), ds_read_b128 instead of vector-memory gathers
+template <uint32_t FEAT>
+__global__ __launch_bounds__(1024) void wf_trace_clds(rtw_launch L, rtw_wf W, uint32_t it) {
+    static_assert((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING)) == 0, "static sphere scenes");
+    if (blockIdx.x == 0 && threadIdx.x < RTW_WF_STRIPES) W.len[(it + 1u) & 1u][threadIdx.x * RTW_WF_LEN_STRIDE] = 0;
+    extern __shared__ uint4 wf_clds[];
+    const uint32_t n4 = L.n_nodes * L.n_orders;
+    for (uint32_t k = threadIdx.x; k < n4; k += blockDim.x) wf_clds[k] = L.cnodes[k];
+    __syncthreads();
+    const rtw_wf_set& S = W.set[it & 1u];
+    Counters cnt;
+    for (WfIter e(W, it); e.more(); e.next()) {
+        uint32_t slot;
+        if (e.get(W, slot)) {
+            uint32_t depth;
+            const Ray r = wf_load_ray(S, slot, depth);
+            if (depth) {
+                float t;
+                const int h = traverse_compact(L, wf_clds, r, t, cnt);
+                W.hit[slot] = make_float2(t, __int_as_float(h));
+                cnt.rays++;
+            }
+        }
+    }
+    flush_counters(L, cnt, 0);
+}
+
 // shade: emission / background and Material.scatter; a surviving path's state
 // moves to its slot in the other set; an ending path stores its radiance by id
 template <uint32_t FEAT>
@@ -418,12 +447,13 @@ __global__ __launch_bounds__(256) void wf_reduce(rtw_launch L, rtw_wf W) {
 
 // resident blocks of `kernel`, rounded down to whole stripes of waves
 template <typename K>
-uint32_t wf_grid(K kernel, int n_cu, size_t lds = 0) {
+uint32_t wf_grid(K kernel, int n_cu, size_t lds = 0, uint32_t threads = 256) {
     int b = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kernel, 256, lds) != hipSuccess || b < 1) b = 1;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kernel, (int)threads, lds) != hipSuccess || b < 1) b = 1;
     uint32_t g = (uint32_t)(b * n_cu);
-    g -= g % (RTW_WF_STRIPES / 4);
-    return g ? g : RTW_WF_STRIPES / 4;
+    const uint32_t per = RTW_WF_STRIPES / (threads / 64);  // blocks per whole set of stripes
+    g -= g % per;
+    return g ? g : per;
 }
 
 template <uint32_t FEAT>
@@ -436,6 +466,7 @@ struct WfGrids {
 
 // largest LDS stage of the wavefront trace (bytes); larger trees read L1/L2
 #define RTW_WF_LDS_MAX (64u * 1024u)
+#define RTW_WF_CLDS_MAX (150u * 1024u)  // compact-node LDS stage (one 1024-thread block per CU)
 
 template <uint32_t FEAT>
 uint32_t wf_lds_grid(int n_cu, size_t lds) {
@@ -462,11 +493,32 @@ void wf_run(const rtw_launch& L, const rtw_wf& W, hipStream_t st, int n_cu, rtw_
     const size_t lds = (L.wf_lds && !L.refill_min && !L.postpone && lds_need <= RTW_WF_LDS_MAX)
                            ? (lds_need + 511u) / 512u * 512u : 0;
     const uint32_t lds_grid = lds ? wf_lds_grid<FEAT>(n_cu, lds) : 0;
+    // compact nodes of every octant copy in LDS (small static sphere trees)
+    const size_t clds = (L.cnodes && L.fast_box && L.wf_clds && !L.refill_min && !L.postpone)
+                            ? (size_t)L.n_nodes * L.n_orders * 16u : 0;
+    static uint32_t clds_grid_cache[2] = {0, 0};
+    uint32_t clds_grid = 0;
+    if constexpr ((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING)) == 0) {
+        if (clds && clds <= RTW_WF_CLDS_MAX) {
+            if (!clds_grid_cache[0] || clds_grid_cache[1] != clds) {
+                clds_grid_cache[0] = wf_grid(wf_trace_clds<FEAT>, n_cu, clds, 1024);
+                clds_grid_cache[1] = (uint32_t)clds;
+            }
+            clds_grid = clds_grid_cache[0];
+        }
+    }
     const char* op = std::getenv("RTW_TRACE_OCC_PAD");
     const size_t occ_pad = op ? (size_t)std::atoi(op) : 0;
     const uint32_t pad_grid = occ_pad ? wf_grid(wf_trace<FEAT, false>, n_cu, occ_pad) : 0;
     for (uint32_t it = 0; it < iters; it++) {
         RTW_TIME_BEGIN(T, RTW_K_TRACE)
+        if constexpr ((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING)) == 0) {
+            if (clds_grid) {
+                hipLaunchKernelGGL(wf_trace_clds<FEAT>, dim3(clds_grid), dim3(1024), clds, st, L, W, it);
+                RTW_TIME_END(T)
+                goto shade_step;
+            }
+        }
         if (lds)
             hipLaunchKernelGGL((wf_trace<FEAT, true>), dim3(lds_grid), dim3(256), lds, st, L, W, it);
         else if (occ_pad)  // DIAGNOSTIC: occupancy sweep (dynamic LDS limits resident blocks)
@@ -474,6 +526,7 @@ void wf_run(const rtw_launch& L, const rtw_wf& W, hipStream_t st, int n_cu, rtw_
         else
             hipLaunchKernelGGL((wf_trace<FEAT, false>), dim3(g.trace), dim3(256), 0, st, L, W, it);
         RTW_TIME_END(T)
+    shade_step:
         RTW_TIME_BEGIN(T, RTW_K_SHADE)
         hipLaunchKernelGGL(wf_shade<FEAT>, dim3(g.shade), dim3(256), 0, st, L, W, it);
         RTW_TIME_END(T)
