@@ -148,11 +148,13 @@ def main():
     dom = max(kms, key=lambda n: kms[n])                        # dominant kernel (device time)
     # algorithmic bytes (reference topology) of the rays each kernel kind traces
     b_ray = NODE_BYTES * (nodes + leaves) / max(1, rays)
+    # (SURVEY §8d prices traversal; a shading-dominated config -- Perlin/image textures, c5 -- has no
+    # algorithmic-byte model here: achieved/frac are null rather than a misleading 0)
     dom_bytes_step = {"trace": b_ray * (rays - cref["tail_rays"]), "tail": b_ray * cref["tail_rays"],
-                      "mega": alg_bytes}.get(dom, 0.0)
+                      "mega": alg_bytes}.get(dom)
     dom_launch_s = kms[dom] / max(1, kcalls[dom]) / 1e3
-    dom_bytes_launch = dom_bytes_step * args.steps / max(1, kcalls[dom])
-    achieved = dom_bytes_launch / dom_launch_s / 1e9 if dom_launch_s > 0 else 0.0
+    dom_bytes_launch = dom_bytes_step * args.steps / max(1, kcalls[dom]) if dom_bytes_step is not None else None
+    achieved = dom_bytes_launch / dom_launch_s / 1e9 if (dom_bytes_launch is not None and dom_launch_s > 0) else None
     path_achieved = alg_bytes / render_s / 1e9
     traffic, traffic_src = pmc_traffic(args, {"trace": "wf_trace", "tail": "wf_tail", "mega": "render_"}.get(dom, dom))
 
@@ -179,13 +181,15 @@ def main():
                        "spp": spp, "max_depth": cam.max_depth, "objects": len(objs), "bvh_nodes": stats["n_nodes"],
                        "bvh_depth": stats["depth"], "parallelism": f"row-interleaved tiles x{world_size}"
                        + (" + RCCL gather" if distributed else ""), "rows_per_block": ROWS_PER_BLOCK},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 2) if achieved is not None else None,
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved is not None else None,
+                         "traffic": traffic,
                          "traffic_source": traffic_src,
                          "kernel": {"trace": "wf_trace", "tail": "wf_tail", "mega": "render_persistent_v1"}.get(dom, dom),
                          "avg_launch_ms": round(dom_launch_s * 1e3, 4),
                          "launches_per_step": kcalls[dom] / args.steps,
-                         "alg_bytes_per_launch": round(dom_bytes_launch),
+                         "alg_bytes_per_launch": round(dom_bytes_launch) if dom_bytes_launch is not None else None,
                          "path": {"achieved": round(path_achieved, 2), "frac": round(path_achieved / HBM_PEAK_GBS, 4),
                                   "render_ms": round(render_s * 1e3, 3), "alg_bytes_per_step": alg_bytes},
                          "kernel_ms_per_step": {n: round(v / args.steps, 3) for n, v in kms.items() if kcalls[n]},

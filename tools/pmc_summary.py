@@ -4,8 +4,14 @@ Counters (MI355X_MICROARCH.md § HBM): FETCH_SIZE / WRITE_SIZE are KiB from the
 L2's memory-side request counters (Infinity-Cache hits included).  gfx950
 correction: FETCH_SIZE reports 1/2 of the bytes of wide coalesced reads, so
 read bytes = 2 x FETCH_SIZE x 1024; WRITE_SIZE is exact for 16-B/lane stores.
-The untimed renders of bench.py (2 counted passes, no warmup) are dropped.
-Writes <dir>/pmc_traffic.json: {kernel: {launches, fetch_bytes, write_bytes, traffic_bytes}} (means per launch).
+
+The profiled command is `bench.py --steps 1 --warmup 0`: two counted passes
+precede the timed step.  Kernels are grouped by kind (wf_gen / wf_trace* /
+wf_shade / wf_tail / wf_reduce: variants of a kind share the group) and the
+LAST n launches of each kind are kept, n = that kind's launches per step in the
+bench JSON line of the same run -- exactly the timed step's launches.
+Writes <dir>/pmc_traffic.json: {kind: {launches, fetch_bytes, write_bytes,
+traffic_bytes, kernels}} (means per launch over the timed step).
 """
 import csv
 import glob
@@ -14,12 +20,21 @@ import os
 import sys
 from collections import defaultdict
 
+KINDS = ("wf_gen", "wf_trace", "wf_shade", "wf_tail", "wf_reduce")
+
+
+def kind_of(name):
+    short = name.replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0]
+    for k in KINDS:
+        if short.startswith(k):
+            return k, short
+    return None, short
+
 
 def load(dirname, counter):
-    files = glob.glob(os.path.join(dirname, counter, "**", "*counter_collection.csv"), recursive=True)
     per = defaultdict(float)
     names = {}
-    for f in files:
+    for f in glob.glob(os.path.join(dirname, counter, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
             if r.get("Counter_Name") != counter:
                 continue
@@ -29,29 +44,38 @@ def load(dirname, counter):
     return per, names
 
 
+def bench_launches(dirname, counter):
+    for line in open(os.path.join(dirname, f"{counter}.log"), errors="replace"):
+        if line.startswith("{"):
+            try:
+                return json.loads(line)["roofline"]["launches"]
+            except (ValueError, KeyError):
+                pass
+    return {}
+
+
 def main():
     d = sys.argv[1]
-    skip_renders = int(sys.argv[2]) if len(sys.argv) > 2 else 2
-    fetch, names = load(d, "FETCH_SIZE")
-    write, names_w = load(d, "WRITE_SIZE")
     out = {}
-    for per, key, scale in ((fetch, "fetch_bytes", 2 * 1024.0), (write, "write_bytes", 1024.0)):
-        nm = names if per is fetch else names_w
+    for counter, key, scale in (("FETCH_SIZE", "fetch_bytes", 2 * 1024.0), ("WRITE_SIZE", "write_bytes", 1024.0)):
+        per, names = load(d, counter)
+        launches = bench_launches(d, counter)
         byk = defaultdict(list)
         for disp in sorted(per):
-            byk[nm[disp]].append(per[disp] * scale)
+            k, short = kind_of(names[disp])
+            if k:
+                byk[k].append((per[disp] * scale, short))
         for k, v in byk.items():
-            short = k.replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0]
-            # bench: renders = 2 counted + timed steps (steps=1, warmup=0); keep the last 1/(skip+1)
-            keep = v[len(v) * skip_renders // (skip_renders + 1):] if len(v) % (skip_renders + 1) == 0 else v
-            e = out.setdefault(short, {"launches": len(keep)})
-            e[key] = sum(keep) / max(1, len(keep))
+            n = launches.get(k[3:], 0) or len(v)
+            keep = v[-n:]
+            e = out.setdefault(k, {"launches": len(keep), "kernels": sorted({s for _, s in keep})})
+            e[key] = sum(b for b, _ in keep) / max(1, len(keep))
     for k, e in out.items():
         e["traffic_bytes"] = e.get("fetch_bytes", 0) + e.get("write_bytes", 0)
     json.dump(out, open(os.path.join(d, "pmc_traffic.json"), "w"), indent=1, sort_keys=True)
     for k, e in sorted(out.items(), key=lambda kv: -kv[1]["traffic_bytes"]):
-        print(f"{k[:40]:40s} launches {e['launches']:4d}  fetch {e.get('fetch_bytes', 0) / 1e9:9.3f} GB  "
-              f"write {e.get('write_bytes', 0) / 1e9:9.3f} GB per launch")
+        print(f"{k:10s} launches/step {e['launches']:3d}  fetch {e.get('fetch_bytes', 0) / 1e9:8.3f} GB  "
+              f"write {e.get('write_bytes', 0) / 1e9:8.3f} GB per launch  ({', '.join(e['kernels'])})")
 
 
 if __name__ == "__main__":
