@@ -664,9 +664,12 @@ uint16_t h_up(float x) {
 
 }  // namespace
 
-bool rtw_compact_nodes(const std::vector<rtw_node>& nodes, std::vector<rtw_cnode>& out) {
+bool rtw_compact_nodes(const std::vector<rtw_node>& nodes, uint32_t orders, std::vector<rtw_cnode>& out) {
+    if (orders != 8 || nodes.size() % 8) return false;  // one copy per ray-direction octant
+    const size_t per = nodes.size() / 8;
     out.resize(nodes.size());
     for (size_t i = 0; i < nodes.size(); i++) {
+        const uint32_t oct = (uint32_t)(i / per);  // order_of: bit k set = negative direction on axis k
         const rtw_node& n = nodes[i];
         rtw_cnode& c = out[i];
         uint32_t w;
@@ -680,11 +683,15 @@ bool rtw_compact_nodes(const std::vector<rtw_node>& nodes, std::vector<rtw_cnode
             c.v[3] = rb | RTW_LEAF_BIT;
             continue;
         }
+        // per axis the slab the copy's rays enter first (near) and leave last (far):
+        // min/max for a non-negative direction component, swapped for a negative one
         uint16_t h[6];
         for (int k = 0; k < 3; k++) {
             if (!(std::fabs(n.a[k]) <= 60000.0f) || !(std::fabs(n.b[k]) <= 60000.0f)) return false;
-            h[k] = h_down(n.a[k]);
-            h[3 + k] = h_up(n.b[k]);
+            const uint16_t lo = h_down(n.a[k]), hi = h_up(n.b[k]);
+            const bool neg = (oct >> k) & 1u;
+            h[k] = neg ? hi : lo;
+            h[3 + k] = neg ? lo : hi;
         }
         c.v[0] = (uint32_t)h[0] | ((uint32_t)h[1] << 16);
         c.v[1] = (uint32_t)h[2] | ((uint32_t)h[3] << 16);

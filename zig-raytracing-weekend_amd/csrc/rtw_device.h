@@ -630,7 +630,15 @@ __device__ __forceinline__ int traverse_compact(const rtw_launch& L, const uint4
                                                 Counters& cnt) {
     const uint32_t oct = order_of(L, r);
     const uint4* __restrict__ cn = base + (size_t)oct * L.n_nodes;
-    const RayTrav rt = ray_trav(r, true);
+    // The copy's boxes are stored (near, far) per axis for its octant (rtw_compact_nodes),
+    // so min(t0, t1) = t(near) without a min/max pair: fma(P, inv, c) is monotone in P,
+    // non-decreasing for inv >= 0.  The sign of inv must then follow the octant, which
+    // tests d < 0: a -0.0 component (octant "positive", rcp = -inf) gets +1e30.
+    RayTrav rt = ray_trav(r, true);
+    rt.inv = mk((oct & 1u) ? -__builtin_fabsf(rt.inv.x) : __builtin_fabsf(rt.inv.x),
+                (oct & 2u) ? -__builtin_fabsf(rt.inv.y) : __builtin_fabsf(rt.inv.y),
+                (oct & 4u) ? -__builtin_fabsf(rt.inv.z) : __builtin_fabsf(rt.inv.z));
+    rt.oinv = mk(-(r.o.x * rt.inv.x), -(r.o.y * rt.inv.y), -(r.o.z * rt.inv.z));
     float closest = kInf;
     int hit = -1;
     uint32_t i = 0;
@@ -645,16 +653,14 @@ __device__ __forceinline__ int traverse_compact(const rtw_launch& L, const uint4
             i++;
         } else {
             cnt.nodes++;
-            const float t0x = __builtin_fmaf(h_lo(c.x), rt.inv.x, rt.oinv.x);
-            const float t1x = __builtin_fmaf(h_hi(c.y), rt.inv.x, rt.oinv.x);
-            const float t0y = __builtin_fmaf(h_hi(c.x), rt.inv.y, rt.oinv.y);
-            const float t1y = __builtin_fmaf(h_lo(c.z), rt.inv.y, rt.oinv.y);
-            const float t0z = __builtin_fmaf(h_lo(c.y), rt.inv.z, rt.oinv.z);
-            const float t1z = __builtin_fmaf(h_hi(c.z), rt.inv.z, rt.oinv.z);
-            const float lo = __builtin_fmaxf(__builtin_fmaxf(kTmin, __builtin_fminf(t0x, t1x)),
-                                             __builtin_fmaxf(__builtin_fminf(t0y, t1y), __builtin_fminf(t0z, t1z)));
-            const float hi = __builtin_fminf(__builtin_fminf(closest, __builtin_fmaxf(t0x, t1x)),
-                                             __builtin_fminf(__builtin_fmaxf(t0y, t1y), __builtin_fmaxf(t0z, t1z)));
+            const float tnx = __builtin_fmaf(h_lo(c.x), rt.inv.x, rt.oinv.x);
+            const float tny = __builtin_fmaf(h_hi(c.x), rt.inv.y, rt.oinv.y);
+            const float tnz = __builtin_fmaf(h_lo(c.y), rt.inv.z, rt.oinv.z);
+            const float tfx = __builtin_fmaf(h_hi(c.y), rt.inv.x, rt.oinv.x);
+            const float tfy = __builtin_fmaf(h_lo(c.z), rt.inv.y, rt.oinv.y);
+            const float tfz = __builtin_fmaf(h_hi(c.z), rt.inv.z, rt.oinv.z);
+            const float lo = __builtin_fmaxf(__builtin_fmaxf(kTmin, tnx), __builtin_fmaxf(tny, tnz));
+            const float hi = __builtin_fminf(__builtin_fminf(closest, tfx), __builtin_fminf(tfy, tfz));
             i = (hi <= lo) ? c.w : i + 1;
         }
     }

@@ -190,7 +190,7 @@ int rtw_scene_create(const rtw_scene_desc* d, int device, rtw_ctx** out) {
         bool want = d->bvh_mode == RTW_BVH_SAH && !objects && ctx->box_pad > 0;
         for (uint32_t i = 0; want && i < d->n_spheres; i++) want = !d->spheres[i].is_moving;
         if (const char* c = std::getenv("RTW_COMPACT")) want = want && std::atoi(c) != 0;
-        if (want && !rtw_compact_nodes(ctx->nodes_host, cnodes)) cnodes.clear();
+        if (want && !rtw_compact_nodes(ctx->nodes_host, orders, cnodes)) cnodes.clear();
     }
 
     // Blob layout (each section 256-B aligned): nodes | cvec | spheres | quads | members | instances | media |

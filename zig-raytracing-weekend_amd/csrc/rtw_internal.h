@@ -153,7 +153,7 @@ struct rtw_cnode {
     uint32_t v[4];
 };
 // false: the tree cannot be encoded (coordinates beyond fp16 range, non-finite radius)
-bool rtw_compact_nodes(const std::vector<rtw_node>& nodes, std::vector<rtw_cnode>& out);
+bool rtw_compact_nodes(const std::vector<rtw_node>& nodes, uint32_t orders, std::vector<rtw_cnode>& out);
 
 int rtw_build_bvh(const rtw_scene_desc& desc, std::vector<rtw_node>& nodes, rtw_geometry& geom,
                   uint32_t* depth, uint32_t* axis_draws, float* box_pad = nullptr, float* extent = nullptr,

@@ -498,10 +498,15 @@ void wf_run(const rtw_launch& L, const rtw_wf& W, hipStream_t st, int n_cu, rtw_
                             ? (size_t)L.n_nodes * L.n_orders * 16u : 0;
     static uint32_t clds_grid_cache[2] = {0, 0};
     uint32_t clds_grid = 0;
+    static const uint32_t clds_threads = [] {  // DIAGNOSTIC: RTW_CLDS_THREADS (occupancy of the LDS walk)
+        const char* e = std::getenv("RTW_CLDS_THREADS");
+        const int t = e ? std::atoi(e) : 1024;
+        return (uint32_t)((t == 256 || t == 512) ? t : 1024);
+    }();
     if constexpr ((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING)) == 0) {
         if (clds && clds <= RTW_WF_CLDS_MAX) {
             if (!clds_grid_cache[0] || clds_grid_cache[1] != clds) {
-                clds_grid_cache[0] = wf_grid(wf_trace_clds<FEAT>, n_cu, clds, 1024);
+                clds_grid_cache[0] = wf_grid(wf_trace_clds<FEAT>, n_cu, clds, clds_threads);
                 clds_grid_cache[1] = (uint32_t)clds;
             }
             clds_grid = clds_grid_cache[0];
@@ -514,7 +519,7 @@ void wf_run(const rtw_launch& L, const rtw_wf& W, hipStream_t st, int n_cu, rtw_
         RTW_TIME_BEGIN(T, RTW_K_TRACE)
         if constexpr ((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING)) == 0) {
             if (clds_grid) {
-                hipLaunchKernelGGL(wf_trace_clds<FEAT>, dim3(clds_grid), dim3(1024), clds, st, L, W, it);
+                hipLaunchKernelGGL(wf_trace_clds<FEAT>, dim3(clds_grid), dim3(clds_threads), clds, st, L, W, it);
                 RTW_TIME_END(T)
                 goto shade_step;
             }
