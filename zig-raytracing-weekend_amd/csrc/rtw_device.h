@@ -503,14 +503,17 @@ __device__ __forceinline__ void sphere_leaf(const rtw_launch& L, const Ray& r, c
     // Written as ONE predicate (no nested branch): a nested-branch form was
     // miscompiled by hipcc 7.2 (numerator left undefined on the guard-false edge).
     {
+        // The exact roots satisfy r1 <= r2 (a > 0), so one of them lies in (tmin, closest)
+        // only if r2 > tmin and r1 < closest: with |r - q| <= e, only if q2 + e > tmin and
+        // q1 - e < closest (a necessary condition; non-short-circuit & and |, no branches).
         const float sa = __builtin_amdgcn_sqrtf(disc);
         const float e = (__builtin_fabsf(half_b) + sa) * rt.rcp_a * 3.8146973e-06f;
         const float q1 = (-half_b - sa) * rt.rcp_a;
         const float q2 = (-half_b + sa) * rt.rcp_a;
-        const bool guard = L.fast_reject && rt.rcp_a != 0.0f && disc > 1e-30f && disc < 1e30f &&
-                           __builtin_fabsf(half_b) < 1e15f;
-        const bool plausible = (q1 + e > kTmin && q1 - e < closest) || (q2 + e > kTmin && q2 - e < closest);
-        exact = exact && (plausible || !guard);
+        const bool guard = L.fast_reject & (rt.rcp_a != 0.0f) & (disc > 1e-30f) & (disc < 1e30f) &
+                           (__builtin_fabsf(half_b) < 1e15f);
+        const bool plausible = (q2 + e > kTmin) & (q1 - e < closest);
+        exact = exact & (plausible | !guard);
     }
 #endif
     if (exact) {
@@ -626,6 +629,7 @@ __device__ __forceinline__ float h_lo(uint32_t w) { return (float)__builtin_bit_
 __device__ __forceinline__ float h_hi(uint32_t w) { return (float)__builtin_bit_cast(_Float16, (unsigned short)(w >> 16)); }
 
 // `base`: L.cnodes, or their copy in LDS
+template <bool COUNT>
 __device__ __forceinline__ int traverse_compact(const rtw_launch& L, const uint4* base, const Ray& r, float& t_out,
                                                 Counters& cnt) {
     const uint32_t oct = order_of(L, r);
@@ -645,14 +649,13 @@ __device__ __forceinline__ int traverse_compact(const rtw_launch& L, const uint4
     const uint32_t n = L.n_nodes;
     while (i < n) {
         const uint4 c = cn[i];
-        asm volatile("" ::"v"(c.x), "v"(c.y), "v"(c.z), "v"(c.w));
         if (c.w & RTW_LEAF_BIT) {
-            cnt.leaves++;
+            if constexpr (COUNT) cnt.leaves++;
             sphere_leaf(L, r, rt, mk(__uint_as_float(c.x), __uint_as_float(c.y), __uint_as_float(c.z)),
                         __uint_as_float(c.w & ~RTW_LEAF_BIT), i, closest, hit);
             i++;
         } else {
-            cnt.nodes++;
+            if constexpr (COUNT) cnt.nodes++;
             const float tnx = __builtin_fmaf(h_lo(c.x), rt.inv.x, rt.oinv.x);
             const float tny = __builtin_fmaf(h_hi(c.x), rt.inv.y, rt.oinv.y);
             const float tnz = __builtin_fmaf(h_lo(c.y), rt.inv.z, rt.oinv.z);
@@ -674,7 +677,10 @@ template <uint32_t FEAT>
 __device__ __forceinline__ int traverse(const float4* __restrict__ nodes, const rtw_launch& L, const Ray& r,
                                         float& t_out, Counters& cnt, uint64_t mkey = 0) {
     if constexpr ((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING)) == 0) {
-        if (L.cnodes && L.fast_box) return traverse_compact(L, L.cnodes, r, t_out, cnt);
+        if (L.cnodes && L.fast_box) {  // per-step counters only in counted passes
+            return L.counters ? traverse_compact<true>(L, L.cnodes, r, t_out, cnt)
+                              : traverse_compact<false>(L, L.cnodes, r, t_out, cnt);
+        }
     }
     const uint32_t oct = order_of(L, r);
     nodes = order_base(nodes, L, oct);

@@ -306,7 +306,8 @@ __global__ __launch_bounds__(1024) void wf_trace_clds(rtw_launch L, rtw_wf W, ui
             const Ray r = wf_load_ray(S, slot, depth);
             if (depth) {
                 float t;
-                const int h = traverse_compact(L, wf_clds, r, t, cnt);
+                const int h = L.counters ? traverse_compact<true>(L, wf_clds, r, t, cnt)
+                                         : traverse_compact<false>(L, wf_clds, r, t, cnt);
                 W.hit[slot] = make_float2(t, __int_as_float(h));
                 cnt.rays++;
             }
