@@ -260,6 +260,35 @@ __device__ f3 texture_value(const rtw_launch& L, uint32_t ti, const HitUV& uv, f
     return ld3(t.even);  // RTW_TEX_SOLID (textures.zig:43-45)
 }
 
+// Correctly rounded fp32 division and square root on operands known to be in range:
+// the exact instruction sequences of the compiler's IEEE expansions with their
+// range scaling and special-value fix-ups left out.  With v_div_scale leaving its
+// operands unscaled (numerator and denominator normal, |exponent difference| < 96,
+// quotient and 1/d normal) and v_div_fixup passing the quotient through, x / d is
+//   y0 = rcp(d); e = fma(-d, y0, 1); y = fma(e, y0, y0)           (rcp_refined)
+//   q0 = x * y; r0 = fma(-d, q0, x); q1 = fma(r0, y, q0);
+//   r1 = fma(-d, q1, x); q = fma(r1, y, q1)                        (div_shared)
+// so several divisions by one d (a ray's |d|^2, a sphere radius, a vector length)
+// share y.  sqrt_refined: for x in [2^-96, 2^128) finite, the compiler's IEEE sqrt
+// is v_sqrt_f32 then a +-1 ulp correction by the signs of fma residuals.
+__device__ __forceinline__ float rcp_refined(float d, float y0) {
+    const float e = __builtin_fmaf(-d, y0, 1.0f);
+    return __builtin_fmaf(e, y0, y0);
+}
+__device__ __forceinline__ float div_shared(float x, float d, float y) {
+    const float q0 = x * y;
+    const float r0 = __builtin_fmaf(-d, q0, x);
+    const float q1 = __builtin_fmaf(r0, y, q0);
+    const float r1 = __builtin_fmaf(-d, q1, x);
+    return __builtin_fmaf(r1, y, q1);
+}
+__device__ __forceinline__ float sqrt_refined(float x, float s /* v_sqrt_f32(x) */) {
+    const float sdn = __uint_as_float(__float_as_uint(s) - 1u), sup = __uint_as_float(__float_as_uint(s) + 1u);
+    const float rdn = __builtin_fmaf(-sdn, s, x), rup = __builtin_fmaf(-sup, s, x);
+    const float r = (rdn <= 0.0f) ? sdn : s;
+    return (rup > 0.0f) ? sup : r;
+}
+
 struct Counters {
     uint32_t rays = 0, nodes = 0, leaves = 0, nans = 0, tail_rays = 0;
 };
@@ -270,6 +299,7 @@ struct RayTrav {
     f3 oinv;     // fast box only: -o * inv
     float a;     // lengthSquared(d) (objects.zig:124)
     float rcp_a; // hardware 1/a estimate for the sphere fast-reject (0 disables it)
+    float ya;    // rcp_refined(a) for div_shared (0: a outside [2^-40, 2^40], IEEE division)
 };
 __device__ __forceinline__ RayTrav ray_trav(const Ray& r, bool fast_box) {
     RayTrav t;
@@ -289,6 +319,7 @@ __device__ __forceinline__ RayTrav ray_trav(const Ray& r, bool fast_box) {
     t.a = length_squared(r.d);
     // fast-reject only where every intermediate below stays normal and finite
     t.rcp_a = (t.a > 1e-30f && t.a < 1e30f) ? __builtin_amdgcn_rcpf(t.a) : 0.0f;
+    t.ya = (t.a >= 0x1p-40f && t.a <= 0x1p40f) ? rcp_refined(t.a, t.rcp_a) : 0.0f;
     return t;
 }
 
@@ -493,6 +524,8 @@ __device__ __forceinline__ void sphere_leaf(const rtw_launch& L, const Ray& r, c
     const float c = length_squared(oc) - rr;
     const float disc = half_b * half_b - rt.a * c;
     bool exact = disc >= 0;
+    bool quick = false;  // the exact roots by sqrt_refined / div_shared (operands in range)
+    float sa = 0.0f;
 #if !defined(RTW_ABLATE_MATH)
     // Exact fast-reject: with hardware sqrt/rcp estimates (<= 1 ulp each) the
     // candidate roots q1, q2 are within (|hb| + sq) / a * 6e-7 of the correctly
@@ -506,7 +539,7 @@ __device__ __forceinline__ void sphere_leaf(const rtw_launch& L, const Ray& r, c
         // The exact roots satisfy r1 <= r2 (a > 0), so one of them lies in (tmin, closest)
         // only if r2 > tmin and r1 < closest: with |r - q| <= e, only if q2 + e > tmin and
         // q1 - e < closest (a necessary condition; non-short-circuit & and |, no branches).
-        const float sa = __builtin_amdgcn_sqrtf(disc);
+        sa = __builtin_amdgcn_sqrtf(disc);
         const float e = (__builtin_fabsf(half_b) + sa) * rt.rcp_a * 3.8146973e-06f;
         const float q1 = (-half_b - sa) * rt.rcp_a;
         const float q2 = (-half_b + sa) * rt.rcp_a;
@@ -514,14 +547,26 @@ __device__ __forceinline__ void sphere_leaf(const rtw_launch& L, const Ray& r, c
                            (__builtin_fabsf(half_b) < 1e15f);
         const bool plausible = (q2 + e > kTmin) & (q1 - e < closest);
         exact = exact & (plausible | !guard);
+        // under the guard |-hb -+ sq| < 2^51 and disc >= 2^-96; with a in [2^-40, 2^40] the
+        // divisions are unscaled except for quotients below 2^-80, which kTmin rejects
+        // either way
+        quick = guard & (rt.ya != 0.0f) & (disc >= 0x1p-96f);
     }
 #endif
     if (exact) {
-        const float sq = __builtin_sqrtf(disc);
-        float root = RTW_DIV(-half_b - sq, rt.a);
+        float sq, root, root2;
+        if (quick) {
+            sq = sqrt_refined(disc, sa);
+            root = div_shared(-half_b - sq, rt.a, rt.ya);
+            root2 = div_shared(-half_b + sq, rt.a, rt.ya);
+        } else {
+            sq = __builtin_sqrtf(disc);
+            root = RTW_DIV(-half_b - sq, rt.a);
+            root2 = RTW_DIV(-half_b + sq, rt.a);
+        }
         bool ok = kTmin < root && root < closest;
         if (!ok) {
-            root = RTW_DIV(-half_b + sq, rt.a);
+            root = root2;
             ok = kTmin < root && root < closest;
         }
         if (ok) {
