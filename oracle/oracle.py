@@ -89,6 +89,7 @@ def lib() -> C.CDLL:
             "oracle_mix64": (u64, [u64]),
             "oracle_rng_floats": (None, [u64, u64, u32, u32, u32, vp]),
             "oracle_rng_u64": (None, [u64, u64, u32, u32, u32, vp]),
+            "oracle_path_floats": (None, [u64, u32, u32, u32, vp]),
             "oracle_aabb_hit": (C.c_int, [vp, vp, vp, C.c_float, C.c_float]),
             "oracle_sphere_uv": (None, [vp, vp]),
             "oracle_pow": (C.c_float, [C.c_float, C.c_float]),
@@ -257,6 +258,13 @@ def gen_perlin(seed: int = 0, table_id: int = 0) -> np.ndarray:
 def rng_floats(seed: int, domain: int, a: int, b: int, n: int) -> np.ndarray:
     out = np.zeros(n, np.float32)
     lib().oracle_rng_floats(seed, domain, a, b, n, _p(out))
+    return out
+
+
+def path_floats(seed: int, pixel: int, sample: int, n: int) -> np.ndarray:
+    """Render-domain draws of path (pixel, sample): rtw_rng.h rtw_path_float."""
+    out = np.zeros(n, np.float32)
+    lib().oracle_path_floats(seed, pixel, sample, n, _p(out))
     return out
 
 

@@ -66,6 +66,23 @@ static inline float rnd(rng_t* r) {
 /* rtweekend.zig:18-20 */
 static inline float rnd_range(rng_t* r, float mn, float mx) { return mn + (mx - mn) * rnd(r); }
 
+/* Render-domain draws (camera, scatter): the same Weyl step, a lowbias32 finalizer
+ * on hi ^ lo, 24-bit float k * 2^-24 (csrc/rtw_rng.h rtw_path_float, DESIGN.md RNG). */
+static inline uint32_t lowbias32(uint32_t x) {
+    x ^= x >> 16;
+    x *= 0x7feb352du;
+    x ^= x >> 15;
+    x *= 0x846ca68bu;
+    x ^= x >> 16;
+    return x;
+}
+static inline float rndp(rng_t* r) {
+    r->s += GOLDEN;
+    uint32_t h = lowbias32((uint32_t)(r->s >> 32) ^ (uint32_t)r->s);
+    return (float)(h >> 8) * 5.9604644775390625e-08f;
+}
+static inline float rndp_range(rng_t* r, float mn, float mx) { return mn + (mx - mn) * rndp(r); }
+
 /* rtweekend.zig:23-27 (biased: returns up to max+1) */
 static inline uint32_t rnd_int_range(rng_t* r, uint32_t mn, uint32_t mx) {
     float mn_f = (float)mn, mx_f = (float)(mx + 1);
@@ -75,6 +92,11 @@ static inline uint32_t rnd_int_range(rng_t* r, uint32_t mn, uint32_t mx) {
 void oracle_rng_floats(uint64_t seed, uint64_t domain, uint32_t a, uint32_t b, uint32_t n, float* out) {
     rng_t r = rng_stream(seed, domain, a, b);
     for (uint32_t i = 0; i < n; i++) out[i] = rnd(&r);
+}
+
+void oracle_path_floats(uint64_t seed, uint32_t a, uint32_t b, uint32_t n, float* out) {
+    rng_t r = rng_stream(seed, 0, a, b);
+    for (uint32_t i = 0; i < n; i++) out[i] = rndp(&r);
 }
 
 void oracle_rng_u64(uint64_t seed, uint64_t domain, uint32_t a, uint32_t b, uint32_t n, uint64_t* out) {
@@ -140,8 +162,8 @@ static inline v3 unit_vector(v3 v) { return vdiv(v, splat(vlength(v))); }
 /* vec3.zig:40-45 */
 static inline v3 random_in_unit_disk(rng_t* r) {
     for (;;) {
-        float x = rnd_range(r, -1, 1);
-        float y = rnd_range(r, -1, 1);
+        float x = rndp_range(r, -1, 1);
+        float y = rndp_range(r, -1, 1);
         v3 p = V(x, y, 0);
         if (length_squared(p) < 1) return p;
     }
@@ -159,7 +181,8 @@ static inline v3 random_range_v(rng_t* r, float mn, float mx) {
 /* vec3.zig:59-64 */
 static inline v3 random_in_unit_sphere(rng_t* r) {
     for (;;) {
-        v3 p = random_range_v(r, -1, 1);
+        float x = rndp_range(r, -1, 1), y = rndp_range(r, -1, 1), z = rndp_range(r, -1, 1);
+        v3 p = V(x, y, z);
         if (length_squared(p) < 1) return p;
     }
 }
@@ -569,7 +592,7 @@ static int scatter(const o_scene_desc* d, const ray3* r_in, const hit_record_t* 
         float sin_theta = sqrtf(1.0f - cos_theta * cos_theta);
         int cannot_refract = refraction_ratio * sin_theta > 1.0f;
         v3 direction;
-        if (cannot_refract || oracle_reflectance(cos_theta, refraction_ratio) > rnd(rng))
+        if (cannot_refract || oracle_reflectance(cos_theta, refraction_ratio) > rndp(rng))
             direction = reflect(unit_direction, rec->normal);
         else
             direction = refract(unit_direction, rec->normal, refraction_ratio);
@@ -1077,8 +1100,8 @@ int oracle_camera_init(const o_camera_params* p, o_camera* c) {       /* camera.
 static ray3 get_ray(const o_camera* c, uint32_t i, uint32_t j, rng_t* rng) {
     v3 p00 = vload(c->pixel00_loc), du = vload(c->pixel_delta_u), dv = vload(c->pixel_delta_v);
     v3 pixel_center = add(add(p00, mul(du, splat((float)i))), mul(dv, splat((float)j)));
-    float px = -0.5f + rnd(rng);
-    float py = -0.5f + rnd(rng);
+    float px = -0.5f + rndp(rng);
+    float py = -0.5f + rndp(rng);
     v3 square = add(mul(splat(px), du), mul(splat(py), dv));
     v3 pixel_sample = add(pixel_center, square);
     v3 origin;
@@ -1092,7 +1115,7 @@ static ray3 get_ray(const o_camera* c, uint32_t i, uint32_t j, rng_t* rng) {
     ray3 r;
     r.origin = origin;
     r.direction = sub(pixel_sample, origin);
-    r.time = rnd(rng);
+    r.time = rndp(rng);
     return r;
 }
 

@@ -147,6 +147,8 @@ typedef struct o_camera {
 uint64_t oracle_mix64(uint64_t z);
 void oracle_rng_floats(uint64_t seed, uint64_t domain, uint32_t a, uint32_t b, uint32_t n, float* out);
 void oracle_rng_u64(uint64_t seed, uint64_t domain, uint32_t a, uint32_t b, uint32_t n, uint64_t* out);
+/* render-domain draws of path (a = pixel, b = sample): rtw_rng.h rtw_path_float */
+void oracle_path_floats(uint64_t seed, uint32_t a, uint32_t b, uint32_t n, float* out);
 
 /* Known-answer hooks */
 int oracle_aabb_hit(const float box[6], const float origin[3], const float dir[3], float tmin, float tmax);

@@ -65,7 +65,7 @@ def test_device_rng_bit_exact(rtw, oracle, book1):
     out = np.zeros(64, np.float32)
     for seed, pix, s in ((0, 0, 0), (1, 959999, 499), (12345, 77, 3)):
         rtw._abi.check(rtw.lib().rtw_debug_rng(world.handle, seed, pix, s, 64, out.ctypes.data), "rtw_debug_rng")
-        assert np.array_equal(out, oracle.rng_floats(seed, 0, pix, s, 64))
+        assert np.array_equal(out, oracle.path_floats(seed, pix, s, 64))
 
 
 def test_per_sample_radiance(rtw, oracle, book1, oracle_book1):

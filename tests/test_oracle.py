@@ -81,6 +81,27 @@ def test_rng_is_counter_based(oracle):
     assert (big > 0).all()
 
 
+def test_path_rng_streams(rtw, oracle):
+    """Render-domain draws: oracle and Python restatements agree; counter-based; uniform
+    24-bit floats; no visible correlation between consecutive draws or neighbouring paths."""
+    s = rtw.rng.Stream(7, 0, 1234, 56)
+    py = np.array([s.path_float() for _ in range(256)], np.float32)
+    assert np.array_equal(py, oracle.path_floats(7, 1234, 56, 256))
+    assert np.array_equal(oracle.path_floats(0, 5, 7, 32), oracle.path_floats(0, 5, 7, 32))
+    assert not np.array_equal(oracle.path_floats(0, 5, 7, 32), oracle.path_floats(0, 5, 8, 32))
+    big = oracle.path_floats(123, 1, 2, 400000).astype(np.float64)
+    assert big.min() >= 0 and big.max() < 1
+    assert np.all(big * 2**24 == np.floor(big * 2**24))          # k * 2^-24
+    assert abs(big.mean() - 0.5) < 0.003
+    hist = np.bincount((big * 64).astype(int), minlength=64)
+    chi2 = ((hist - len(big) / 64) ** 2 / (len(big) / 64)).sum()
+    assert chi2 < 120                                             # 63 dof: p ~ 1e-5
+    assert abs(np.corrcoef(big[:-1], big[1:])[0, 1]) < 0.01
+    nb = np.array([oracle.path_floats(9, p, 0, 1)[0] for p in range(20000)], np.float64)
+    assert abs(np.corrcoef(nb[:-1], nb[1:])[0, 1]) < 0.03
+    assert abs(nb.mean() - 0.5) < 0.01
+
+
 def test_rng_python_host_matches_oracle(rtw, oracle):
     s = rtw.rng.Stream(99, 1, 3, 4)
     py = np.array([s.float() for _ in range(256)], np.float32)

@@ -71,18 +71,18 @@ __device__ __forceinline__ f3 refract(f3 uv, f3 n, float e) {                   
 __device__ __forceinline__ uint32_t fbits(float f) { return __float_as_uint(f); }
 
 // ---- RNG helpers (rtweekend.zig / vec3.zig samplers) ----
-__device__ __forceinline__ float rnd(rtw_rng& r) { return rtw_rng_float(r); }
+__device__ __forceinline__ float rnd(rtw_rng& r) { return rtw_path_float(r); }  // render-domain draw
 __device__ __forceinline__ f3 random_unit_vector(rtw_rng& r) {  // vec3.zig:59-68
 #if defined(RTW_ABLATE_REJECT)
     {   // timing ablation only: one candidate, no rejection loop (wrong distribution)
-        float x = rtw_rng_range(r, -1, 1), y = rtw_rng_range(r, -1, 1), z = rtw_rng_range(r, -1, 1);
+        float x = rtw_path_range(r, -1, 1), y = rtw_path_range(r, -1, 1), z = rtw_path_range(r, -1, 1);
         return unit_vector(mk(x, y, z + 1e-3f));
     }
 #endif
     for (;;) {
-        float x = rtw_rng_range(r, -1, 1);
-        float y = rtw_rng_range(r, -1, 1);
-        float z = rtw_rng_range(r, -1, 1);
+        float x = rtw_path_range(r, -1, 1);
+        float y = rtw_path_range(r, -1, 1);
+        float z = rtw_path_range(r, -1, 1);
         f3 p = mk(x, y, z);
         if (length_squared(p) < 1) return unit_vector(p);
     }
@@ -154,8 +154,8 @@ __device__ __forceinline__ Ray get_ray(const rtw_launch& L, uint32_t i, uint32_t
     } else {
         float dx, dy;
         for (;;) {  // vec3.randomInUnitDisk (vec3.zig:40-45)
-            dx = rtw_rng_range(rng, -1, 1);
-            dy = rtw_rng_range(rng, -1, 1);
+            dx = rtw_path_range(rng, -1, 1);
+            dy = rtw_path_range(rng, -1, 1);
             if (dx * dx + dy * dy + 0.0f * 0.0f < 1) break;
         }
         origin = (ld3(L.center) + ld3(L.disk_u) * splat(dx)) + ld3(L.disk_v) * splat(dy);
@@ -997,7 +997,7 @@ __device__ __forceinline__ void seq_reject(rtw_rng& rng, float (&out)[D]) {
         float w[D];
         float ls;
 #pragma unroll
-        for (int d = 0; d < D; d++) w[d] = rtw_rng_range(rng, -1, 1);
+        for (int d = 0; d < D; d++) w[d] = rtw_path_range(rng, -1, 1);
         if constexpr (D == 3) ls = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
         else ls = w[0] * w[0] + w[1] * w[1];
         if (ls < 1.0f) {

@@ -345,7 +345,7 @@ __global__ void debug_rng_kernel(uint64_t seed, uint32_t pixel, uint32_t sample,
     if (threadIdx.x | blockIdx.x) return;
     rtw_rng r;
     r.s = rtw_mix64(rtw_mix64(seed) ^ (((uint64_t)pixel << 32) | (uint64_t)sample));
-    for (uint32_t k = 0; k < n; k++) out[k] = rtw_rng_float(r);
+    for (uint32_t k = 0; k < n; k++) out[k] = rtw_path_float(r);
 }
 
 // Diagnostic: for every bounce of one sample, brute-force all leaves with the

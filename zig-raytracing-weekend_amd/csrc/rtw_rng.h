@@ -85,6 +85,28 @@ RTW_HD float rtw_rng_float(rtw_rng& r) {
 // rtweekend.zig:18-20
 RTW_HD float rtw_rng_range(rtw_rng& r, float mn, float mx) { return mn + (mx - mn) * rtw_rng_float(r); }
 
+// Render-domain draws (camera jitter, defocus disk, ray time, every scatter draw):
+// the path's state takes the same Weyl step, and a 32-bit finalizer (lowbias32,
+// C. Wellons' hash-prospector: two 32-bit multiplies instead of SplitMix64's two
+// 64-bit ones, a third of the cost per draw on gfx950) mixes hi ^ lo of it into a
+// 24-bit uniform in [0, 1): k * 2^-24.  Keys stay mix64 (rtw_rng_stream), so
+// paths are independent streams; the scene / BVH / Perlin domains keep
+// rtw_rng_float (Zig's float(f32) mapping).
+RTW_HD uint32_t rtw_lowbias32(uint32_t x) {
+    x ^= x >> 16;
+    x *= 0x7feb352du;
+    x ^= x >> 15;
+    x *= 0x846ca68bu;
+    x ^= x >> 16;
+    return x;
+}
+RTW_HD float rtw_path_float(rtw_rng& r) {
+    r.s += RTW_GOLDEN;
+    const uint32_t h = rtw_lowbias32((uint32_t)(r.s >> 32) ^ (uint32_t)r.s);
+    return (float)(h >> 8) * 5.9604644775390625e-08f;  // exact: (h >> 8) < 2^24
+}
+RTW_HD float rtw_path_range(rtw_rng& r, float mn, float mx) { return mn + (mx - mn) * rtw_path_float(r); }
+
 // ConstantMedium.hit's one draw (objects.zig:484), keyed instead of sequential so
 // it does not depend on the order the BVH visits leaves: a float from the stream
 // started at mix64(path_state ^ K * (medium + 1)), path_state = the path's RNG

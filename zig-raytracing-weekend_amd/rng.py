@@ -51,6 +51,17 @@ class Stream:
         bits = ((126 - lz) << 23) | (x & 0x7FFFFF)
         return f32(struct.unpack("<f", struct.pack("<I", bits))[0])
 
+    def path_float(self) -> np.float32:
+        """Render-domain draw (rtw_rng.h rtw_path_float): Weyl step, lowbias32 of hi ^ lo, k * 2^-24."""
+        self.s = (self.s + GOLDEN) & MASK
+        x = ((self.s >> 32) ^ self.s) & 0xFFFFFFFF
+        x ^= x >> 16
+        x = (x * 0x7FEB352D) & 0xFFFFFFFF
+        x ^= x >> 15
+        x = (x * 0x846CA68B) & 0xFFFFFFFF
+        x ^= x >> 16
+        return f32((x >> 8) * 2.0 ** -24)
+
     def range(self, mn, mx) -> np.float32:
         """rtweekend.randomDoubleRange (src/rtweekend.zig:18-20)."""
         mn, mx = f32(mn), f32(mx)
