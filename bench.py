@@ -156,7 +156,11 @@ def main():
     dom_bytes_launch = dom_bytes_step * args.steps / max(1, kcalls[dom]) if dom_bytes_step is not None else None
     achieved = dom_bytes_launch / dom_launch_s / 1e9 if (dom_bytes_launch is not None and dom_launch_s > 0) else None
     path_achieved = alg_bytes / render_s / 1e9
-    traffic, traffic_src = pmc_traffic(args, {"trace": "wf_trace", "tail": "wf_tail", "mega": "render_"}.get(dom, dom))
+    # fused path (compact LDS stage): one gen+trace+shade kernel per iteration, timed as "trace"
+    fused = kcalls["trace"] > 0 and kcalls["shade"] == 0
+    knames = {"trace": "wf_step_clds" if fused else "wf_trace", "tail": "wf_tail", "mega": "render_persistent_v1"}
+    traffic, traffic_src = pmc_traffic(args, {"trace": "wf_step" if fused else "wf_trace", "tail": "wf_tail",
+                                              "mega": "render_"}.get(dom, dom))
 
     cpu = None
     if rank == 0 and world_size == 1 and not args.no_cpu_baseline:
@@ -186,7 +190,8 @@ def main():
                          "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved is not None else None,
                          "traffic": traffic,
                          "traffic_source": traffic_src,
-                         "kernel": {"trace": "wf_trace", "tail": "wf_tail", "mega": "render_persistent_v1"}.get(dom, dom),
+                         "kernel": knames.get(dom, dom),
+                         "fused_step": fused,
                          "avg_launch_ms": round(dom_launch_s * 1e3, 4),
                          "launches_per_step": kcalls[dom] / args.steps,
                          "alg_bytes_per_launch": round(dom_bytes_launch) if dom_bytes_launch is not None else None,

@@ -317,12 +317,13 @@ def test_v1_knobs_invariant(rtw, book1, knob, monkeypatch):
 @pytest.mark.parametrize("knob", [("RTW_WF_ITERS", "1"), ("RTW_WF_ITERS", "50"), ("RTW_WF_PATHS", "4096"),
                                   ("RTW_REFILL_MIN", "16"), ("RTW_FASTBOX", "0"), ("RTW_WF_LDS", "0"),
                                   ("RTW_SAH_LEAF", "4"), ("RTW_COMPACT", "0"),
-                                  ("RTW_WF_CLDS", "0")])
+                                  ("RTW_WF_CLDS", "0"), ("RTW_WF_FUSE", "0"), ("RTW_WF_FUSE", "1")])
 def test_wavefront_knobs_invariant(rtw, book1, knob, monkeypatch):
     """Wavefront knobs (bounces before the tail kernel, batch size -> many batches,
     per-lane refill in trace, FMA vs reference slab test, LDS-staged nodes, SAH
     leaf runs of up to 4 spheres, 16-B fp16-box nodes vs 32-B nodes, compact nodes in
-    LDS) never change a pixel."""
+    LDS, fused gen+trace+shade kernel vs separate kernels, LDS vs L1/L2 tail) never
+    change a pixel."""
     arr, world = book1
     cam = rtw.book1_camera(image_width=300, aspect_ratio=1.5, spp=5).init()
     ref = render_rows(rtw, world, cam, 0, 200, 0, 5, 4)

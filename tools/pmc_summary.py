@@ -20,7 +20,9 @@ import os
 import sys
 from collections import defaultdict
 
-KINDS = ("wf_gen", "wf_trace", "wf_shade", "wf_tail", "wf_reduce")
+KINDS = ("wf_gen", "wf_trace", "wf_step", "wf_shade", "wf_tail", "wf_reduce")
+# bench JSON launch key of each kind (wf_step: the fused gen+trace+shade kernel, timed as "trace")
+LAUNCH_KEY = {"wf_step": "trace"}
 
 
 def kind_of(name):
@@ -66,7 +68,7 @@ def main():
             if k:
                 byk[k].append((per[disp] * scale, short))
         for k, v in byk.items():
-            n = launches.get(k[3:], 0) or len(v)
+            n = launches.get(LAUNCH_KEY.get(k, k[3:]), 0) or len(v)
             keep = v[-n:]
             e = out.setdefault(k, {"launches": len(keep), "kernels": sorted({s for _, s in keep})})
             e[key] = sum(b for b, _ in keep) / max(1, len(keep))

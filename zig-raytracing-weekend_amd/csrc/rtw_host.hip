@@ -360,6 +360,10 @@ int rtw_scene_create(const rtw_scene_desc* d, int device, rtw_ctx** out) {
     L.wf_clds = 1;
     if (const char* cl = std::getenv("RTW_WF_CLDS")) L.wf_clds = (uint32_t)std::atoi(cl);
     if (const char* wl = std::getenv("RTW_WF_LDS")) L.wf_lds = (uint32_t)std::atoi(wl);
+    // compact LDS stage: gen, trace and shade of an iteration fused in one kernel
+    // (the ray/hit hand-off through HBM disappears), tail on the LDS stage
+    L.wf_fuse = 3;
+    if (const char* fu = std::getenv("RTW_WF_FUSE")) L.wf_fuse = (uint32_t)std::atoi(fu);
     // SAH trees: FMA slab test on the padded boxes + leaf postponement (both only
     // enlarge the set of visited nodes; reference trees keep the exact aabb.zig walk)
     const bool sah = ctx->box_pad > 0;
@@ -519,7 +523,7 @@ int run_wavefront(rtw_ctx* ctx, rtw_launch L, hipStream_t stream, rtw_timer* T) 
         ctx->wf_cap = 0;
         const uint64_t Q = slots(need);
         const size_t bytes = 2 * Q * (4 * 16 + 8 + 4) + Q * 8 + need * 16 +
-                             2 * RTW_WF_STRIPES * RTW_WF_LEN_STRIDE * 4 + 16 * 256;
+                             3 * (RTW_WF_STRIPES * RTW_WF_LEN_STRIDE * 4 + 256);
         HIP_TRY(hipMalloc(&ctx->d_wf, bytes));
         ctx->wf_cap = need;
     }
@@ -541,8 +545,7 @@ int run_wavefront(rtw_ctx* ctx, rtw_launch L, hipStream_t stream, rtw_timer* T) 
     }
     W.hit = reinterpret_cast<float2*>(take(Q * 8));
     W.ls = reinterpret_cast<float4*>(take(P * 16));
-    W.len[0] = reinterpret_cast<uint32_t*>(take(RTW_WF_STRIPES * RTW_WF_LEN_STRIDE * 4));
-    W.len[1] = reinterpret_cast<uint32_t*>(take(RTW_WF_STRIPES * RTW_WF_LEN_STRIDE * 4));
+    for (int k = 0; k < 3; k++) W.len[k] = reinterpret_cast<uint32_t*>(take(RTW_WF_STRIPES * RTW_WF_LEN_STRIDE * 4));
     W.n_pix = (uint32_t)n_pix;
     W.iters = ctx->wf_iters;
     const uint32_t s_end = L.s1;

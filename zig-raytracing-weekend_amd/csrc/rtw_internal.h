@@ -66,6 +66,8 @@ struct rtw_launch {
     uint32_t n_orders;           // 1, or 8 octant-ordered copies of the node array (SAH sphere scenes)
     uint32_t wf_lds;             // wavefront trace: stage the node array(s) in LDS when they fit
     uint32_t wf_clds;            // wavefront trace: stage the compact nodes (all orders) in LDS when they fit
+    uint32_t wf_fuse;            // with the compact LDS stage: one gen+trace+shade kernel per iteration,
+                                 // bit 1: the tail walks the LDS stage too
 };
 
 #define RTW_TILE_W 16

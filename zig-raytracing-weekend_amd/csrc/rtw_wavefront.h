@@ -39,7 +39,9 @@ struct rtw_wf {
     rtw_wf_set set[2];
     float2* hit;        // t, bits(hit leaf or -1), by slot of the iteration's input set
     float4* ls;         // final radiance .xyz by path id
-    uint32_t* len[2];   // stripe lengths of set[k], [s * RTW_WF_LEN_STRIDE]
+    uint32_t* len[3];   // stripe lengths of iteration it's input: len[it % 3][s * RTW_WF_LEN_STRIDE]
+                        // (three sets: a fused step kernel zeroes the counters of
+                        // iteration it+2 while it appends to those of it+1)
     uint32_t n_pix, n_s, n_paths, n_tx;
     uint32_t stripe_cap;
     uint32_t iters;     // wavefront iterations before the tail kernel

@@ -59,7 +59,7 @@ struct WfIter {
             const uint32_t s = w % RTW_WF_STRIPES;
             j = w / RTW_WF_STRIPES;
             step = nw / RTW_WF_STRIPES;
-            base = W.len[it & 1u][s * RTW_WF_LEN_STRIDE];  // slots used in the stripe
+            base = W.len[it % 3u][s * RTW_WF_LEN_STRIDE];  // slots used in the stripe
             n = (base + 63u) >> 6;
             off = s * W.stripe_cap;
         }
@@ -85,18 +85,19 @@ __device__ __forceinline__ bool wf_nth(const rtw_wf& W, uint32_t it, uint32_t m,
     }
     const uint32_t s = w % RTW_WF_STRIPES, R = nw / RTW_WF_STRIPES;
     const uint32_t k = ((((m >> 6) * R) + w / RTW_WF_STRIPES) << 6) | (m & 63u);
-    const uint32_t n = W.len[it & 1u][s * RTW_WF_LEN_STRIDE];
+    const uint32_t n = W.len[it % 3u][s * RTW_WF_LEN_STRIDE];
     end = (k & ~63u) >= n;
     slot = s * W.stripe_cap + k;
     return k < n;
 }
 
 // wave-aggregated slot allocation in this wave's output stripe of set[(it+1)&1]
+// (its counter: len[(it+1) % 3])
 __device__ __forceinline__ uint32_t wf_push(const rtw_wf& W, uint32_t it, bool push) {
     const uint64_t m = __ballot(push);
     if (!m) return 0;
     const uint32_t s = wf_wave() % RTW_WF_STRIPES, lane = __lane_id();
-    uint32_t* len = &W.len[(it + 1u) & 1u][s * RTW_WF_LEN_STRIDE];
+    uint32_t* len = &W.len[(it + 1u) % 3u][s * RTW_WF_LEN_STRIDE];
     uint32_t base = 0;
     if (lane == 0) base = atomicAdd(len, (uint32_t)__popcll(m));
     base = __shfl(base, 0);
@@ -167,7 +168,7 @@ __global__ __launch_bounds__(256) void wf_gen(rtw_launch L, rtw_wf W) {
 template <uint32_t FEAT, bool LDS>
 __global__ __launch_bounds__(256) void wf_trace(rtw_launch L, rtw_wf W, uint32_t it) {
     // the stripes shade(it) appends to start empty (they were iteration it-1's input)
-    if (blockIdx.x == 0) W.len[(it + 1u) & 1u][threadIdx.x * RTW_WF_LEN_STRIDE] = 0;
+    if (blockIdx.x == 0) W.len[(it + 1u) % 3u][threadIdx.x * RTW_WF_LEN_STRIDE] = 0;
     static_assert(RTW_WF_STRIPES == 256, "one block zeroes the stripe counters");
     const rtw_wf_set& S = W.set[it & 1u];
     Counters cnt;
@@ -292,7 +293,7 @@ __global__ __launch_bounds__(256) void wf_trace(rtw_launch L, rtw_wf W, uint32_t
 template <uint32_t FEAT>
 __global__ __launch_bounds__(1024) void wf_trace_clds(rtw_launch L, rtw_wf W, uint32_t it) {
     static_assert((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING)) == 0, "static sphere scenes");
-    if (blockIdx.x == 0 && threadIdx.x < RTW_WF_STRIPES) W.len[(it + 1u) & 1u][threadIdx.x * RTW_WF_LEN_STRIDE] = 0;
+    if (blockIdx.x == 0 && threadIdx.x < RTW_WF_STRIPES) W.len[(it + 1u) % 3u][threadIdx.x * RTW_WF_LEN_STRIDE] = 0;
     extern __shared__ uint4 wf_clds[];
     const uint32_t n4 = L.n_nodes * L.n_orders;
     for (uint32_t k = threadIdx.x; k < n4; k += blockDim.x) wf_clds[k] = L.cnodes[k];
@@ -361,9 +362,10 @@ __global__ __launch_bounds__(256) void wf_shade(rtw_launch L, rtw_wf W, uint32_t
 }
 
 // tail: the paths still queued after the last wavefront iteration, each to
-// completion; a lane whose path ends takes the wave's next path at once
-template <uint32_t FEAT>
-__global__ __launch_bounds__(256) void wf_tail(rtw_launch L, rtw_wf W, uint32_t it) {
+// completion; a lane whose path ends takes the wave's next path at once.
+// CLDS: the walk reads the compact nodes staged in LDS (`lds`) instead of L1/L2.
+template <uint32_t FEAT, bool CLDS>
+__device__ __forceinline__ void wf_tail_body(const rtw_launch& L, const rtw_wf& W, uint32_t it, const uint4* lds) {
     const uint32_t lane = __lane_id();
     const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     const rtw_wf_set& S = W.set[it & 1u];
@@ -399,7 +401,11 @@ __global__ __launch_bounds__(256) void wf_tail(rtw_launch L, rtw_wf W, uint32_t 
             cnt.rays++;
             cnt.tail_rays++;
             float t;
-            const int hit = traverse<FEAT>(L.nodes, L, r, t, cnt, rng.s);
+            int hit;
+            if constexpr (CLDS)
+                hit = L.counters ? traverse_compact<true>(L, lds, r, t, cnt) : traverse_compact<false>(L, lds, r, t, cnt);
+            else
+                hit = traverse<FEAT>(L.nodes, L, r, t, cnt, rng.s);
             bool done = true;
             if (hit < 0) {
                 acc = acc + thr * background(L, r);
@@ -417,6 +423,108 @@ __global__ __launch_bounds__(256) void wf_tail(rtw_launch L, rtw_wf W, uint32_t 
                 W.ls[pid] = make_float4(acc.x, acc.y, acc.z, 0);
                 active = false;
             }
+        }
+    }
+    flush_counters(L, cnt, 0);
+}
+
+template <uint32_t FEAT>
+__global__ __launch_bounds__(256) void wf_tail(rtw_launch L, rtw_wf W, uint32_t it) {
+    wf_tail_body<FEAT, false>(L, W, it, nullptr);
+}
+
+// every octant copy of the compact nodes into this block's LDS
+__device__ __forceinline__ void stage_clds(const rtw_launch& L, uint4* lds) {
+    const uint32_t n4 = L.n_nodes * L.n_orders;
+    for (uint32_t k = threadIdx.x; k < n4; k += blockDim.x) lds[k] = L.cnodes[k];
+    __syncthreads();
+}
+
+template <uint32_t FEAT>
+__global__ __launch_bounds__(1024) void wf_tail_clds(rtw_launch L, rtw_wf W, uint32_t it) {
+    static_assert((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING)) == 0, "static sphere scenes");
+    extern __shared__ uint4 wf_clds[];
+    stage_clds(L, wf_clds);
+    wf_tail_body<FEAT, true>(L, W, it, wf_clds);
+}
+
+// One fused wavefront iteration over the compact nodes staged in LDS (static
+// sphere SAH trees that fit, e.g. C2): iteration 0 generates the camera ray of
+// path p = slot in registers (wf_gen), every iteration walks the LDS copy
+// (wf_trace_clds) and shades (wf_shade) in the same kernel, appending the
+// survivors to the next set.  The ray never round-trips through HBM between
+// trace and shade (no hit records: 48 B/ray less traffic, no gen pass), and
+// the state streams of one wave overlap the LDS-bound walks of the others.
+// Same operations in the same order as gen/trace/shade: bit-identical.
+// The stripe counters: this kernel appends to len[(it+1)%3] (zeroed by the
+// previous iteration, or by the host for it = 0) and zeroes len[(it+2)%3],
+// iteration it-1's input, for the next iteration.
+template <uint32_t FEAT>
+__global__ __launch_bounds__(1024) void wf_step_clds(rtw_launch L, rtw_wf W, uint32_t it) {
+    static_assert((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING | RTW_F_LIGHT)) == 0, "static sphere scenes");
+    if (blockIdx.x == 0 && threadIdx.x < RTW_WF_STRIPES) W.len[(it + 2u) % 3u][threadIdx.x * RTW_WF_LEN_STRIDE] = 0;
+    extern __shared__ uint4 wf_clds[];
+    stage_clds(L, wf_clds);
+    const rtw_wf_set& S = W.set[it & 1u];
+    const rtw_wf_set& O = W.set[(it + 1u) & 1u];
+    Counters cnt;
+    for (WfIter e(W, it); e.more(); e.next()) {
+        bool live = false, push = false;
+        uint32_t slot = 0, pid = 0, depth = 0;
+        Ray r;
+        r.o = r.d = mk(0, 0, 0);
+        r.time = 0;
+        rtw_rng rng;
+        rng.s = 0;
+        f3 thr = mk(1, 1, 1);
+        if (e.get(W, slot)) {
+            if (it == 0) {  // wf_gen: camera.zig:169-180 with the +1 pixel offset (camera.zig:100-101)
+                pid = slot;
+                const uint32_t s_local = slot / W.n_pix, q = slot - s_local * W.n_pix;
+                uint32_t pixel, out_idx, x, y;
+                if (wf_pixel(L, W, q, pixel, out_idx, x, y) && L.max_depth > 0) {
+                    rng.s = rtw_mix64(L.key0 ^ (((uint64_t)pixel << 32) | (uint64_t)(L.s0 + s_local)));
+                    r = get_ray(L, x + L.pixel_offset, y + L.pixel_offset, rng);
+                    depth = L.max_depth;
+                    live = true;
+                } else {
+                    W.ls[slot] = make_float4(0, 0, 0, 0);  // rayColor(r, 0) = 0
+                }
+            } else {
+                r = wf_load_ray(S, slot, depth);
+                live = depth != 0;
+                if (live) {  // issued before the walk: the loads land while it runs
+                    pid = S.pid[slot];
+                    rng.s = S.rng[slot];
+                    const float4 t4 = S.thr[slot];
+                    thr = mk(t4.x, t4.y, t4.z);
+                }
+            }
+        }
+        Ray sc;
+        f3 acc = mk(0, 0, 0);
+        if (live) {
+            float t;
+            const int hit = L.counters ? traverse_compact<true>(L, wf_clds, r, t, cnt)
+                                       : traverse_compact<false>(L, wf_clds, r, t, cnt);
+            cnt.rays++;
+            if (hit < 0) {
+                acc = acc + thr * background(L, r);
+            } else {
+                f3 att;
+                if (shade<FEAT>(L.nodes, L, r, hit, t, rng, thr, acc, att, sc) && depth > 1) {
+                    thr = thr * att;
+                    push = true;
+                }
+            }
+            if (!push) W.ls[pid] = make_float4(acc.x, acc.y, acc.z, 0);
+        }
+        const uint32_t out = wf_push(W, it, push);
+        if (push) {
+            wf_store_ray(O, out, sc, depth - 1);
+            O.thr[out] = make_float4(thr.x, thr.y, thr.z, 0);
+            O.rng[out] = rng.s;
+            O.pid[out] = pid;
         }
     }
     flush_counters(L, cnt, 0);
@@ -483,9 +591,49 @@ const WfGrids<FEAT>& wf_grids(int n_cu) {
     return g;
 }
 
+// Fused path (L.wf_fuse & 1, compact LDS stage): wf_step_clds per iteration,
+// then the tail (on the LDS stage when L.wf_fuse & 2) and the reduce.
+template <uint32_t FEAT>
+void wf_run_fused(const rtw_launch& L, const rtw_wf& W, hipStream_t st, int n_cu, size_t clds, rtw_timer* T) {
+    static uint32_t grid[2] = {0, 0}, tgrid[2] = {0, 0};
+    if (grid[1] != clds) {
+        grid[0] = wf_grid(wf_step_clds<FEAT>, n_cu, clds, 1024);
+        tgrid[0] = wf_grid(wf_tail_clds<FEAT>, n_cu, clds, 1024);
+        grid[1] = tgrid[1] = (uint32_t)clds;
+    }
+    // iteration 0 appends to len[1]; every later iteration's output counters are
+    // zeroed by the kernel two iterations before (wf_step_clds)
+    (void)hipMemsetAsync(W.len[1], 0, RTW_WF_STRIPES * RTW_WF_LEN_STRIDE * 4, st);
+    const uint32_t iters = L.max_depth < W.iters ? L.max_depth : W.iters;
+    for (uint32_t it = 0; it < iters; it++) {
+        RTW_TIME_BEGIN(T, RTW_K_TRACE)
+        hipLaunchKernelGGL(wf_step_clds<FEAT>, dim3(grid[0]), dim3(1024), clds, st, L, W, it);
+        RTW_TIME_END(T)
+    }
+    if (iters < L.max_depth) {
+        RTW_TIME_BEGIN(T, RTW_K_TAIL)
+        if (L.wf_fuse & 2u)
+            hipLaunchKernelGGL(wf_tail_clds<FEAT>, dim3(tgrid[0]), dim3(1024), clds, st, L, W, iters);
+        else
+            hipLaunchKernelGGL(wf_tail<FEAT>, dim3(wf_grids<FEAT>(n_cu).tail), dim3(256), 0, st, L, W, iters);
+        RTW_TIME_END(T)
+    }
+    RTW_TIME_BEGIN(T, RTW_K_REDUCE)
+    hipLaunchKernelGGL(wf_reduce, dim3((W.n_pix + 255u) / 256u), dim3(256), 0, st, L, W);
+    RTW_TIME_END(T)
+}
+
 template <uint32_t FEAT>
 void wf_run(const rtw_launch& L, const rtw_wf& W, hipStream_t st, int n_cu, rtw_timer* T) {
     const WfGrids<FEAT>& g = wf_grids<FEAT>(n_cu);
+    if constexpr ((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING | RTW_F_LIGHT)) == 0) {
+        const size_t fclds = (size_t)L.n_nodes * L.n_orders * 16u;
+        if ((L.wf_fuse & 1u) && L.cnodes && L.fast_box && L.wf_clds && !L.refill_min && !L.postpone &&
+            fclds <= RTW_WF_CLDS_MAX) {
+            wf_run_fused<FEAT>(L, W, st, n_cu, fclds, T);
+            return;
+        }
+    }
     RTW_TIME_BEGIN(T, RTW_K_GEN)
     hipLaunchKernelGGL(wf_gen<FEAT>, dim3((W.n_paths + 255u) / 256u), dim3(256), 0, st, L, W);
     RTW_TIME_END(T)
