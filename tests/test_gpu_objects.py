@@ -107,6 +107,27 @@ def test_object_kernels_bit_identical(rtw, name, monkeypatch):
     assert np.array_equal(outs["v0"], outs["v1"]) and np.array_equal(outs["v0"], outs["wf"])
 
 
+@pytest.mark.parametrize("name", ["cornell", "cornell_smoke", "simple_light", "stress"])
+def test_fused_step_bit_identical(rtw, name, monkeypatch):
+    """The fused wavefront step (gen+trace+shade in one kernel; tree in LDS, or through
+    L1/L2 with RTW_WF_FUSE=7) renders exactly what the separate kernels render."""
+    if name == "stress":
+        arr = rtw.flatten(rtw.worlds.stress_world(5000, 1))
+        kw = dict(aspect_ratio=1.5, vfov=20.0, lookfrom=(13.0, 2.0, 3.0), lookat=(0.0, 0.0, 0.0),
+                  defocus_angle=0.6, focus_dist=10.0)
+    else:
+        arr = rtw.flatten(SCENES[name][0](rtw.worlds))
+        kw = SCENES[name][1]
+    cam = rtw.Camera(image_width=80, samples_per_pixel=6, max_depth=50, **kw).init()
+    outs = {}
+    for fuse in ("0", "3", "7"):
+        monkeypatch.setenv("RTW_WF_FUSE", fuse)
+        world = rtw.World(arr)
+        outs[fuse] = render_all(rtw, world, cam, 6, 5)
+        world.close()
+    assert np.array_equal(outs["0"], outs["3"]) and np.array_equal(outs["0"], outs["7"])
+
+
 def test_object_counters_equal_reference_traversal(rtw, oracle):
     """Reference topology: the device walk tests exactly the oracle's boxes and leaves."""
     import torch

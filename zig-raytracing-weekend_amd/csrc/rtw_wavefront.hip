@@ -448,23 +448,37 @@ __global__ __launch_bounds__(1024) void wf_tail_clds(rtw_launch L, rtw_wf W, uin
     wf_tail_body<FEAT, true>(L, W, it, wf_clds);
 }
 
-// One fused wavefront iteration over the compact nodes staged in LDS (static
-// sphere SAH trees that fit, e.g. C2): iteration 0 generates the camera ray of
-// path p = slot in registers (wf_gen), every iteration walks the LDS copy
-// (wf_trace_clds) and shades (wf_shade) in the same kernel, appending the
-// survivors to the next set.  The ray never round-trips through HBM between
-// trace and shade (no hit records: 48 B/ray less traffic, no gen pass), and
-// the state streams of one wave overlap the LDS-bound walks of the others.
-// Same operations in the same order as gen/trace/shade: bit-identical.
+// Where the fused step's walk reads the tree:
+//   WALK_CLDS   the compact nodes of every octant copy staged in LDS (small static sphere SAH trees, C2)
+//   WALK_LDS    the 32-B node array of one ordering staged in LDS (small object scenes: Cornell)
+//   WALK_GLOBAL L.cnodes / L.nodes through L1/L2 (large trees: C4)
+enum { WALK_CLDS = 0, WALK_LDS = 1, WALK_GLOBAL = 2 };
+
+template <uint32_t FEAT, int WALK>
+__device__ __forceinline__ int wf_walk(const rtw_launch& L, const void* lds, const Ray& r, float& t, Counters& cnt,
+                                       uint64_t mkey) {
+    if constexpr (WALK == WALK_CLDS) {
+        const uint4* cn = static_cast<const uint4*>(lds);
+        return L.counters ? traverse_compact<true>(L, cn, r, t, cnt) : traverse_compact<false>(L, cn, r, t, cnt);
+    } else if constexpr (WALK == WALK_LDS) {
+        return traverse<FEAT>(static_cast<const float4*>(lds), L, r, t, cnt, mkey);
+    } else {
+        return traverse<FEAT>(L.nodes, L, r, t, cnt, mkey);
+    }
+}
+
+// One fused wavefront iteration: iteration 0 generates the camera ray of path
+// p = slot in registers (wf_gen), every iteration walks the tree (wf_trace) and
+// shades (wf_shade) in the same kernel, appending the survivors to the next set.
+// The ray never round-trips through HBM between trace and shade (no hit records:
+// 48 B/ray less traffic, no gen pass), and the state streams of one wave overlap
+// the walks of the others.  Same operations in the same order as
+// gen/trace/shade: bit-identical.
 // The stripe counters: this kernel appends to len[(it+1)%3] (zeroed by the
 // previous iteration, or by the host for it = 0) and zeroes len[(it+2)%3],
 // iteration it-1's input, for the next iteration.
-template <uint32_t FEAT>
-__global__ __launch_bounds__(1024) void wf_step_clds(rtw_launch L, rtw_wf W, uint32_t it) {
-    static_assert((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING | RTW_F_LIGHT)) == 0, "static sphere scenes");
-    if (blockIdx.x == 0 && threadIdx.x < RTW_WF_STRIPES) W.len[(it + 2u) % 3u][threadIdx.x * RTW_WF_LEN_STRIDE] = 0;
-    extern __shared__ uint4 wf_clds[];
-    stage_clds(L, wf_clds);
+template <uint32_t FEAT, int WALK>
+__device__ __forceinline__ void wf_step_body(const rtw_launch& L, const rtw_wf& W, uint32_t it, const void* lds) {
     const rtw_wf_set& S = W.set[it & 1u];
     const rtw_wf_set& O = W.set[(it + 1u) & 1u];
     Counters cnt;
@@ -476,7 +490,7 @@ __global__ __launch_bounds__(1024) void wf_step_clds(rtw_launch L, rtw_wf W, uin
         r.time = 0;
         rtw_rng rng;
         rng.s = 0;
-        f3 thr = mk(1, 1, 1);
+        f3 thr = mk(1, 1, 1), acc = mk(0, 0, 0);
         if (e.get(W, slot)) {
             if (it == 0) {  // wf_gen: camera.zig:169-180 with the +1 pixel offset (camera.zig:100-101)
                 pid = slot;
@@ -496,17 +510,14 @@ __global__ __launch_bounds__(1024) void wf_step_clds(rtw_launch L, rtw_wf W, uin
                 if (live) {  // issued before the walk: the loads land while it runs
                     pid = S.pid[slot];
                     rng.s = S.rng[slot];
-                    const float4 t4 = S.thr[slot];
-                    thr = mk(t4.x, t4.y, t4.z);
+                    wf_load_state<FEAT>(L, S, slot, depth, thr, acc);
                 }
             }
         }
         Ray sc;
-        f3 acc = mk(0, 0, 0);
         if (live) {
             float t;
-            const int hit = L.counters ? traverse_compact<true>(L, wf_clds, r, t, cnt)
-                                       : traverse_compact<false>(L, wf_clds, r, t, cnt);
+            const int hit = wf_walk<FEAT, WALK>(L, lds, r, t, cnt, rng.s);
             cnt.rays++;
             if (hit < 0) {
                 acc = acc + thr * background(L, r);
@@ -525,9 +536,39 @@ __global__ __launch_bounds__(1024) void wf_step_clds(rtw_launch L, rtw_wf W, uin
             O.thr[out] = make_float4(thr.x, thr.y, thr.z, 0);
             O.rng[out] = rng.s;
             O.pid[out] = pid;
+            if constexpr ((FEAT & RTW_F_LIGHT) != 0) O.acc[out] = make_float4(acc.x, acc.y, acc.z, 0);
         }
     }
     flush_counters(L, cnt, 0);
+}
+
+__device__ __forceinline__ void wf_step_zero_next(const rtw_wf& W, uint32_t it) {
+    if (blockIdx.x == 0 && threadIdx.x < RTW_WF_STRIPES) W.len[(it + 2u) % 3u][threadIdx.x * RTW_WF_LEN_STRIDE] = 0;
+}
+
+// compact nodes of every octant copy in LDS (one 1024-thread block per CU)
+template <uint32_t FEAT>
+__global__ __launch_bounds__(1024) void wf_step_clds(rtw_launch L, rtw_wf W, uint32_t it) {
+    static_assert((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING)) == 0, "static sphere scenes");
+    wf_step_zero_next(W, it);
+    extern __shared__ uint4 wf_clds[];
+    stage_clds(L, wf_clds);
+    wf_step_body<FEAT, WALK_CLDS>(L, W, it, wf_clds);
+}
+
+// the 32-B node array (one ordering) in LDS, or the tree through L1/L2
+template <uint32_t FEAT, bool LDS>
+__global__ __launch_bounds__(256) void wf_step(rtw_launch L, rtw_wf W, uint32_t it) {
+    wf_step_zero_next(W, it);
+    if constexpr (LDS) {
+        extern __shared__ float4 wf_lds_nodes[];
+        const uint32_t n4 = 2u * L.n_nodes * L.n_orders;
+        for (uint32_t k = threadIdx.x; k < n4; k += 256u) wf_lds_nodes[k] = L.nodes[k];
+        __syncthreads();
+        wf_step_body<FEAT, WALK_LDS>(L, W, it, wf_lds_nodes);
+    } else {
+        wf_step_body<FEAT, WALK_GLOBAL>(L, W, it, nullptr);
+    }
 }
 
 // reduce: accum[pixel] += radiance of samples s0.. in sample order; .w = sample count
@@ -591,31 +632,64 @@ const WfGrids<FEAT>& wf_grids(int n_cu) {
     return g;
 }
 
-// Fused path (L.wf_fuse & 1, compact LDS stage): wf_step_clds per iteration,
-// then the tail (on the LDS stage when L.wf_fuse & 2) and the reduce.
+// Fused path (L.wf_fuse & 1): one wf_step* kernel per iteration, then the tail
+// (on the compact LDS stage when L.wf_fuse & 2) and the reduce.
+//   clds > 0: compact nodes of all orders in LDS (wf_step_clds, 1024 threads)
+//   lds  > 0: the 32-B node array in LDS (wf_step<FEAT, true>)
+//   else    : the tree through L1/L2 (wf_step<FEAT, false>)
 template <uint32_t FEAT>
-void wf_run_fused(const rtw_launch& L, const rtw_wf& W, hipStream_t st, int n_cu, size_t clds, rtw_timer* T) {
-    static uint32_t grid[2] = {0, 0}, tgrid[2] = {0, 0};
-    if (grid[1] != clds) {
-        grid[0] = wf_grid(wf_step_clds<FEAT>, n_cu, clds, 1024);
-        tgrid[0] = wf_grid(wf_tail_clds<FEAT>, n_cu, clds, 1024);
-        grid[1] = tgrid[1] = (uint32_t)clds;
+void wf_run_fused(const rtw_launch& L, const rtw_wf& W, hipStream_t st, int n_cu, size_t clds, size_t lds,
+                  rtw_timer* T) {
+    static uint32_t cgrid[2] = {0, 0}, tgrid[2] = {0, 0}, lgrid[2] = {0, 0}, ggrid = 0;
+    uint32_t grid = 0;
+    if constexpr ((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING)) == 0) {
+        if (clds && cgrid[1] != clds) {
+            cgrid[0] = wf_grid(wf_step_clds<FEAT>, n_cu, clds, 1024);
+            tgrid[0] = wf_grid(wf_tail_clds<FEAT>, n_cu, clds, 1024);
+            cgrid[1] = tgrid[1] = (uint32_t)clds;
+        }
+    }
+    if (clds) {
+        grid = cgrid[0];
+    } else if (lds) {
+        if (lgrid[1] != lds) {
+            lgrid[0] = wf_grid(wf_step<FEAT, true>, n_cu, lds);
+            lgrid[1] = (uint32_t)lds;
+        }
+        grid = lgrid[0];
+    } else {
+        if (!ggrid) ggrid = wf_grid(wf_step<FEAT, false>, n_cu);
+        grid = ggrid;
     }
     // iteration 0 appends to len[1]; every later iteration's output counters are
-    // zeroed by the kernel two iterations before (wf_step_clds)
+    // zeroed by the kernel two iterations before (wf_step_zero_next)
     (void)hipMemsetAsync(W.len[1], 0, RTW_WF_STRIPES * RTW_WF_LEN_STRIDE * 4, st);
     const uint32_t iters = L.max_depth < W.iters ? L.max_depth : W.iters;
     for (uint32_t it = 0; it < iters; it++) {
         RTW_TIME_BEGIN(T, RTW_K_TRACE)
-        hipLaunchKernelGGL(wf_step_clds<FEAT>, dim3(grid[0]), dim3(1024), clds, st, L, W, it);
+        if constexpr ((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING)) == 0) {
+            if (clds) {
+                hipLaunchKernelGGL(wf_step_clds<FEAT>, dim3(grid), dim3(1024), clds, st, L, W, it);
+                RTW_TIME_END(T)
+                continue;
+            }
+        }
+        if (lds)
+            hipLaunchKernelGGL((wf_step<FEAT, true>), dim3(grid), dim3(256), lds, st, L, W, it);
+        else
+            hipLaunchKernelGGL((wf_step<FEAT, false>), dim3(grid), dim3(256), 0, st, L, W, it);
         RTW_TIME_END(T)
     }
     if (iters < L.max_depth) {
         RTW_TIME_BEGIN(T, RTW_K_TAIL)
-        if (L.wf_fuse & 2u)
-            hipLaunchKernelGGL(wf_tail_clds<FEAT>, dim3(tgrid[0]), dim3(1024), clds, st, L, W, iters);
-        else
-            hipLaunchKernelGGL(wf_tail<FEAT>, dim3(wf_grids<FEAT>(n_cu).tail), dim3(256), 0, st, L, W, iters);
+        bool done = false;
+        if constexpr ((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING)) == 0) {
+            if (clds && (L.wf_fuse & 2u)) {
+                hipLaunchKernelGGL(wf_tail_clds<FEAT>, dim3(tgrid[0]), dim3(1024), clds, st, L, W, iters);
+                done = true;
+            }
+        }
+        if (!done) hipLaunchKernelGGL(wf_tail<FEAT>, dim3(wf_grids<FEAT>(n_cu).tail), dim3(256), 0, st, L, W, iters);
         RTW_TIME_END(T)
     }
     RTW_TIME_BEGIN(T, RTW_K_REDUCE)
@@ -626,11 +700,19 @@ void wf_run_fused(const rtw_launch& L, const rtw_wf& W, hipStream_t st, int n_cu
 template <uint32_t FEAT>
 void wf_run(const rtw_launch& L, const rtw_wf& W, hipStream_t st, int n_cu, rtw_timer* T) {
     const WfGrids<FEAT>& g = wf_grids<FEAT>(n_cu);
-    if constexpr ((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING | RTW_F_LIGHT)) == 0) {
-        const size_t fclds = (size_t)L.n_nodes * L.n_orders * 16u;
-        if ((L.wf_fuse & 1u) && L.cnodes && L.fast_box && L.wf_clds && !L.refill_min && !L.postpone &&
-            fclds <= RTW_WF_CLDS_MAX) {
-            wf_run_fused<FEAT>(L, W, st, n_cu, fclds, T);
+    if ((L.wf_fuse & 1u) && !L.refill_min && !L.postpone) {
+        size_t fclds = 0, flds = 0;
+        if constexpr ((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING)) == 0) {
+            const size_t c = (size_t)L.n_nodes * L.n_orders * 16u;
+            if (L.cnodes && L.fast_box && L.wf_clds && c <= RTW_WF_CLDS_MAX) fclds = c;
+        }
+        const size_t need = (size_t)L.n_nodes * L.n_orders * 32u;
+        if (!fclds && L.wf_lds && need <= RTW_WF_LDS_MAX) flds = (need + 511u) / 512u * 512u;
+        // measured: fused wins on C2 (+8.5 %), C5 (+24 %), Cornell (+2 %);
+        // through L1/L2 (C4, RTW_WF_FUSE bit 2) and with media (Cornell smoke) it loses 6 % / 1 %
+        const bool media = (L.feat & RTW_F_MEDIUM) != 0;
+        if (((fclds || flds) && !media) || (L.wf_fuse & 4u)) {
+            wf_run_fused<FEAT>(L, W, st, n_cu, fclds, flds, T);
             return;
         }
     }
