@@ -673,6 +673,66 @@ __device__ __forceinline__ int hit_with_order(int hit, uint32_t oct) {
 __device__ __forceinline__ float h_lo(uint32_t w) { return (float)__builtin_bit_cast(_Float16, (unsigned short)(w & 0xFFFFu)); }
 __device__ __forceinline__ float h_hi(uint32_t w) { return (float)__builtin_bit_cast(_Float16, (unsigned short)(w >> 16)); }
 
+// Compact walk with speculative leaf postponement (Aila & Laine 2009): a lane
+// that reaches a leaf keeps it pending and walks on through inner nodes; it
+// only waits when it reaches a second leaf.  The pending leaves are tested
+// together once at least leaf_min/64 of the walking lanes hold one, so the
+// sphere code runs in fewer wave steps (with 64 lanes and ~14 % of the node
+// visits at leaves it otherwise runs in nearly every step, lanes at inner
+// nodes idle).  Each lane's leaves are tested in walk order; boxes passed
+// meanwhile saw a larger `closest`: a superset of visits, the same closest hit.
+template <bool COUNT>
+__device__ __forceinline__ int traverse_compact_spec(const rtw_launch& L, const uint4* __restrict__ cn, const Ray& r,
+                                                     const RayTrav& rt, uint32_t oct, float& t_out, Counters& cnt) {
+    float closest = kInf;
+    int hit = -1;
+    uint32_t i = 0, pi = 0;
+    const uint32_t n = L.n_nodes;
+    bool pend = false, blocked = false;
+    uint4 pc = make_uint4(0, 0, 0, 0);
+    for (;;) {
+        if (i < n && !blocked) {
+            const uint4 c = cn[i];
+            if (c.w & RTW_LEAF_BIT) {
+                if (pend) {
+                    blocked = true;  // a second leaf: wait for the leaf round
+                } else {
+                    pend = true;
+                    pc = c;
+                    pi = i;
+                    i++;  // a leaf's skip is i + 1
+                }
+            } else {
+                if constexpr (COUNT) cnt.nodes++;
+                const float tnx = __builtin_fmaf(h_lo(c.x), rt.inv.x, rt.oinv.x);
+                const float tny = __builtin_fmaf(h_hi(c.x), rt.inv.y, rt.oinv.y);
+                const float tnz = __builtin_fmaf(h_lo(c.y), rt.inv.z, rt.oinv.z);
+                const float tfx = __builtin_fmaf(h_hi(c.y), rt.inv.x, rt.oinv.x);
+                const float tfy = __builtin_fmaf(h_lo(c.z), rt.inv.y, rt.oinv.y);
+                const float tfz = __builtin_fmaf(h_hi(c.z), rt.inv.z, rt.oinv.z);
+                const float lo = __builtin_fmaxf(__builtin_fmaxf(kTmin, tnx), __builtin_fmaxf(tny, tnz));
+                const float hi = __builtin_fminf(__builtin_fminf(closest, tfx), __builtin_fminf(tfy, tfz));
+                i = (hi <= lo) ? c.w : i + 1;
+            }
+        }
+        const uint64_t busy = __ballot(i < n || pend);
+        if (!busy) break;
+        const uint32_t n_pend = (uint32_t)__popcll(__ballot(pend));
+        const uint32_t n_walk = (uint32_t)__popcll(__ballot(i < n && !blocked));
+        if (n_pend && (n_walk == 0 || n_pend * 64u >= (uint32_t)__popcll(busy) * L.leaf_min)) {
+            if (pend) {
+                if constexpr (COUNT) cnt.leaves++;
+                sphere_leaf(L, r, rt, mk(__uint_as_float(pc.x), __uint_as_float(pc.y), __uint_as_float(pc.z)),
+                            __uint_as_float(pc.w & ~RTW_LEAF_BIT), pi, closest, hit);
+                pend = false;
+                blocked = false;
+            }
+        }
+    }
+    t_out = closest;
+    return hit_with_order(hit, oct);
+}
+
 // `base`: L.cnodes, or their copy in LDS
 template <bool COUNT>
 __device__ __forceinline__ int traverse_compact(const rtw_launch& L, const uint4* base, const Ray& r, float& t_out,
@@ -688,6 +748,7 @@ __device__ __forceinline__ int traverse_compact(const rtw_launch& L, const uint4
                 (oct & 2u) ? -__builtin_fabsf(rt.inv.y) : __builtin_fabsf(rt.inv.y),
                 (oct & 4u) ? -__builtin_fabsf(rt.inv.z) : __builtin_fabsf(rt.inv.z));
     rt.oinv = mk(-(r.o.x * rt.inv.x), -(r.o.y * rt.inv.y), -(r.o.z * rt.inv.z));
+    if (L.walk_spec) return traverse_compact_spec<COUNT>(L, cn, r, rt, oct, t_out, cnt);
     float closest = kInf;
     int hit = -1;
     uint32_t i = 0;
@@ -977,20 +1038,14 @@ __device__ __forceinline__ bool shade(const float4* __restrict__ nodes, const rt
 // Wave-cooperative rejection sampling (vec3.randomInUnitSphere D=3 /
 // randomInUnitDisk D=2, vec3.zig:40-45, 59-64).  The sequential loop runs until
 // the slowest lane of the wave accepts (E[max] ~ 6 iterations for 48 lanes at
-// p = 0.52).  The RNG is counter-based, so candidate j of a lane is simply draws
-// j*D+1 .. j*D+D after its current state: every round, all 64 lanes evaluate
-// candidates of the still-unresolved lanes (64/n helpers each, consecutive j),
-// and each lane takes its FIRST accepted candidate -- exactly the sequential
-// result and stream position.  A draw on Zig's rare extra-draw path
-// (clz >= 41, p = 2^-41) would shift positions: such a lane falls back to the
-// sequential loop from its start.  Must be called with every lane of the wave
-// converged (helpers are idle lanes).
+// p = 0.52).  Render-domain draws are counter-based (rtw_path_float: one Weyl
+// step each), so candidate j of a lane is draws j*D+1 .. j*D+D after its current
+// state: every round, all 64 lanes evaluate candidates of the still-unresolved
+// lanes (64/n helpers each, consecutive j), and each lane takes its FIRST
+// accepted candidate -- exactly the sequential result and stream position.
+// Must be called with every lane of the wave converged (helpers are idle
+// lanes); `slot` is 64 u32 of per-wave LDS scratch.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ float float_from_draw(uint64_t x, int lz) {
-    const uint32_t bits = ((uint32_t)(126 - lz) << 23) | (uint32_t)(x & 0x7FFFFFu);
-    return __uint_as_float(bits);
-}
-
 template <int D>
 __device__ __forceinline__ void seq_reject(rtw_rng& rng, float (&out)[D]) {
     for (;;) {
@@ -1021,53 +1076,45 @@ __device__ __forceinline__ void coop_reject(bool active, rtw_rng& rng, float (&o
     if (!pend) return;
     const uint64_t s0 = rng.s;
     uint32_t base = 0;
-    bool done = !active, fall = false;
     while (pend) {
         const uint32_t n = (uint32_t)__popcll(pend);
         const uint32_t k = 64u / n;
         const bool me = (pend >> lane) & 1ull;
         const uint32_t rank = (uint32_t)__popcll(pend & lt);
         if (me) slot[rank] = lane;
+        __builtin_amdgcn_wave_barrier();
         const uint32_t tr = lane / k;
         const bool helper = tr < n;
         const uint32_t tl = helper ? slot[tr] : lane;
         const uint32_t ts_lo = __shfl((uint32_t)s0, (int)tl), ts_hi = __shfl((uint32_t)(s0 >> 32), (int)tl);
         const uint32_t tj = (uint32_t)__shfl((int)base, (int)tl) + (lane - tr * k);
         float v[D];
-        bool acc = false, rare = false;
+        bool acc = false;
         if (helper) {
-            uint64_t st = (((uint64_t)ts_hi << 32) | ts_lo) + (uint64_t)(tj * (uint32_t)D) * RTW_GOLDEN;
-            float ls = 0.0f;
+            rtw_rng c;
+            c.s = (((uint64_t)ts_hi << 32) | ts_lo) + (uint64_t)(tj * (uint32_t)D) * RTW_GOLDEN;
 #pragma unroll
-            for (int d = 0; d < D; d++) {
-                st += RTW_GOLDEN;
-                const uint64_t x = rtw_mix64(st);
-                const int lz = rtw_clz64(x);
-                rare = rare || lz >= 41;
-                v[d] = -1.0f + 2.0f * float_from_draw(x, lz);  // randomDoubleRange(-1, 1)
-            }
+            for (int d = 0; d < D; d++) v[d] = rtw_path_range(c, -1, 1);
+            float ls;
             if constexpr (D == 3) ls = v[0] * v[0] + v[1] * v[1] + v[2] * v[2];
-            else ls = v[0] * v[0] + v[1] * v[1];            // + 0*0 of the disk's z (exact)
-            acc = !rare && ls < 1.0f;
+            else ls = v[0] * v[0] + v[1] * v[1];  // + 0*0 of the disk's z (exact)
+            acc = ls < 1.0f;
         } else {
 #pragma unroll
             for (int d = 0; d < D; d++) v[d] = 0.0f;
         }
-        const uint64_t accb = __ballot(acc), rareb = __ballot(rare);
+        const uint64_t accb = __ballot(acc);
         const uint32_t off = me ? rank * k : 0u;
         const uint64_t m = (k >= 64u) ? ~0ull : ((1ull << k) - 1ull);
         const uint64_t a = me ? ((accb >> off) & m) : 0ull;
-        const uint64_t q = me ? ((rareb >> off) & m) : 0ull;
         const uint32_t fa = a ? (uint32_t)__builtin_ctzll(a) : 64u;
-        const uint32_t fq = q ? (uint32_t)__builtin_ctzll(q) : 64u;
         const int src = (int)((me && fa < 64u) ? off + fa : lane);
         float got[D];
 #pragma unroll
         for (int d = 0; d < D; d++) got[d] = __shfl(v[d], src);
+        bool done = !me;
         if (me) {
-            if (fq < 64u && fq <= fa) {
-                fall = true;
-            } else if (fa < 64u) {
+            if (fa < 64u) {
 #pragma unroll
                 for (int d = 0; d < D; d++) out[d] = got[d];
                 rng.s = s0 + (uint64_t)((base + fa + 1u) * (uint32_t)D) * RTW_GOLDEN;
@@ -1076,12 +1123,35 @@ __device__ __forceinline__ void coop_reject(bool active, rtw_rng& rng, float (&o
                 base += k;
             }
         }
-        pend = __ballot(!done && !fall);
+        __builtin_amdgcn_wave_barrier();  // slot[] is rewritten next round
+        pend = __ballot(!done);
     }
-    if (fall) {  // exact sequential path (rare-draw safe)
-        rng.s = s0;
-        seq_reject<D>(rng, out);
+}
+
+// Camera.getRay for every lane of the wave (`active` lanes get a ray), the
+// defocus disk's rejection loop wave-cooperatively (coop_reject): the same draws
+// in the same order as get_ray.  Must be called with the wave converged.
+__device__ __forceinline__ Ray get_ray_wave(const rtw_launch& L, bool active, uint32_t i, uint32_t j, rtw_rng& rng,
+                                            uint32_t* slot) {
+    const f3 du = ld3(L.du), dv = ld3(L.dv);
+    f3 pixel_sample = mk(0, 0, 0);
+    if (active) {
+        const f3 pixel_center = (ld3(L.pixel00) + du * splat((float)i)) + dv * splat((float)j);
+        const float px = -0.5f + rnd(rng);
+        const float py = -0.5f + rnd(rng);
+        pixel_sample = pixel_center + (splat(px) * du + splat(py) * dv);
     }
+    f3 origin = ld3(L.center);
+    if (L.defocus_angle > 0) {
+        float dsk[2] = {0.0f, 0.0f};
+        coop_reject<2>(active, rng, dsk, slot, L.coop != 0);
+        origin = (origin + ld3(L.disk_u) * splat(dsk[0])) + ld3(L.disk_v) * splat(dsk[1]);
+    }
+    Ray r;
+    r.o = origin;
+    r.d = pixel_sample - origin;
+    r.time = active ? rnd(rng) : 0.0f;
+    return r;
 }
 
 // One sample's radiance: getRay + iterative rayColor (camera.zig:169-208).

@@ -478,11 +478,12 @@ __device__ __forceinline__ int wf_walk(const rtw_launch& L, const void* lds, con
 // previous iteration, or by the host for it = 0) and zeroes len[(it+2)%3],
 // iteration it-1's input, for the next iteration.
 template <uint32_t FEAT, int WALK>
-__device__ __forceinline__ void wf_step_body(const rtw_launch& L, const rtw_wf& W, uint32_t it, const void* lds) {
+__device__ __forceinline__ void wf_step_body(const rtw_launch& L, const rtw_wf& W, uint32_t it, const void* lds,
+                                             uint32_t* coop_slot) {
     const rtw_wf_set& S = W.set[it & 1u];
     const rtw_wf_set& O = W.set[(it + 1u) & 1u];
     Counters cnt;
-    for (WfIter e(W, it); e.more(); e.next()) {
+    for (WfIter e(W, it); e.more(); e.next()) {  // wave-uniform: the body starts converged
         bool live = false, push = false;
         uint32_t slot = 0, pid = 0, depth = 0;
         Ray r;
@@ -491,45 +492,79 @@ __device__ __forceinline__ void wf_step_body(const rtw_launch& L, const rtw_wf& 
         rtw_rng rng;
         rng.s = 0;
         f3 thr = mk(1, 1, 1), acc = mk(0, 0, 0);
-        if (e.get(W, slot)) {
-            if (it == 0) {  // wf_gen: camera.zig:169-180 with the +1 pixel offset (camera.zig:100-101)
+        const bool got = e.get(W, slot);
+        if (it == 0) {  // wf_gen: camera.zig:169-180 with the +1 pixel offset (camera.zig:100-101)
+            uint32_t pixel = 0, out_idx, x = 0, y = 0;
+            if (got) {
                 pid = slot;
                 const uint32_t s_local = slot / W.n_pix, q = slot - s_local * W.n_pix;
-                uint32_t pixel, out_idx, x, y;
-                if (wf_pixel(L, W, q, pixel, out_idx, x, y) && L.max_depth > 0) {
-                    rng.s = rtw_mix64(L.key0 ^ (((uint64_t)pixel << 32) | (uint64_t)(L.s0 + s_local)));
-                    r = get_ray(L, x + L.pixel_offset, y + L.pixel_offset, rng);
-                    depth = L.max_depth;
-                    live = true;
-                } else {
-                    W.ls[slot] = make_float4(0, 0, 0, 0);  // rayColor(r, 0) = 0
-                }
+                live = wf_pixel(L, W, q, pixel, out_idx, x, y) && L.max_depth > 0;
+                if (live) rng.s = rtw_mix64(L.key0 ^ (((uint64_t)pixel << 32) | (uint64_t)(L.s0 + s_local)));
+                else W.ls[slot] = make_float4(0, 0, 0, 0);  // rayColor(r, 0) = 0
+            }
+            if constexpr ((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM)) == 0) {
+                r = get_ray_wave(L, live, x + L.pixel_offset, y + L.pixel_offset, rng, coop_slot);
             } else {
-                r = wf_load_ray(S, slot, depth);
-                live = depth != 0;
-                if (live) {  // issued before the walk: the loads land while it runs
-                    pid = S.pid[slot];
-                    rng.s = S.rng[slot];
-                    wf_load_state<FEAT>(L, S, slot, depth, thr, acc);
-                }
+                if (live) r = get_ray(L, x + L.pixel_offset, y + L.pixel_offset, rng);
+            }
+            depth = live ? L.max_depth : 0;
+        } else if (got) {
+            r = wf_load_ray(S, slot, depth);
+            live = depth != 0;
+            if (live) {  // issued before the walk: the loads land while it runs
+                pid = S.pid[slot];
+                rng.s = S.rng[slot];
+                wf_load_state<FEAT>(L, S, slot, depth, thr, acc);
             }
         }
         Ray sc;
-        if (live) {
-            float t;
-            const int hit = wf_walk<FEAT, WALK>(L, lds, r, t, cnt, rng.s);
-            cnt.rays++;
-            if (hit < 0) {
-                acc = acc + thr * background(L, r);
-            } else {
+        if constexpr ((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM)) == 0) {
+            // sphere scenes: hit record, then the randomUnitVector draw of every lane
+            // that needs one (wave-cooperatively with RTW_COOP=1), then the material --
+            // measured faster than the nested form below (C2 +6 %, C5 +3 %)
+            HitPrep hp;
+            bool hitp = false, need_uv = false;
+            if (live) {
+                float t;
+                const int hit = wf_walk<FEAT, WALK>(L, lds, r, t, cnt, rng.s);
+                cnt.rays++;
+                if (hit < 0) {
+                    acc = acc + thr * background(L, r);
+                } else {
+                    hp = hit_prep<FEAT>(L.nodes, L, r, hit, t);
+                    hitp = true;
+                    need_uv = needs_unit_vector<FEAT>(hp.m.kind);
+                }
+            }
+            float uv3[3] = {0.0f, 0.0f, 0.0f};
+            coop_reject<3>(need_uv, rng, uv3, coop_slot, L.coop != 0);
+            if (hitp) {
+                const f3 ruv = need_uv ? unit_vector(mk(uv3[0], uv3[1], uv3[2])) : mk(0, 0, 0);
                 f3 att;
-                if (shade<FEAT>(L.nodes, L, r, hit, t, rng, thr, acc, att, sc) && depth > 1) {
+                if (scatter_finish<FEAT>(L, r, hp, ruv, rng, thr, acc, att, sc) && depth > 1) {
                     thr = thr * att;
                     push = true;
                 }
             }
-            if (!push) W.ls[pid] = make_float4(acc.x, acc.y, acc.z, 0);
+        } else {
+            // object scenes: Material.scatter inline (the split form's live hit record
+            // costs a wave per SIMD here: Cornell -12 %)
+            if (live) {
+                float t;
+                const int hit = wf_walk<FEAT, WALK>(L, lds, r, t, cnt, rng.s);
+                cnt.rays++;
+                if (hit < 0) {
+                    acc = acc + thr * background(L, r);
+                } else {
+                    f3 att;
+                    if (shade<FEAT>(L.nodes, L, r, hit, t, rng, thr, acc, att, sc) && depth > 1) {
+                        thr = thr * att;
+                        push = true;
+                    }
+                }
+            }
         }
+        if (live && !push) W.ls[pid] = make_float4(acc.x, acc.y, acc.z, 0);
         const uint32_t out = wf_push(W, it, push);
         if (push) {
             wf_store_ray(O, out, sc, depth - 1);
@@ -553,21 +588,24 @@ __global__ __launch_bounds__(1024) void wf_step_clds(rtw_launch L, rtw_wf W, uin
     wf_step_zero_next(W, it);
     extern __shared__ uint4 wf_clds[];
     stage_clds(L, wf_clds);
-    wf_step_body<FEAT, WALK_CLDS>(L, W, it, wf_clds);
+    // per-wave coop_reject scratch after the nodes (the host adds RTW_WF_COOP_LDS(1024) bytes)
+    uint32_t* coop = reinterpret_cast<uint32_t*>(wf_clds + L.n_nodes * L.n_orders) + 64u * (threadIdx.x >> 6);
+    wf_step_body<FEAT, WALK_CLDS>(L, W, it, wf_clds, coop);
 }
 
 // the 32-B node array (one ordering) in LDS, or the tree through L1/L2
 template <uint32_t FEAT, bool LDS>
 __global__ __launch_bounds__(256) void wf_step(rtw_launch L, rtw_wf W, uint32_t it) {
     wf_step_zero_next(W, it);
+    extern __shared__ float4 wf_lds_nodes[];
+    const uint32_t n4 = LDS ? 2u * L.n_nodes * L.n_orders : 0u;
+    uint32_t* coop = reinterpret_cast<uint32_t*>(wf_lds_nodes + n4) + 64u * (threadIdx.x >> 6);
     if constexpr (LDS) {
-        extern __shared__ float4 wf_lds_nodes[];
-        const uint32_t n4 = 2u * L.n_nodes * L.n_orders;
         for (uint32_t k = threadIdx.x; k < n4; k += 256u) wf_lds_nodes[k] = L.nodes[k];
         __syncthreads();
-        wf_step_body<FEAT, WALK_LDS>(L, W, it, wf_lds_nodes);
+        wf_step_body<FEAT, WALK_LDS>(L, W, it, wf_lds_nodes, coop);
     } else {
-        wf_step_body<FEAT, WALK_GLOBAL>(L, W, it, nullptr);
+        wf_step_body<FEAT, WALK_GLOBAL>(L, W, it, nullptr, coop);
     }
 }
 
@@ -637,14 +675,18 @@ const WfGrids<FEAT>& wf_grids(int n_cu) {
 //   clds > 0: compact nodes of all orders in LDS (wf_step_clds, 1024 threads)
 //   lds  > 0: the 32-B node array in LDS (wf_step<FEAT, true>)
 //   else    : the tree through L1/L2 (wf_step<FEAT, false>)
+// dynamic LDS of the fused kernels: tree stage + 64 u32 of coop_reject scratch per wave
+#define RTW_WF_COOP_LDS(threads) ((threads) / 64u * 256u)
+
 template <uint32_t FEAT>
 void wf_run_fused(const rtw_launch& L, const rtw_wf& W, hipStream_t st, int n_cu, size_t clds, size_t lds,
                   rtw_timer* T) {
+    const size_t cdyn = clds + RTW_WF_COOP_LDS(1024), ldyn = lds + RTW_WF_COOP_LDS(256), gdyn = RTW_WF_COOP_LDS(256);
     static uint32_t cgrid[2] = {0, 0}, tgrid[2] = {0, 0}, lgrid[2] = {0, 0}, ggrid = 0;
     uint32_t grid = 0;
     if constexpr ((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING)) == 0) {
         if (clds && cgrid[1] != clds) {
-            cgrid[0] = wf_grid(wf_step_clds<FEAT>, n_cu, clds, 1024);
+            cgrid[0] = wf_grid(wf_step_clds<FEAT>, n_cu, cdyn, 1024);
             tgrid[0] = wf_grid(wf_tail_clds<FEAT>, n_cu, clds, 1024);
             cgrid[1] = tgrid[1] = (uint32_t)clds;
         }
@@ -653,12 +695,12 @@ void wf_run_fused(const rtw_launch& L, const rtw_wf& W, hipStream_t st, int n_cu
         grid = cgrid[0];
     } else if (lds) {
         if (lgrid[1] != lds) {
-            lgrid[0] = wf_grid(wf_step<FEAT, true>, n_cu, lds);
+            lgrid[0] = wf_grid(wf_step<FEAT, true>, n_cu, ldyn);
             lgrid[1] = (uint32_t)lds;
         }
         grid = lgrid[0];
     } else {
-        if (!ggrid) ggrid = wf_grid(wf_step<FEAT, false>, n_cu);
+        if (!ggrid) ggrid = wf_grid(wf_step<FEAT, false>, n_cu, gdyn);
         grid = ggrid;
     }
     // iteration 0 appends to len[1]; every later iteration's output counters are
@@ -669,15 +711,15 @@ void wf_run_fused(const rtw_launch& L, const rtw_wf& W, hipStream_t st, int n_cu
         RTW_TIME_BEGIN(T, RTW_K_TRACE)
         if constexpr ((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING)) == 0) {
             if (clds) {
-                hipLaunchKernelGGL(wf_step_clds<FEAT>, dim3(grid), dim3(1024), clds, st, L, W, it);
+                hipLaunchKernelGGL(wf_step_clds<FEAT>, dim3(grid), dim3(1024), cdyn, st, L, W, it);
                 RTW_TIME_END(T)
                 continue;
             }
         }
         if (lds)
-            hipLaunchKernelGGL((wf_step<FEAT, true>), dim3(grid), dim3(256), lds, st, L, W, it);
+            hipLaunchKernelGGL((wf_step<FEAT, true>), dim3(grid), dim3(256), ldyn, st, L, W, it);
         else
-            hipLaunchKernelGGL((wf_step<FEAT, false>), dim3(grid), dim3(256), 0, st, L, W, it);
+            hipLaunchKernelGGL((wf_step<FEAT, false>), dim3(grid), dim3(256), gdyn, st, L, W, it);
         RTW_TIME_END(T)
     }
     if (iters < L.max_depth) {
