@@ -102,7 +102,13 @@ RTW_HD uint32_t rtw_lowbias32(uint32_t x) {
 }
 RTW_HD float rtw_path_float(rtw_rng& r) {
     r.s += RTW_GOLDEN;
+#if defined(RTW_ABLATE_RNG) && defined(__HIP_DEVICE_COMPILE__)
+    // timing ablation only (wrong numbers): multiply-free xorshift finalizer
+    uint32_t h = (uint32_t)(r.s >> 32) ^ (uint32_t)r.s;
+    h ^= h << 13; h ^= h >> 17; h ^= h << 5;
+#else
     const uint32_t h = rtw_lowbias32((uint32_t)(r.s >> 32) ^ (uint32_t)r.s);
+#endif
     return (float)(h >> 8) * 5.9604644775390625e-08f;  // exact: (h >> 8) < 2^24
 }
 RTW_HD float rtw_path_range(rtw_rng& r, float mn, float mx) { return mn + (mx - mn) * rtw_path_float(r); }
