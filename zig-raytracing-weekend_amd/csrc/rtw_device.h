@@ -540,15 +540,13 @@ __device__ __forceinline__ void sphere_leaf(const rtw_launch& L, const Ray& r, c
         // only if r2 > tmin and r1 < closest: with |r - q| <= e, only if q2 + e > tmin and
         // q1 - e < closest (a necessary condition; non-short-circuit & and |, no branches).
         sa = __builtin_amdgcn_sqrtf(disc);
-        const bool guard = (L.fast_reject != 0) & (rt.rcp_a != 0.0f) & (disc > 1e-30f) & (disc < 1e30f) &
+        const float e = (__builtin_fabsf(half_b) + sa) * rt.rcp_a * 3.8146973e-06f;
+        const float q1 = (-half_b - sa) * rt.rcp_a;
+        const float q2 = (-half_b + sa) * rt.rcp_a;
+        const bool guard = L.fast_reject & (rt.rcp_a != 0.0f) & (disc > 1e-30f) & (disc < 1e30f) &
                            (__builtin_fabsf(half_b) < 1e15f);
-        if (L.fast_reject == 1) {  // the filter (RTW_FAST_REJECT=2: none, every disc >= 0 runs the exact roots)
-            const float e = (__builtin_fabsf(half_b) + sa) * rt.rcp_a * 3.8146973e-06f;
-            const float q1 = (-half_b - sa) * rt.rcp_a;
-            const float q2 = (-half_b + sa) * rt.rcp_a;
-            const bool plausible = (q2 + e > kTmin) & (q1 - e < closest);
-            exact = exact & (plausible | !guard);
-        }
+        const bool plausible = (q2 + e > kTmin) & (q1 - e < closest);
+        exact = exact & (plausible | !guard);
         // under the guard |-hb -+ sq| < 2^51 and disc >= 2^-96; with a in [2^-40, 2^40] the
         // divisions are unscaled except for quotients below 2^-80, which kTmin rejects
         // either way
