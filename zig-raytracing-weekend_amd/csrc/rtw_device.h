@@ -673,66 +673,6 @@ __device__ __forceinline__ int hit_with_order(int hit, uint32_t oct) {
 __device__ __forceinline__ float h_lo(uint32_t w) { return (float)__builtin_bit_cast(_Float16, (unsigned short)(w & 0xFFFFu)); }
 __device__ __forceinline__ float h_hi(uint32_t w) { return (float)__builtin_bit_cast(_Float16, (unsigned short)(w >> 16)); }
 
-// Compact walk with speculative leaf postponement (Aila & Laine 2009): a lane
-// that reaches a leaf keeps it pending and walks on through inner nodes; it
-// only waits when it reaches a second leaf.  The pending leaves are tested
-// together once at least leaf_min/64 of the walking lanes hold one, so the
-// sphere code runs in fewer wave steps (with 64 lanes and ~14 % of the node
-// visits at leaves it otherwise runs in nearly every step, lanes at inner
-// nodes idle).  Each lane's leaves are tested in walk order; boxes passed
-// meanwhile saw a larger `closest`: a superset of visits, the same closest hit.
-template <bool COUNT>
-__device__ __forceinline__ int traverse_compact_spec(const rtw_launch& L, const uint4* __restrict__ cn, const Ray& r,
-                                                     const RayTrav& rt, uint32_t oct, float& t_out, Counters& cnt) {
-    float closest = kInf;
-    int hit = -1;
-    uint32_t i = 0, pi = 0;
-    const uint32_t n = L.n_nodes;
-    bool pend = false, blocked = false;
-    uint4 pc = make_uint4(0, 0, 0, 0);
-    for (;;) {
-        if (i < n && !blocked) {
-            const uint4 c = cn[i];
-            if (c.w & RTW_LEAF_BIT) {
-                if (pend) {
-                    blocked = true;  // a second leaf: wait for the leaf round
-                } else {
-                    pend = true;
-                    pc = c;
-                    pi = i;
-                    i++;  // a leaf's skip is i + 1
-                }
-            } else {
-                if constexpr (COUNT) cnt.nodes++;
-                const float tnx = __builtin_fmaf(h_lo(c.x), rt.inv.x, rt.oinv.x);
-                const float tny = __builtin_fmaf(h_hi(c.x), rt.inv.y, rt.oinv.y);
-                const float tnz = __builtin_fmaf(h_lo(c.y), rt.inv.z, rt.oinv.z);
-                const float tfx = __builtin_fmaf(h_hi(c.y), rt.inv.x, rt.oinv.x);
-                const float tfy = __builtin_fmaf(h_lo(c.z), rt.inv.y, rt.oinv.y);
-                const float tfz = __builtin_fmaf(h_hi(c.z), rt.inv.z, rt.oinv.z);
-                const float lo = __builtin_fmaxf(__builtin_fmaxf(kTmin, tnx), __builtin_fmaxf(tny, tnz));
-                const float hi = __builtin_fminf(__builtin_fminf(closest, tfx), __builtin_fminf(tfy, tfz));
-                i = (hi <= lo) ? c.w : i + 1;
-            }
-        }
-        const uint64_t busy = __ballot(i < n || pend);
-        if (!busy) break;
-        const uint32_t n_pend = (uint32_t)__popcll(__ballot(pend));
-        const uint32_t n_walk = (uint32_t)__popcll(__ballot(i < n && !blocked));
-        if (n_pend && (n_walk == 0 || n_pend * 64u >= (uint32_t)__popcll(busy) * L.leaf_min)) {
-            if (pend) {
-                if constexpr (COUNT) cnt.leaves++;
-                sphere_leaf(L, r, rt, mk(__uint_as_float(pc.x), __uint_as_float(pc.y), __uint_as_float(pc.z)),
-                            __uint_as_float(pc.w & ~RTW_LEAF_BIT), pi, closest, hit);
-                pend = false;
-                blocked = false;
-            }
-        }
-    }
-    t_out = closest;
-    return hit_with_order(hit, oct);
-}
-
 // `base`: L.cnodes, or their copy in LDS
 template <bool COUNT>
 __device__ __forceinline__ int traverse_compact(const rtw_launch& L, const uint4* base, const Ray& r, float& t_out,
@@ -748,7 +688,6 @@ __device__ __forceinline__ int traverse_compact(const rtw_launch& L, const uint4
                 (oct & 2u) ? -__builtin_fabsf(rt.inv.y) : __builtin_fabsf(rt.inv.y),
                 (oct & 4u) ? -__builtin_fabsf(rt.inv.z) : __builtin_fabsf(rt.inv.z));
     rt.oinv = mk(-(r.o.x * rt.inv.x), -(r.o.y * rt.inv.y), -(r.o.z * rt.inv.z));
-    if (L.walk_spec) return traverse_compact_spec<COUNT>(L, cn, r, rt, oct, t_out, cnt);
     float closest = kInf;
     int hit = -1;
     uint32_t i = 0;

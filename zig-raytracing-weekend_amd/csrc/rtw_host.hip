@@ -364,8 +364,6 @@ int rtw_scene_create(const rtw_scene_desc* d, int device, rtw_ctx** out) {
     // (the ray/hit hand-off through HBM disappears), tail on the LDS stage
     L.wf_fuse = 3;
     if (const char* fu = std::getenv("RTW_WF_FUSE")) L.wf_fuse = (uint32_t)std::atoi(fu);
-    L.walk_spec = 0;
-    if (const char* sp = std::getenv("RTW_WALK_SPEC")) L.walk_spec = (uint32_t)std::atoi(sp);
     // SAH trees: FMA slab test on the padded boxes + leaf postponement (both only
     // enlarge the set of visited nodes; reference trees keep the exact aabb.zig walk)
     const bool sah = ctx->box_pad > 0;
