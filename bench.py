@@ -27,7 +27,7 @@ sys.path.insert(0, REPO)
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 NODE_BYTES = 32                # one BVH node / leaf record (rtw_layout.h)
-ROWS_PER_BLOCK = 16
+ROWS_PER_BLOCK = 8   # row blocks interleaved over ranks: C2 at 8 GPUs 6.97x predicted (16: 6.87x; tools/shard_sim.py)
 
 
 def parse():
