@@ -240,3 +240,35 @@ def test_crops_fixture_reproducible(oracle, earth_rgba):
                                   threads=os.cpu_count() or 1)
         assert np.array_equal(acc, fx[name]), name
         assert np.isfinite(acc).all()
+
+
+def test_perlin_interp_folded_weights_bit_identical():
+    """The device's perlin_noise folds perlin_interp's weights i*uu + (1-i)*(1-uu)
+    (perlin.zig:42-50) to (1-uu) / uu for i = 0 / 1: bit-identical for uu in [0, 1]
+    (every fp32 operation below is correctly rounded in numpy as on the GPU)."""
+    rng = np.random.default_rng(7)
+    n = 200_000
+    f = np.float32
+    u, v, w = (rng.random(n, dtype=np.float32) for _ in range(3))
+    u[:64] = 0.0
+    v[64:128] = np.nextafter(f(1), f(0))
+    c = rng.standard_normal((2, 2, 2, 3, n)).astype(np.float32)
+    one, two, three = f(1), f(2), f(3)
+    uu, vv, ww = (x * x * (three - two * x) for x in (u, v, w))
+    ref = np.zeros(n, np.float32)
+    fold = np.zeros(n, np.float32)
+    for i in (0, 1):
+        for j in (0, 1):
+            for k in (0, 1):
+                fi, fj, fk = f(i), f(j), f(k)
+                wv = (u - fi, v - fj, w - fk)
+                d = (c[i, j, k, 0] * wv[0] + c[i, j, k, 1] * wv[1]) + c[i, j, k, 2] * wv[2]
+                ref += (fi * uu + (one - fi) * (one - uu)) * (fj * vv + (one - fj) * (one - vv)) * \
+                       (fk * ww + (one - fk) * (one - ww)) * d
+                wx = uu if i else one - uu
+                wy = vv if j else one - vv
+                wz = ww if k else one - ww
+                wv2 = (u - one if i else u, v - one if j else v, w - one if k else w)
+                d2 = (c[i, j, k, 0] * wv2[0] + c[i, j, k, 1] * wv2[1]) + c[i, j, k, 2] * wv2[2]
+                fold += wx * wy * wz * d2
+    assert np.array_equal(ref.view(np.uint32), fold.view(np.uint32))

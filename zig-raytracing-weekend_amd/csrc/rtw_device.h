@@ -179,6 +179,15 @@ __device__ float perlin_noise(const float4* tab, f3 p) {  // perlin.zig:117-162 
     float uu = u * u * (3 - 2 * u);
     float vv = v * v * (3 - 2 * v);
     float ww = w * w * (3 - 2 * w);
+    // perlin_interp's weights i*uu + (1-i)*(1-uu) for i in {0, 1}: with uu, vv, ww finite in
+    // [0, 1] (u in [0, 1)), 0*uu = +0 and 1*x = x exactly, and +0 + x = x for x >= 0, so the
+    // weight IS (1 - uu) for i = 0 and uu for i = 1, bit for bit: the folded form below does
+    // the same rounded operations as perlin.zig:42-50 without the multiplications by 0 and 1
+    // the compiler must keep (it cannot assume uu finite).
+    const float wx[2] = {1 - uu, uu}, wy[2] = {1 - vv, vv}, wz[2] = {1 - ww, ww};
+    const uint32_t px[2] = {perm[i & 255], perm[(i + 1) & 255]};
+    const uint32_t py[2] = {perm[256 + (j & 255)], perm[256 + ((j + 1) & 255)]};
+    const uint32_t pz[2] = {perm[512 + (k & 255)], perm[512 + ((k + 1) & 255)]};
     float accum = 0;
 #pragma unroll
     for (int di = 0; di < 2; di++)
@@ -186,12 +195,11 @@ __device__ float perlin_noise(const float4* tab, f3 p) {  // perlin.zig:117-162 
         for (int dj = 0; dj < 2; dj++)
 #pragma unroll
             for (int dk = 0; dk < 2; dk++) {
-                uint32_t idx = perm[(i + di) & 255] ^ perm[256 + ((j + dj) & 255)] ^ perm[512 + ((k + dk) & 255)];
-                float4 c = tab[idx & 255];
-                const float i_f = (float)di, j_f = (float)dj, k_f = (float)dk;
-                f3 wv = mk(u - i_f, v - j_f, w - k_f);
-                accum += (i_f * uu + (1 - i_f) * (1 - uu)) * (j_f * vv + (1 - j_f) * (1 - vv)) *
-                         (k_f * ww + (1 - k_f) * (1 - ww)) * dot(mk(c.x, c.y, c.z), wv);
+                const uint32_t idx = px[di] ^ py[dj] ^ pz[dk];
+                const float4 c = tab[idx & 255];
+                // (u - i, v - j, w - k): u - 0 = u exactly
+                const f3 wv = mk(di ? u - 1.0f : u, dj ? v - 1.0f : v, dk ? w - 1.0f : w);
+                accum += wx[di] * wy[dj] * wz[dk] * dot(mk(c.x, c.y, c.z), wv);
             }
     return accum;
 }
