@@ -364,6 +364,9 @@ int rtw_scene_create(const rtw_scene_desc* d, int device, rtw_ctx** out) {
     // (the ray/hit hand-off through HBM disappears), tail on the LDS stage
     L.wf_fuse = 3;
     if (const char* fu = std::getenv("RTW_WF_FUSE")) L.wf_fuse = (uint32_t)std::atoi(fu);
+    // Perlin tables (7 KiB each) staged in LDS by the fused step when at most 4 (noise scenes)
+    L.perlin_lds = (ctx->feat & RTW_F_NOISE) && d->n_perlins <= 4 ? 1u : 0u;
+    if (const char* pl = std::getenv("RTW_PERLIN_LDS")) L.perlin_lds = L.perlin_lds && std::atoi(pl) != 0;
     // SAH trees: FMA slab test on the padded boxes + leaf postponement (both only
     // enlarge the set of visited nodes; reference trees keep the exact aabb.zig walk)
     const bool sah = ctx->box_pad > 0;

@@ -68,6 +68,7 @@ struct rtw_launch {
     uint32_t wf_clds;            // wavefront trace: stage the compact nodes (all orders) in LDS when they fit
     uint32_t wf_fuse;            // with the compact LDS stage: one gen+trace+shade kernel per iteration,
                                  // bit 1: the tail walks the LDS stage too
+    uint32_t perlin_lds;         // fused step with the node array in LDS: Perlin tables staged in LDS too
 };
 
 #define RTW_TILE_W 16

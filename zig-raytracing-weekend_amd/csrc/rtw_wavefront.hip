@@ -448,6 +448,9 @@ __global__ __launch_bounds__(1024) void wf_tail_clds(rtw_launch L, rtw_wf W, uin
     wf_tail_body<FEAT, true>(L, W, it, wf_clds);
 }
 
+// dynamic LDS of the fused kernels: tree stage + 64 u32 of coop_reject scratch per wave
+#define RTW_WF_COOP_LDS(threads) ((threads) / 64u * 256u)
+
 // Where the fused step's walk reads the tree:
 //   WALK_CLDS   the compact nodes of every octant copy staged in LDS (small static sphere SAH trees, C2)
 //   WALK_LDS    the 32-B node array of one ordering staged in LDS (small object scenes: Cornell)
@@ -602,6 +605,18 @@ __global__ __launch_bounds__(256) void wf_step(rtw_launch L, rtw_wf W, uint32_t 
     uint32_t* coop = reinterpret_cast<uint32_t*>(wf_lds_nodes + n4) + 64u * (threadIdx.x >> 6);
     if constexpr (LDS) {
         for (uint32_t k = threadIdx.x; k < n4; k += 256u) wf_lds_nodes[k] = L.nodes[k];
+        if constexpr ((FEAT & RTW_F_NOISE) != 0) {
+            if (L.perlin_lds) {  // the Perlin tables after the coop scratch: noise gathers from LDS
+                float4* pl = wf_lds_nodes + n4 + RTW_WF_COOP_LDS(256u) / 16u;
+                const uint32_t np4 = L.n_perlin * (RTW_PERLIN_BYTES / 16u);
+                for (uint32_t k = threadIdx.x; k < np4; k += 256u) pl[k] = L.perlin[k];
+                __syncthreads();
+                rtw_launch Lp = L;
+                Lp.perlin = pl;
+                wf_step_body<FEAT, WALK_LDS>(Lp, W, it, wf_lds_nodes, coop);
+                return;
+            }
+        }
         __syncthreads();
         wf_step_body<FEAT, WALK_LDS>(L, W, it, wf_lds_nodes, coop);
     } else {
@@ -676,12 +691,13 @@ const WfGrids<FEAT>& wf_grids(int n_cu) {
 //   lds  > 0: the 32-B node array in LDS (wf_step<FEAT, true>)
 //   else    : the tree through L1/L2 (wf_step<FEAT, false>)
 // dynamic LDS of the fused kernels: tree stage + 64 u32 of coop_reject scratch per wave
-#define RTW_WF_COOP_LDS(threads) ((threads) / 64u * 256u)
 
 template <uint32_t FEAT>
 void wf_run_fused(const rtw_launch& L, const rtw_wf& W, hipStream_t st, int n_cu, size_t clds, size_t lds,
                   rtw_timer* T) {
-    const size_t cdyn = clds + RTW_WF_COOP_LDS(1024), ldyn = lds + RTW_WF_COOP_LDS(256), gdyn = RTW_WF_COOP_LDS(256);
+    const size_t cdyn = clds + RTW_WF_COOP_LDS(1024),
+                 ldyn = lds + RTW_WF_COOP_LDS(256) + (L.perlin_lds ? (size_t)L.n_perlin * RTW_PERLIN_BYTES : 0),
+                 gdyn = RTW_WF_COOP_LDS(256);
     static uint32_t cgrid[2] = {0, 0}, tgrid[2] = {0, 0}, lgrid[2] = {0, 0}, ggrid = 0;
     uint32_t grid = 0;
     if constexpr ((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING)) == 0) {
@@ -694,9 +710,9 @@ void wf_run_fused(const rtw_launch& L, const rtw_wf& W, hipStream_t st, int n_cu
     if (clds) {
         grid = cgrid[0];
     } else if (lds) {
-        if (lgrid[1] != lds) {
+        if (lgrid[1] != ldyn) {
             lgrid[0] = wf_grid(wf_step<FEAT, true>, n_cu, ldyn);
-            lgrid[1] = (uint32_t)lds;
+            lgrid[1] = (uint32_t)ldyn;
         }
         grid = lgrid[0];
     } else {
