@@ -365,7 +365,8 @@ __global__ __launch_bounds__(256) void wf_shade(rtw_launch L, rtw_wf W, uint32_t
 // completion; a lane whose path ends takes the wave's next path at once.
 // CLDS: the walk reads the compact nodes staged in LDS (`lds`) instead of L1/L2.
 template <uint32_t FEAT, bool CLDS>
-__device__ __forceinline__ void wf_tail_body(const rtw_launch& L, const rtw_wf& W, uint32_t it, const uint4* lds) {
+__device__ __forceinline__ void wf_tail_body(const rtw_launch& L, const rtw_wf& W, uint32_t it, const uint4* lds,
+                                             const float4* nodes = nullptr) {
     const uint32_t lane = __lane_id();
     const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     const rtw_wf_set& S = W.set[it & 1u];
@@ -405,7 +406,7 @@ __device__ __forceinline__ void wf_tail_body(const rtw_launch& L, const rtw_wf& 
             if constexpr (CLDS)
                 hit = L.counters ? traverse_compact<true>(L, lds, r, t, cnt) : traverse_compact<false>(L, lds, r, t, cnt);
             else
-                hit = traverse<FEAT>(L.nodes, L, r, t, cnt, rng.s);
+                hit = traverse<FEAT>(nodes ? nodes : L.nodes, L, r, t, cnt, rng.s);
             bool done = true;
             if (hit < 0) {
                 acc = acc + thr * background(L, r);
@@ -431,6 +432,16 @@ __device__ __forceinline__ void wf_tail_body(const rtw_launch& L, const rtw_wf& 
 template <uint32_t FEAT>
 __global__ __launch_bounds__(256) void wf_tail(rtw_launch L, rtw_wf W, uint32_t it) {
     wf_tail_body<FEAT, false>(L, W, it, nullptr);
+}
+
+// the 32-B node array(s) staged in LDS (small object scenes: Cornell)
+template <uint32_t FEAT>
+__global__ __launch_bounds__(256) void wf_tail_lds(rtw_launch L, rtw_wf W, uint32_t it) {
+    extern __shared__ float4 wf_tail_nodes[];
+    const uint32_t n4 = 2u * L.n_nodes * L.n_orders;
+    for (uint32_t k = threadIdx.x; k < n4; k += 256u) wf_tail_nodes[k] = L.nodes[k];
+    __syncthreads();
+    wf_tail_body<FEAT, false>(L, W, it, nullptr, wf_tail_nodes);
 }
 
 // every octant copy of the compact nodes into this block's LDS
@@ -746,6 +757,15 @@ void wf_run_fused(const rtw_launch& L, const rtw_wf& W, hipStream_t st, int n_cu
                 hipLaunchKernelGGL(wf_tail_clds<FEAT>, dim3(tgrid[0]), dim3(1024), clds, st, L, W, iters);
                 done = true;
             }
+        }
+        if (!done && lds && (L.wf_fuse & 2u)) {  // the node array in LDS for the tail too
+            static uint32_t tl[2] = {0, 0};
+            if (tl[1] != lds) {
+                tl[0] = wf_grid(wf_tail_lds<FEAT>, n_cu, lds);
+                tl[1] = (uint32_t)lds;
+            }
+            hipLaunchKernelGGL(wf_tail_lds<FEAT>, dim3(tl[0]), dim3(256), lds, st, L, W, iters);
+            done = true;
         }
         if (!done) hipLaunchKernelGGL(wf_tail<FEAT>, dim3(wf_grids<FEAT>(n_cu).tail), dim3(256), 0, st, L, W, iters);
         RTW_TIME_END(T)
