@@ -1091,7 +1091,7 @@ __device__ __forceinline__ Ray get_ray_wave(const rtw_launch& L, bool active, ui
     f3 origin = ld3(L.center);
     if (L.defocus_angle > 0) {
         float dsk[2] = {0.0f, 0.0f};
-        coop_reject<2>(active, rng, dsk, slot, L.coop != 0);
+        coop_reject<2>(active, rng, dsk, slot, (L.coop & 2u) != 0);
         origin = (origin + ld3(L.disk_u) * splat(dsk[0])) + ld3(L.disk_v) * splat(dsk[1]);
     }
     Ray r;

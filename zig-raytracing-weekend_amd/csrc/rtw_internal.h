@@ -57,7 +57,7 @@ struct rtw_launch {
     uint32_t waves;              // launch-bound variant (min waves per SIMD): 1, 6 or 8
     uint32_t tile_order;         // 1 = last tile row first (default), 0 = first row first
     uint32_t use_lds;            // 1 = stage the BVH in LDS when it fits (default), 0 = read nodes from L1/L2
-    uint32_t coop;               // 1 = wave-cooperative rejection sampling (default), 0 = per-lane loops
+    uint32_t coop;               // wave-cooperative rejection sampling: bit 0 unit sphere (shading), bit 1 disk (camera; v1: any bit)
     uint32_t fast_reject;        // 1 = exact sphere fast-reject filter (default), 0 = always the IEEE path
     uint32_t fast_box;           // 1 = FMA slab test on padded boxes (SAH trees only), 0 = aabb.zig arithmetic
     uint32_t postpone;           // 1 = postpone leaf tests until leaf_min/64 of the walking lanes hold one

@@ -551,7 +551,7 @@ __device__ __forceinline__ void wf_step_body(const rtw_launch& L, const rtw_wf& 
                 }
             }
             float uv3[3] = {0.0f, 0.0f, 0.0f};
-            coop_reject<3>(need_uv, rng, uv3, coop_slot, L.coop != 0);
+            coop_reject<3>(need_uv, rng, uv3, coop_slot, (L.coop & 1u) != 0);
             if (hitp) {
                 const f3 ruv = need_uv ? unit_vector(mk(uv3[0], uv3[1], uv3[2])) : mk(0, 0, 0);
                 f3 att;
