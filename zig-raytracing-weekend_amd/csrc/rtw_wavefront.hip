@@ -855,8 +855,13 @@ void wf_run(const rtw_launch& L, const rtw_wf& W, hipStream_t st, int n_cu, rtw_
     RTW_TIME_END(T)
 }
 
+// Object scenes without media, image / noise textures or motion (quads, instances, lights,
+// solid / checker textures: the Cornell box, HEAD's default scene) get their own
+// instantiation: without the unused code paths the fused step needs fewer registers.
+#define RTW_F_OBJECTS (RTW_F_GEOM | RTW_F_LIGHT | RTW_F_CHECKER)
 uint32_t wf_pick_feat(uint32_t f) {
     if ((f & ~RTW_F_CHECKER) == 0) return f ? RTW_F_CHECKER : 0u;
+    if ((f & RTW_F_GEOM) && (f & ~RTW_F_OBJECTS) == 0) return RTW_F_OBJECTS;
     return (f & (RTW_F_GEOM | RTW_F_MEDIUM)) ? RTW_F_ALL : RTW_F_SPHERES;
 }
 
@@ -868,6 +873,7 @@ void rtw_wavefront_batch(const rtw_launch& L, const rtw_wf& W, void* stream, int
     case 0u: wf_run<0u>(L, W, st, n_cu, T); break;
     case RTW_F_CHECKER: wf_run<RTW_F_CHECKER>(L, W, st, n_cu, T); break;
     case RTW_F_SPHERES: wf_run<RTW_F_SPHERES>(L, W, st, n_cu, T); break;
+    case RTW_F_OBJECTS: wf_run<RTW_F_OBJECTS>(L, W, st, n_cu, T); break;
     default: wf_run<RTW_F_ALL>(L, W, st, n_cu, T); break;
     }
 }
@@ -875,7 +881,8 @@ void rtw_wavefront_batch(const rtw_launch& L, const rtw_wf& W, void* stream, int
 uint32_t rtw_wavefront_max_waves(int n_cu) {
     uint32_t m = 0;
     for (uint32_t g : {wf_grids<0u>(n_cu).shade, wf_grids<RTW_F_CHECKER>(n_cu).shade,
-                       wf_grids<RTW_F_SPHERES>(n_cu).shade, wf_grids<RTW_F_ALL>(n_cu).shade})
+                       wf_grids<RTW_F_SPHERES>(n_cu).shade, wf_grids<RTW_F_OBJECTS>(n_cu).shade,
+                       wf_grids<RTW_F_ALL>(n_cu).shade})
         m = g > m ? g : m;
     return 4 * m;
 }
