@@ -726,10 +726,11 @@ __device__ __forceinline__ int traverse_compact(const rtw_launch& L, const uint4
 
 // mkey: the path's RNG state (keys ConstantMedium draws; unused without media).
 // `nodes` is the base of the node arrays (the octant copy is picked here).
-template <uint32_t FEAT>
+// COMPACT = false: walk `nodes` (e.g. their LDS stage) even where compact nodes exist.
+template <uint32_t FEAT, bool COMPACT = true>
 __device__ __forceinline__ int traverse(const float4* __restrict__ nodes, const rtw_launch& L, const Ray& r,
                                         float& t_out, Counters& cnt, uint64_t mkey = 0) {
-    if constexpr ((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING)) == 0) {
+    if constexpr (COMPACT && (FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING)) == 0) {
         if (L.cnodes && L.fast_box) {  // per-step counters only in counted passes
             return L.counters ? traverse_compact<true>(L, L.cnodes, r, t_out, cnt)
                               : traverse_compact<false>(L, L.cnodes, r, t_out, cnt);

@@ -406,7 +406,8 @@ __device__ __forceinline__ void wf_tail_body(const rtw_launch& L, const rtw_wf& 
             if constexpr (CLDS)
                 hit = L.counters ? traverse_compact<true>(L, lds, r, t, cnt) : traverse_compact<false>(L, lds, r, t, cnt);
             else
-                hit = traverse<FEAT>(nodes ? nodes : L.nodes, L, r, t, cnt, rng.s);
+                hit = nodes ? traverse<FEAT, false>(nodes, L, r, t, cnt, rng.s)  // the LDS stage
+                            : traverse<FEAT>(L.nodes, L, r, t, cnt, rng.s);
             bool done = true;
             if (hit < 0) {
                 acc = acc + thr * background(L, r);
@@ -475,7 +476,7 @@ __device__ __forceinline__ int wf_walk(const rtw_launch& L, const void* lds, con
         const uint4* cn = static_cast<const uint4*>(lds);
         return L.counters ? traverse_compact<true>(L, cn, r, t, cnt) : traverse_compact<false>(L, cn, r, t, cnt);
     } else if constexpr (WALK == WALK_LDS) {
-        return traverse<FEAT>(static_cast<const float4*>(lds), L, r, t, cnt, mkey);
+        return traverse<FEAT, false>(static_cast<const float4*>(lds), L, r, t, cnt, mkey);  // the LDS stage
     } else {
         return traverse<FEAT>(L.nodes, L, r, t, cnt, mkey);
     }
@@ -780,7 +781,9 @@ void wf_run(const rtw_launch& L, const rtw_wf& W, hipStream_t st, int n_cu, rtw_
     const WfGrids<FEAT>& g = wf_grids<FEAT>(n_cu);
     if ((L.wf_fuse & 1u) && !L.refill_min && !L.postpone) {
         size_t fclds = 0, flds = 0;
-        if constexpr ((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING)) == 0) {
+        // (textured scenes keep the 32-B node stage: it leaves LDS for the Perlin tables and the
+        // 1024-thread compact kernel would spill at its 128-VGPR cap -- C5 -20 % measured)
+        if constexpr ((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING | RTW_F_IMAGE | RTW_F_NOISE)) == 0) {
             const size_t c = (size_t)L.n_nodes * L.n_orders * 16u;
             if (L.cnodes && L.fast_box && L.wf_clds && c <= RTW_WF_CLDS_MAX) fclds = c;
         }
@@ -858,10 +861,16 @@ void wf_run(const rtw_launch& L, const rtw_wf& W, hipStream_t st, int n_cu, rtw_
 // Object scenes without media, image / noise textures or motion (quads, instances, lights,
 // solid / checker textures: the Cornell box, HEAD's default scene) get their own
 // instantiation: without the unused code paths the fused step needs fewer registers.
+// Likewise static, unlit sphere scenes with image / noise textures (BASELINE config 5) and
+// object scenes with media but no image / noise textures or motion (Cornell smoke).
 #define RTW_F_OBJECTS (RTW_F_GEOM | RTW_F_LIGHT | RTW_F_CHECKER)
+#define RTW_F_TEXTURED (RTW_F_CHECKER | RTW_F_IMAGE | RTW_F_NOISE)
+#define RTW_F_MEDIA (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_LIGHT | RTW_F_CHECKER)
 uint32_t wf_pick_feat(uint32_t f) {
     if ((f & ~RTW_F_CHECKER) == 0) return f ? RTW_F_CHECKER : 0u;
     if ((f & RTW_F_GEOM) && (f & ~RTW_F_OBJECTS) == 0) return RTW_F_OBJECTS;
+    if ((f & ~RTW_F_TEXTURED) == 0) return RTW_F_TEXTURED;
+    if ((f & RTW_F_MEDIUM) && (f & ~RTW_F_MEDIA) == 0) return RTW_F_MEDIA;
     return (f & (RTW_F_GEOM | RTW_F_MEDIUM)) ? RTW_F_ALL : RTW_F_SPHERES;
 }
 
@@ -874,6 +883,8 @@ void rtw_wavefront_batch(const rtw_launch& L, const rtw_wf& W, void* stream, int
     case RTW_F_CHECKER: wf_run<RTW_F_CHECKER>(L, W, st, n_cu, T); break;
     case RTW_F_SPHERES: wf_run<RTW_F_SPHERES>(L, W, st, n_cu, T); break;
     case RTW_F_OBJECTS: wf_run<RTW_F_OBJECTS>(L, W, st, n_cu, T); break;
+    case RTW_F_TEXTURED: wf_run<RTW_F_TEXTURED>(L, W, st, n_cu, T); break;
+    case RTW_F_MEDIA: wf_run<RTW_F_MEDIA>(L, W, st, n_cu, T); break;
     default: wf_run<RTW_F_ALL>(L, W, st, n_cu, T); break;
     }
 }
@@ -882,6 +893,7 @@ uint32_t rtw_wavefront_max_waves(int n_cu) {
     uint32_t m = 0;
     for (uint32_t g : {wf_grids<0u>(n_cu).shade, wf_grids<RTW_F_CHECKER>(n_cu).shade,
                        wf_grids<RTW_F_SPHERES>(n_cu).shade, wf_grids<RTW_F_OBJECTS>(n_cu).shade,
+                       wf_grids<RTW_F_TEXTURED>(n_cu).shade, wf_grids<RTW_F_MEDIA>(n_cu).shade,
                        wf_grids<RTW_F_ALL>(n_cu).shade})
         m = g > m ? g : m;
     return 4 * m;
