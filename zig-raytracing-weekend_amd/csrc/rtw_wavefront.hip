@@ -610,7 +610,7 @@ __global__ __launch_bounds__(1024) void wf_step_clds(rtw_launch L, rtw_wf W, uin
 
 // the 32-B node array (one ordering) in LDS, or the tree through L1/L2
 template <uint32_t FEAT, bool LDS>
-__global__ __launch_bounds__(256) void wf_step(rtw_launch L, rtw_wf W, uint32_t it) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void wf_step(rtw_launch L, rtw_wf W, uint32_t it) {
     wf_step_zero_next(W, it);
     extern __shared__ float4 wf_lds_nodes[];
     const uint32_t n4 = LDS ? 2u * L.n_nodes * L.n_orders : 0u;
