@@ -685,7 +685,7 @@ struct WfGrids {
 
 template <uint32_t FEAT>
 uint32_t wf_lds_grid(int n_cu, size_t lds) {
-    static uint32_t cache[RTW_WF_LDS_MAX / 512 + 1] = {0};
+    thread_local uint32_t cache[RTW_WF_LDS_MAX / 512 + 1] = {0};
     uint32_t& g = cache[lds / 512];
     if (!g) g = wf_grid(wf_trace<FEAT, true>, n_cu, lds);
     return g;
@@ -697,6 +697,7 @@ const WfGrids<FEAT>& wf_grids(int n_cu) {
     return g;
 }
 
+// (Grid sizes are cached per host thread: rtw_render may be called from several threads at once.)
 // Fused path (L.wf_fuse & 1): one wf_step* kernel per iteration, then the tail
 // (on the compact LDS stage when L.wf_fuse & 2) and the reduce.
 //   clds > 0: compact nodes of all orders in LDS (wf_step_clds, 1024 threads)
@@ -710,7 +711,7 @@ void wf_run_fused(const rtw_launch& L, const rtw_wf& W, hipStream_t st, int n_cu
     const size_t cdyn = clds + RTW_WF_COOP_LDS(1024),
                  ldyn = lds + RTW_WF_COOP_LDS(256) + (L.perlin_lds ? (size_t)L.n_perlin * RTW_PERLIN_BYTES : 0),
                  gdyn = RTW_WF_COOP_LDS(256);
-    static uint32_t cgrid[2] = {0, 0}, tgrid[2] = {0, 0}, lgrid[2] = {0, 0}, ggrid = 0;
+    thread_local uint32_t cgrid[2] = {0, 0}, tgrid[2] = {0, 0}, lgrid[2] = {0, 0}, ggrid = 0;
     uint32_t grid = 0;
     if constexpr ((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING)) == 0) {
         if (clds && cgrid[1] != clds) {
@@ -760,7 +761,7 @@ void wf_run_fused(const rtw_launch& L, const rtw_wf& W, hipStream_t st, int n_cu
             }
         }
         if (!done && lds && (L.wf_fuse & 2u)) {  // the node array in LDS for the tail too
-            static uint32_t tl[2] = {0, 0};
+            thread_local uint32_t tl[2] = {0, 0};
             if (tl[1] != lds) {
                 tl[0] = wf_grid(wf_tail_lds<FEAT>, n_cu, lds);
                 tl[1] = (uint32_t)lds;
@@ -808,7 +809,7 @@ void wf_run(const rtw_launch& L, const rtw_wf& W, hipStream_t st, int n_cu, rtw_
     // compact nodes of every octant copy in LDS (small static sphere trees)
     const size_t clds = (L.cnodes && L.fast_box && L.wf_clds && !L.refill_min && !L.postpone)
                             ? (size_t)L.n_nodes * L.n_orders * 16u : 0;
-    static uint32_t clds_grid_cache[2] = {0, 0};
+    thread_local uint32_t clds_grid_cache[2] = {0, 0};
     uint32_t clds_grid = 0;
     static const uint32_t clds_threads = [] {  // DIAGNOSTIC: RTW_CLDS_THREADS (occupancy of the LDS walk)
         const char* e = std::getenv("RTW_CLDS_THREADS");
