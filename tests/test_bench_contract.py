@@ -1,0 +1,48 @@
+"""The committed bench line (profiles/r1_c2_wavefront_bench.json, written by bench.py on
+an MI355X) carries every field of the driver's contract: the headline metric of
+BASELINE.json on config 2, the dominant kernel's roofline and the CPU baseline."""
+import json
+import os
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def load(name):
+    with open(os.path.join(REPO, "profiles", name)) as f:
+        return json.loads(f.read().strip().splitlines()[-1])
+
+
+def test_c2_bench_line_contract():
+    d = load("r1_c2_wavefront_bench.json")
+    base = json.load(open(os.path.join(REPO, "BASELINE.json")))
+    assert d["metric"] == base["metric"]
+    for k in ("value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
+        assert k in d, k
+    assert d["unit"] == "Msamples/s" and d["higher_is_better"] is True and d["n_gpus"] == 1
+    assert d["config"]["workload"] and (d["config"]["width"], d["config"]["height"], d["config"]["spp"]) == (1200, 800, 500)
+    # value = samples / wall time of the timed steps
+    assert abs(d["value"] - 1200 * 800 * 500 / (d["ms_per_step"] / 1e3) / 1e6) <= 0.01 * d["value"]
+    r = d["roofline"]
+    for k in ("bound", "achieved", "peak", "unit", "frac", "traffic"):
+        assert k in r, k
+    assert r["bound"] == "hbm" and r["unit"] == "GB/s" and r["peak"] == 8000.0
+    assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-3
+    assert r["traffic"] and r["traffic"] > 0
+    c = d["cpu_baseline"]
+    for k in ("value", "unit", "cores", "kind", "sample"):
+        assert k in c, k
+    assert c["kind"] in ("port", "reference") and c["cores"] >= 1 and c["value"] > 0
+
+
+def test_rocprof_summary_agrees_with_bench_events():
+    """profiles/r1_c2_wavefront_timed_summary.txt (rocprofv3 --kernel-trace --stats of the
+    bench command) and the bench's HIP-event average of the dominant kernel agree."""
+    d = load("r1_c2_wavefront_bench.json")
+    kernel = d["roofline"]["kernel"]
+    for line in open(os.path.join(REPO, "profiles", "r1_c2_wavefront_timed_summary.txt")):
+        if kernel + "<" in line:
+            mean_us = float(line.split()[-3])
+            assert abs(mean_us / 1e3 - d["roofline"]["avg_launch_ms"]) <= 0.05 * d["roofline"]["avg_launch_ms"]
+            return
+    raise AssertionError(f"{kernel} not in the rocprof summary")
