@@ -3,7 +3,7 @@
 For N in (1, 2, 4, 8) renders every rank's shard (rtw_render_rows_device, the
 call bench.py makes per rank) back to back on this GPU and reports the slowest
 rank's render time: the N-GPU step time minus the RCCL gather (C2: 15.4 MB,
-~1-2 ms over xGMI).  Usage: python tools/shard_sim.py [config] [spp] [rows_per_block]
+~1-2 ms over xGMI).  Usage: python tools/shard_sim.py [config] [spp] [rows_per_block] [ranks, e.g. 1,8]
 """
 import importlib
 import json
@@ -18,6 +18,7 @@ pkg = importlib.import_module("zig-raytracing-weekend_amd")
 cfg_name = sys.argv[1] if len(sys.argv) > 1 else "c2"
 spp_override = int(sys.argv[2]) if len(sys.argv) > 2 else 0
 rpb = int(sys.argv[3]) if len(sys.argv) > 3 else 16
+ns = [int(v) for v in sys.argv[4].split(",")] if len(sys.argv) > 4 else [1, 2, 4, 8]
 cfg = pkg.configs.CONFIGS[cfg_name]
 world = pkg.World(pkg.flatten(cfg.objects()))
 cam = cfg.camera()
@@ -29,7 +30,7 @@ W, H = cam.derived.image_width, cam.derived.image_height
 stream = torch.cuda.Stream()
 torch.cuda.set_stream(stream)
 base = None
-for n in (1, 2, 4, 8):
+for n in ns:
     times = []
     for r in range(n if n > 1 else 1):
         sh = pkg.distributed.ShardedRender(world, cam, r, n, rpb)
