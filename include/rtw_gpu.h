@@ -22,6 +22,12 @@
  * device buffers are passed as void*).  Every function returns an RTW_* status;
  * rtw_last_error() returns a thread-local message for the last failure.
  * No exceptions cross the ABI.  The library never frees caller memory.
+ *
+ * Threading: render calls on one rtw_ctx may come from several threads at once
+ * (the reference's 8 RenderThreads, src/main.zig:314-326): they are serialised
+ * per context, and a device-API call on another stream than the previous call
+ * waits for that call's work on the device.  rtw_scene_destroy must not race a
+ * render on the same context.
  */
 #ifndef RTW_GPU_H
 #define RTW_GPU_H

@@ -399,7 +399,9 @@ int rtw_scene_create(const rtw_scene_desc* d, int device, rtw_ctx** out) {
 void rtw_scene_destroy(rtw_ctx* ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
+    if (ctx->last_done) (void)hipEventSynchronize(ctx->last_done);  // a render left on a caller's stream
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->last_done) (void)hipEventDestroy(ctx->last_done);
     if (ctx->d_blob) (void)hipFree(ctx->d_blob);
     if (ctx->d_scratch) (void)hipFree(ctx->d_scratch);
     if (ctx->d_dbg) (void)hipFree(ctx->d_dbg);
@@ -614,6 +616,18 @@ void set_tiles(rtw_launch& L) {
     L.n_tiles = L.n_tiles_x * ((L.n_rows + RTW_TILE_H - 1) / RTW_TILE_H);
 }
 
+// Order this call's stream after the previous call's work on this context (another stream).
+int stream_enter(rtw_ctx* ctx, hipStream_t s) {
+    if (ctx->last_stream && ctx->last_stream != s) HIP_TRY(hipStreamWaitEvent(s, ctx->last_done, 0));
+    return RTW_OK;
+}
+int stream_leave(rtw_ctx* ctx, hipStream_t s) {
+    if (!ctx->last_done) HIP_TRY(hipEventCreateWithFlags(&ctx->last_done, hipEventDisableTiming));
+    HIP_TRY(hipEventRecord(ctx->last_done, s));
+    ctx->last_stream = s;
+    return RTW_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -626,10 +640,15 @@ int rtw_render(rtw_ctx* ctx, const rtw_camera* cam, uint32_t pix_begin, uint32_t
     if (pix_end > cam->size || pix_begin > pix_end) return fail(RTW_E_INVALID, "pixel range out of image");
     if (spp_begin > spp_end) return fail(RTW_E_INVALID, "bad sample range");
     if (pix_begin == pix_end || spp_begin == spp_end) return RTW_OK;
+    std::lock_guard<std::mutex> lock(ctx->mu);
     HIP_TRY(hipSetDevice(ctx->device));
+    if (int rc = stream_enter(ctx, ctx->stream)) return rc;
     const size_t bytes = (size_t)cam->size * 16;
     if (ctx->scratch_bytes < bytes) {
-        if (ctx->d_scratch) (void)hipFree(ctx->d_scratch);
+        if (ctx->d_scratch) {
+            HIP_TRY(hipStreamSynchronize(ctx->stream));
+            (void)hipFree(ctx->d_scratch);
+        }
         ctx->d_scratch = nullptr;
         ctx->scratch_bytes = 0;
         HIP_TRY(hipMalloc(&ctx->d_scratch, bytes));
@@ -653,6 +672,7 @@ int rtw_render(rtw_ctx* ctx, const rtw_camera* cam, uint32_t pix_begin, uint32_t
     hipError_t e = hipMemcpyAsync((char*)accum + o, (char*)ctx->d_scratch + o, nb, hipMemcpyDeviceToHost, ctx->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
     if (e != hipSuccess) return hip_fail(e, "rtw_render copy back");
+    ctx->last_stream = nullptr;  // synchronised: nothing of this context is in flight
     return rc;
 }
 
@@ -663,8 +683,10 @@ int rtw_render_device(rtw_ctx* ctx, const rtw_camera* cam, uint32_t pix_begin, u
     if (pix_end > cam->size || pix_begin > pix_end) return fail(RTW_E_INVALID, "pixel range out of image");
     if (spp_begin > spp_end) return fail(RTW_E_INVALID, "bad sample range");
     if (pix_begin == pix_end || spp_begin == spp_end) return RTW_OK;
+    std::lock_guard<std::mutex> lock(ctx->mu);
     HIP_TRY(hipSetDevice(ctx->device));
     hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+    if (int rc = stream_enter(ctx, s)) return rc;
     rtw_launch L = make_launch(ctx, cam, seed);
     L.accum = reinterpret_cast<float4*>(d_accum);
     L.pix_begin = pix_begin;
@@ -681,6 +703,7 @@ int rtw_render_device(rtw_ctx* ctx, const rtw_camera* cam, uint32_t pix_begin, u
     rtw_timer* tp = (opts && opts->timing) ? &T : nullptr;
     int rc = run_batches(ctx, L, spp_begin, spp_end, batch, s, false, nullptr, nullptr, nullptr, pix_end - pix_begin, tp);
     ctx->ev_pool.swap(T.pool);
+    if (int rl = stream_leave(ctx, s)) return rl;
     if (tp && rc == RTW_OK) rc = harvest_timing(ctx, T, opts->timing);
     if (rc) return rc;
     if (!(opts && (opts->flags & RTW_RENDER_NO_SYNC))) HIP_TRY(hipStreamSynchronize(s));
@@ -707,8 +730,10 @@ int rtw_render_rows_device(rtw_ctx* ctx, const rtw_camera* cam, uint32_t rpb, ui
     if (spp_begin > spp_end) return fail(RTW_E_INVALID, "bad sample range");
     const uint32_t rows = rtw_shard_rows(cam->image_height, rpb, n_shards, shard);
     if (rows == 0 || spp_begin == spp_end) return RTW_OK;
+    std::lock_guard<std::mutex> lock(ctx->mu);
     HIP_TRY(hipSetDevice(ctx->device));
     hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+    if (int rc = stream_enter(ctx, s)) return rc;
     rtw_launch L = make_launch(ctx, cam, seed);
     L.accum = reinterpret_cast<float4*>(d_tile);
     L.row0 = 0;
@@ -731,6 +756,7 @@ int rtw_render_rows_device(rtw_ctx* ctx, const rtw_camera* cam, uint32_t rpb, ui
     int rc = run_batches(ctx, L, spp_begin, spp_end, batch, s, false, nullptr, nullptr, nullptr,
                          (uint64_t)rows * cam->image_width, tp);
     ctx->ev_pool.swap(T.pool);
+    if (int rl = stream_leave(ctx, s)) return rl;
     if (tp && rc == RTW_OK) rc = harvest_timing(ctx, T, opts->timing);
     if (rc) return rc;
     if (!(opts && (opts->flags & RTW_RENDER_NO_SYNC))) HIP_TRY(hipStreamSynchronize(s));
@@ -756,7 +782,10 @@ int rtw_texture_from_accum(const float* accum, uint32_t n, uint8_t* out) {
 
 int rtw_debug_rng(rtw_ctx* ctx, uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t n, float* out) {
     if (!ctx || !out || n > 64) return fail(RTW_E_INVALID, "bad debug_rng args (n <= 64)");
+    std::lock_guard<std::mutex> lock(ctx->mu);
     HIP_TRY(hipSetDevice(ctx->device));
+    if (int rc = stream_enter(ctx, ctx->stream)) return rc;
+    ctx->last_stream = nullptr;  // synchronised below
     rtw_launch_debug_rng(seed, pixel, sample, n, ctx->d_dbg, ctx->stream);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipMemcpyAsync(out, ctx->d_dbg, n * sizeof(float), hipMemcpyDeviceToHost, ctx->stream));
@@ -769,7 +798,10 @@ int rtw_debug_sample(rtw_ctx* ctx, const rtw_camera* cam, uint64_t seed, uint32_
     if (!ctx || !out) return fail(RTW_E_INVALID, "null args");
     if (int rc = validate_cam(cam)) return rc;
     if (pixel >= cam->size) return fail(RTW_E_INVALID, "pixel out of range");
+    std::lock_guard<std::mutex> lock(ctx->mu);
     HIP_TRY(hipSetDevice(ctx->device));
+    if (int rc = stream_enter(ctx, ctx->stream)) return rc;
+    ctx->last_stream = nullptr;  // synchronised below
     rtw_launch L = make_launch(ctx, cam, seed);
     rtw_launch_debug_sample(L, pixel, sample, ctx->d_dbg, ctx->stream);
     HIP_TRY(hipGetLastError());

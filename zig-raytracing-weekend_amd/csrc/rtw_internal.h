@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <mutex>
 #include <vector>
 
 #include "rtw_layout.h"
@@ -188,4 +189,10 @@ struct rtw_ctx {
     uint64_t scene_hash = 0;       // FNV-1a 64 of the uploaded scene image
     float box_pad = 0;             // absolute pad baked into the inner boxes (SAH trees), 0 = none
     float extent = 0;              // max |coordinate| over the scene's boxes
+    // Concurrent callers (the reference's 8 RenderThreads call Camera.render at once, main.zig:314-326):
+    // one render call at a time per context -- the wavefront state and staging buffers are per context --
+    // and a call on another stream than the previous one waits for that call's work on the device.
+    std::mutex mu;
+    hipEvent_t last_done = nullptr;
+    hipStream_t last_stream = nullptr;
 };
