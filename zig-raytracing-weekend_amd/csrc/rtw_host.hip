@@ -367,6 +367,11 @@ int rtw_scene_create(const rtw_scene_desc* d, int device, rtw_ctx** out) {
     // Perlin tables (7 KiB each) staged in LDS by the fused step when at most 4 (noise scenes)
     L.perlin_lds = (ctx->feat & RTW_F_NOISE) && d->n_perlins <= 4 ? 1u : 0u;
     if (const char* pl = std::getenv("RTW_PERLIN_LDS")) L.perlin_lds = L.perlin_lds && std::atoi(pl) != 0;
+    // quads, instance member lists and instances of small object scenes (Cornell: ~2 KiB) staged in LDS
+    // with the node array: the member loop's loads stop waiting on L1
+    const size_t geom_bytes = (size_t)(o_med - o_quad);
+    L.geom_lds = (ctx->feat & RTW_F_GEOM) && geom_bytes <= 16384 ? (uint32_t)geom_bytes : 0u;
+    if (const char* gl = std::getenv("RTW_GEOM_LDS")) L.geom_lds = std::atoi(gl) != 0 ? L.geom_lds : 0u;
     // SAH trees: FMA slab test on the padded boxes + leaf postponement (both only
     // enlarge the set of visited nodes; reference trees keep the exact aabb.zig walk)
     const bool sah = ctx->box_pad > 0;

@@ -164,6 +164,20 @@ __global__ __launch_bounds__(256) void wf_gen(rtw_launch L, rtw_wf W) {
     }
 }
 
+// L.geom_lds: copy the scene's quads | members | instances (one contiguous range of the scene
+// blob, 16-B aligned) to `lds` and point a copy of L at it (the caller synchronises)
+__device__ __forceinline__ rtw_launch stage_geom(const rtw_launch& L, float4* lds) {
+    const float4* src = reinterpret_cast<const float4*>(L.quads);
+    for (uint32_t k = threadIdx.x; k < L.geom_lds / 16u; k += blockDim.x) lds[k] = src[k];
+    rtw_launch G = L;
+    const char* base = reinterpret_cast<const char*>(L.quads);
+    char* lb = reinterpret_cast<char*>(lds);
+    G.quads = reinterpret_cast<const rtw_dev_quad*>(lb);
+    G.members = reinterpret_cast<const uint32_t*>(lb + (reinterpret_cast<const char*>(L.members) - base));
+    G.insts = reinterpret_cast<const rtw_dev_instance*>(lb + (reinterpret_cast<const char*>(L.insts) - base));
+    return G;
+}
+
 // trace: closest hit per ray of the input set (no shading state in registers)
 template <uint32_t FEAT, bool LDS>
 __global__ __launch_bounds__(256) void wf_trace(rtw_launch L, rtw_wf W, uint32_t it) {
@@ -177,6 +191,10 @@ __global__ __launch_bounds__(256) void wf_trace(rtw_launch L, rtw_wf W, uint32_t
         extern __shared__ float4 wf_lds_nodes[];
         const uint32_t n4 = 2u * L.n_nodes * L.n_orders;
         for (uint32_t k = threadIdx.x; k < n4; k += 256u) wf_lds_nodes[k] = L.nodes[k];
+        rtw_launch G = L;
+        if constexpr ((FEAT & RTW_F_GEOM) != 0) {
+            if (L.geom_lds) G = stage_geom(L, wf_lds_nodes + n4);
+        }
         __syncthreads();
         for (WfIter e(W, it); e.more(); e.next()) {
             uint32_t slot;
@@ -185,7 +203,7 @@ __global__ __launch_bounds__(256) void wf_trace(rtw_launch L, rtw_wf W, uint32_t
                 const Ray r = wf_load_ray(S, slot, depth);
                 if (depth) {
                     float t;
-                    const int h = traverse<FEAT>(wf_lds_nodes, L, r, t, cnt, wf_mkey<FEAT>(S, slot));
+                    const int h = traverse<FEAT>(wf_lds_nodes, G, r, t, cnt, wf_mkey<FEAT>(S, slot));
                     W.hit[slot] = make_float2(t, __int_as_float(h));
                     cnt.rays++;
                 }
@@ -435,12 +453,20 @@ __global__ __launch_bounds__(256) void wf_tail(rtw_launch L, rtw_wf W, uint32_t 
     wf_tail_body<FEAT, false>(L, W, it, nullptr);
 }
 
-// the 32-B node array(s) staged in LDS (small object scenes: Cornell)
+// the 32-B node array(s) staged in LDS (small object scenes: Cornell), + L.geom_lds bytes of geometry
 template <uint32_t FEAT>
 __global__ __launch_bounds__(256) void wf_tail_lds(rtw_launch L, rtw_wf W, uint32_t it) {
     extern __shared__ float4 wf_tail_nodes[];
     const uint32_t n4 = 2u * L.n_nodes * L.n_orders;
     for (uint32_t k = threadIdx.x; k < n4; k += 256u) wf_tail_nodes[k] = L.nodes[k];
+    if constexpr ((FEAT & RTW_F_GEOM) != 0) {
+        if (L.geom_lds) {
+            const rtw_launch G = stage_geom(L, wf_tail_nodes + n4);
+            __syncthreads();
+            wf_tail_body<FEAT, false>(G, W, it, nullptr, wf_tail_nodes);
+            return;
+        }
+    }
     __syncthreads();
     wf_tail_body<FEAT, false>(L, W, it, nullptr, wf_tail_nodes);
 }
@@ -617,14 +643,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
     uint32_t* coop = reinterpret_cast<uint32_t*>(wf_lds_nodes + n4) + 64u * (threadIdx.x >> 6);
     if constexpr (LDS) {
         for (uint32_t k = threadIdx.x; k < n4; k += 256u) wf_lds_nodes[k] = L.nodes[k];
-        if constexpr ((FEAT & RTW_F_NOISE) != 0) {
-            if (L.perlin_lds) {  // the Perlin tables after the coop scratch: noise gathers from LDS
-                float4* pl = wf_lds_nodes + n4 + RTW_WF_COOP_LDS(256u) / 16u;
-                const uint32_t np4 = L.n_perlin * (RTW_PERLIN_BYTES / 16u);
-                for (uint32_t k = threadIdx.x; k < np4; k += 256u) pl[k] = L.perlin[k];
-                __syncthreads();
+        if constexpr ((FEAT & (RTW_F_NOISE | RTW_F_GEOM)) != 0) {
+            if (L.perlin_lds || L.geom_lds) {  // after the coop scratch: Perlin tables, then geometry
+                float4* extra = wf_lds_nodes + n4 + RTW_WF_COOP_LDS(256u) / 16u;
                 rtw_launch Lp = L;
-                Lp.perlin = pl;
+                if ((FEAT & RTW_F_NOISE) != 0 && L.perlin_lds) {  // noise gathers from LDS
+                    const uint32_t np4 = L.n_perlin * (RTW_PERLIN_BYTES / 16u);
+                    for (uint32_t k = threadIdx.x; k < np4; k += 256u) extra[k] = L.perlin[k];
+                    Lp.perlin = extra;
+                    extra += np4;
+                }
+                if ((FEAT & RTW_F_GEOM) != 0 && L.geom_lds) Lp = stage_geom(Lp, extra);
+                __syncthreads();
                 wf_step_body<FEAT, WALK_LDS>(Lp, W, it, wf_lds_nodes, coop);
                 return;
             }
@@ -685,7 +715,7 @@ struct WfGrids {
 
 template <uint32_t FEAT>
 uint32_t wf_lds_grid(int n_cu, size_t lds) {
-    thread_local uint32_t cache[RTW_WF_LDS_MAX / 512 + 1] = {0};
+    thread_local uint32_t cache[(RTW_WF_LDS_MAX + 16384) / 512 + 1] = {0};  // + geometry (L.geom_lds)
     uint32_t& g = cache[lds / 512];
     if (!g) g = wf_grid(wf_trace<FEAT, true>, n_cu, lds);
     return g;
@@ -709,7 +739,9 @@ template <uint32_t FEAT>
 void wf_run_fused(const rtw_launch& L, const rtw_wf& W, hipStream_t st, int n_cu, size_t clds, size_t lds,
                   rtw_timer* T) {
     const size_t cdyn = clds + RTW_WF_COOP_LDS(1024),
-                 ldyn = lds + RTW_WF_COOP_LDS(256) + (L.perlin_lds ? (size_t)L.n_perlin * RTW_PERLIN_BYTES : 0),
+                 ldyn = lds + RTW_WF_COOP_LDS(256) + (L.perlin_lds ? (size_t)L.n_perlin * RTW_PERLIN_BYTES : 0) +
+                        ((FEAT & RTW_F_GEOM) ? L.geom_lds : 0u),
+                 tdyn = lds + ((FEAT & RTW_F_GEOM) ? L.geom_lds : 0u),
                  gdyn = RTW_WF_COOP_LDS(256);
     thread_local uint32_t cgrid[2] = {0, 0}, tgrid[2] = {0, 0}, lgrid[2] = {0, 0}, ggrid = 0;
     uint32_t grid = 0;
@@ -762,11 +794,11 @@ void wf_run_fused(const rtw_launch& L, const rtw_wf& W, hipStream_t st, int n_cu
         }
         if (!done && lds && (L.wf_fuse & 2u)) {  // the node array in LDS for the tail too
             thread_local uint32_t tl[2] = {0, 0};
-            if (tl[1] != lds) {
-                tl[0] = wf_grid(wf_tail_lds<FEAT>, n_cu, lds);
-                tl[1] = (uint32_t)lds;
+            if (tl[1] != tdyn) {
+                tl[0] = wf_grid(wf_tail_lds<FEAT>, n_cu, tdyn);
+                tl[1] = (uint32_t)tdyn;
             }
-            hipLaunchKernelGGL(wf_tail_lds<FEAT>, dim3(tl[0]), dim3(256), lds, st, L, W, iters);
+            hipLaunchKernelGGL(wf_tail_lds<FEAT>, dim3(tl[0]), dim3(256), tdyn, st, L, W, iters);
             done = true;
         }
         if (!done) hipLaunchKernelGGL(wf_tail<FEAT>, dim3(wf_grids<FEAT>(n_cu).tail), dim3(256), 0, st, L, W, iters);
@@ -805,7 +837,8 @@ void wf_run(const rtw_launch& L, const rtw_wf& W, hipStream_t st, int n_cu, rtw_
     const size_t lds_need = (size_t)L.n_nodes * L.n_orders * 32u;
     const size_t lds = (L.wf_lds && !L.refill_min && !L.postpone && lds_need <= RTW_WF_LDS_MAX)
                            ? (lds_need + 511u) / 512u * 512u : 0;
-    const uint32_t lds_grid = lds ? wf_lds_grid<FEAT>(n_cu, lds) : 0;
+    const size_t tlds = lds ? lds + ((FEAT & RTW_F_GEOM) ? L.geom_lds : 0u) : 0;  // + quads/members/instances
+    const uint32_t lds_grid = lds ? wf_lds_grid<FEAT>(n_cu, tlds) : 0;
     // compact nodes of every octant copy in LDS (small static sphere trees)
     const size_t clds = (L.cnodes && L.fast_box && L.wf_clds && !L.refill_min && !L.postpone)
                             ? (size_t)L.n_nodes * L.n_orders * 16u : 0;
@@ -838,7 +871,7 @@ void wf_run(const rtw_launch& L, const rtw_wf& W, hipStream_t st, int n_cu, rtw_
             }
         }
         if (lds)
-            hipLaunchKernelGGL((wf_trace<FEAT, true>), dim3(lds_grid), dim3(256), lds, st, L, W, it);
+            hipLaunchKernelGGL((wf_trace<FEAT, true>), dim3(lds_grid), dim3(256), tlds, st, L, W, it);
         else if (occ_pad)  // DIAGNOSTIC: occupancy sweep (dynamic LDS limits resident blocks)
             hipLaunchKernelGGL((wf_trace<FEAT, false>), dim3(pad_grid), dim3(256), occ_pad, st, L, W, it);
         else
