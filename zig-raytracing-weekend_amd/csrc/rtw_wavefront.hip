@@ -884,7 +884,16 @@ void wf_run(const rtw_launch& L, const rtw_wf& W, hipStream_t st, int n_cu, rtw_
     }
     if (iters < L.max_depth) {
         RTW_TIME_BEGIN(T, RTW_K_TAIL)
-        hipLaunchKernelGGL(wf_tail<FEAT>, dim3(g.tail), dim3(256), 0, st, L, W, iters);
+        if (lds && (L.wf_fuse & 2u)) {  // the node array (+ geometry) in LDS for the tail (smoke +5 %)
+            thread_local uint32_t tl[2] = {0, 0};
+            if (tl[1] != tlds) {
+                tl[0] = wf_grid(wf_tail_lds<FEAT>, n_cu, tlds);
+                tl[1] = (uint32_t)tlds;
+            }
+            hipLaunchKernelGGL(wf_tail_lds<FEAT>, dim3(tl[0]), dim3(256), tlds, st, L, W, iters);
+        } else {
+            hipLaunchKernelGGL(wf_tail<FEAT>, dim3(g.tail), dim3(256), 0, st, L, W, iters);
+        }
         RTW_TIME_END(T)
     }
     RTW_TIME_BEGIN(T, RTW_K_REDUCE)
