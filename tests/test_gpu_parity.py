@@ -318,7 +318,8 @@ def test_v1_knobs_invariant(rtw, book1, knob, monkeypatch):
                                   ("RTW_REFILL_MIN", "16"), ("RTW_FASTBOX", "0"), ("RTW_WF_LDS", "0"),
                                   ("RTW_SAH_LEAF", "4"), ("RTW_COMPACT", "0"),
                                   ("RTW_WF_CLDS", "0"), ("RTW_WF_FUSE", "0"), ("RTW_WF_FUSE", "1"),
-                                  ("RTW_COOP", "0"), ("RTW_COOP", "1"), ("RTW_COOP", "2")])
+                                  ("RTW_COOP", "0"), ("RTW_COOP", "1"), ("RTW_COOP", "2"),
+                                  ("RTW_MAT_LDS", "0")])
 def test_wavefront_knobs_invariant(rtw, book1, knob, monkeypatch):
     """Wavefront knobs (bounces before the tail kernel, batch size -> many batches,
     per-lane refill in trace, FMA vs reference slab test, LDS-staged nodes, SAH

@@ -70,6 +70,7 @@ struct rtw_launch {
     uint32_t wf_fuse;            // with the compact LDS stage: one gen+trace+shade kernel per iteration,
                                  // bit 1: the tail walks the LDS stage too
     uint32_t perlin_lds;         // fused step with the node array in LDS: Perlin tables staged in LDS too
+    uint32_t mat_lds;            // compact-LDS fused step: bytes of the material array staged in LDS (0: off)
     uint32_t geom_lds;           // node-LDS step/tail: bytes of quads | members | instances (contiguous in the
                                  // scene blob) staged in LDS too; 0 = read through L1/L2
 };

@@ -631,6 +631,16 @@ __global__ __launch_bounds__(1024) void wf_step_clds(rtw_launch L, rtw_wf W, uin
     stage_clds(L, wf_clds);
     // per-wave coop_reject scratch after the nodes (the host adds RTW_WF_COOP_LDS(1024) bytes)
     uint32_t* coop = reinterpret_cast<uint32_t*>(wf_clds + L.n_nodes * L.n_orders) + 64u * (threadIdx.x >> 6);
+    if (L.mat_lds) {  // the materials after the coop scratch (the host checked that they fit)
+        uint4* ml = wf_clds + L.n_nodes * L.n_orders + RTW_WF_COOP_LDS(1024u) / 16u;
+        const uint4* src = reinterpret_cast<const uint4*>(L.mats);
+        for (uint32_t k = threadIdx.x; k < L.mat_lds / 16u; k += 1024u) ml[k] = src[k];
+        __syncthreads();
+        rtw_launch Lm = L;
+        Lm.mats = reinterpret_cast<const rtw_dev_material*>(ml);
+        wf_step_body<FEAT, WALK_CLDS>(Lm, W, it, wf_clds, coop);
+        return;
+    }
     wf_step_body<FEAT, WALK_CLDS>(L, W, it, wf_clds, coop);
 }
 
@@ -738,7 +748,8 @@ const WfGrids<FEAT>& wf_grids(int n_cu) {
 template <uint32_t FEAT>
 void wf_run_fused(const rtw_launch& L, const rtw_wf& W, hipStream_t st, int n_cu, size_t clds, size_t lds,
                   rtw_timer* T) {
-    const size_t cdyn = clds + RTW_WF_COOP_LDS(1024),
+    const size_t cdyn0 = clds + RTW_WF_COOP_LDS(1024),
+                 cdyn = cdyn0 + L.mat_lds <= 160u * 1024u ? cdyn0 + L.mat_lds : cdyn0,
                  ldyn = lds + RTW_WF_COOP_LDS(256) + (L.perlin_lds ? (size_t)L.n_perlin * RTW_PERLIN_BYTES : 0) +
                         ((FEAT & RTW_F_GEOM) ? L.geom_lds : 0u),
                  tdyn = lds + ((FEAT & RTW_F_GEOM) ? L.geom_lds : 0u),
@@ -746,10 +757,10 @@ void wf_run_fused(const rtw_launch& L, const rtw_wf& W, hipStream_t st, int n_cu
     thread_local uint32_t cgrid[2] = {0, 0}, tgrid[2] = {0, 0}, lgrid[2] = {0, 0}, ggrid = 0;
     uint32_t grid = 0;
     if constexpr ((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING)) == 0) {
-        if (clds && cgrid[1] != clds) {
+        if (clds && cgrid[1] != cdyn) {
             cgrid[0] = wf_grid(wf_step_clds<FEAT>, n_cu, cdyn, 1024);
             tgrid[0] = wf_grid(wf_tail_clds<FEAT>, n_cu, clds, 1024);
-            cgrid[1] = tgrid[1] = (uint32_t)clds;
+            cgrid[1] = tgrid[1] = (uint32_t)cdyn;
         }
     }
     if (clds) {
@@ -772,7 +783,9 @@ void wf_run_fused(const rtw_launch& L, const rtw_wf& W, hipStream_t st, int n_cu
         RTW_TIME_BEGIN(T, RTW_K_TRACE)
         if constexpr ((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING)) == 0) {
             if (clds) {
-                hipLaunchKernelGGL(wf_step_clds<FEAT>, dim3(grid), dim3(1024), cdyn, st, L, W, it);
+                rtw_launch Lc = L;  // the materials are staged only when they fit
+                if (cdyn == cdyn0) Lc.mat_lds = 0;
+                hipLaunchKernelGGL(wf_step_clds<FEAT>, dim3(grid), dim3(1024), cdyn, st, Lc, W, it);
                 RTW_TIME_END(T)
                 continue;
             }
