@@ -338,7 +338,15 @@ __global__ __launch_bounds__(1024) void wf_trace_clds(rtw_launch L, rtw_wf W, ui
 // shade: emission / background and Material.scatter; a surviving path's state
 // moves to its slot in the other set; an ending path stores its radiance by id
 template <uint32_t FEAT>
-__global__ __launch_bounds__(256) void wf_shade(rtw_launch L, rtw_wf W, uint32_t it) {
+__global__ __launch_bounds__(256) void wf_shade(rtw_launch L0, rtw_wf W, uint32_t it) {
+    rtw_launch L = L0;
+    if constexpr ((FEAT & RTW_F_GEOM) != 0) {
+        if (L0.geom_lds) {  // quads / members / instances in LDS (hit records of object scenes)
+            extern __shared__ float4 wf_shade_geom[];
+            L = stage_geom(L0, wf_shade_geom);
+            __syncthreads();
+        }
+    }
     const rtw_wf_set& S = W.set[it & 1u];
     const rtw_wf_set& O = W.set[(it + 1u) & 1u];
     for (WfIter e(W, it); e.more(); e.next()) {
@@ -892,7 +900,8 @@ void wf_run(const rtw_launch& L, const rtw_wf& W, hipStream_t st, int n_cu, rtw_
         RTW_TIME_END(T)
     shade_step:
         RTW_TIME_BEGIN(T, RTW_K_SHADE)
-        hipLaunchKernelGGL(wf_shade<FEAT>, dim3(g.shade), dim3(256), 0, st, L, W, it);
+        hipLaunchKernelGGL(wf_shade<FEAT>, dim3(g.shade), dim3(256), (FEAT & RTW_F_GEOM) ? L.geom_lds : 0u, st, L,
+                           W, it);
         RTW_TIME_END(T)
     }
     if (iters < L.max_depth) {
