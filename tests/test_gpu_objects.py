@@ -110,8 +110,8 @@ def test_object_kernels_bit_identical(rtw, name, monkeypatch):
 @pytest.mark.parametrize("name", ["cornell", "cornell_smoke", "simple_light", "stress"])
 def test_fused_step_bit_identical(rtw, name, monkeypatch):
     """The fused wavefront step (gen+trace+shade in one kernel; tree in LDS, or through
-    L1/L2 with RTW_WF_FUSE=7; Perlin tables in LDS or not; quads / members / instances
-    in LDS or not) renders exactly what the separate kernels render."""
+    L1/L2 with RTW_WF_FUSE=7; Perlin tables, quads / members / instances, materials /
+    textures in LDS or not) renders exactly what the separate kernels render."""
     if name == "stress":
         arr = rtw.flatten(rtw.worlds.stress_world(5000, 1))
         kw = dict(aspect_ratio=1.5, vfov=20.0, lookfrom=(13.0, 2.0, 3.0), lookat=(0.0, 0.0, 0.0),
@@ -121,15 +121,16 @@ def test_fused_step_bit_identical(rtw, name, monkeypatch):
         kw = SCENES[name][1]
     cam = rtw.Camera(image_width=80, samples_per_pixel=6, max_depth=50, **kw).init()
     outs = {}
-    for fuse, plds, glds in (("0", "1", "1"), ("3", "1", "1"), ("7", "1", "1"), ("3", "0", "1"), ("3", "1", "0")):
-        monkeypatch.setenv("RTW_WF_FUSE", fuse)
-        monkeypatch.setenv("RTW_PERLIN_LDS", plds)
-        monkeypatch.setenv("RTW_GEOM_LDS", glds)
+    for v in ("0111", "3111", "7111", "3011", "3101", "3110"):  # fuse, Perlin / geometry / material LDS
+        monkeypatch.setenv("RTW_WF_FUSE", v[0])
+        monkeypatch.setenv("RTW_PERLIN_LDS", v[1])
+        monkeypatch.setenv("RTW_GEOM_LDS", v[2])
+        monkeypatch.setenv("RTW_SHADE_LDS", v[3])
         world = rtw.World(arr)
-        outs[fuse + plds + glds] = render_all(rtw, world, cam, 6, 5)
+        outs[v] = render_all(rtw, world, cam, 6, 5)
         world.close()
-    for k in ("311", "711", "301", "310"):
-        assert np.array_equal(outs["011"], outs[k]), k
+    for k in ("3111", "7111", "3011", "3101", "3110"):
+        assert np.array_equal(outs["0111"], outs[k]), k
 
 
 def test_object_counters_equal_reference_traversal(rtw, oracle):

@@ -373,6 +373,9 @@ int rtw_scene_create(const rtw_scene_desc* d, int device, rtw_ctx** out) {
     // nodes (wf_run_fused checks the total): hit_prep's material load stops waiting on L1/L2
     L.mat_lds = (uint32_t)((d->n_materials * sizeof(rtw_dev_material) + 15) & ~size_t(15));
     if (const char* ml = std::getenv("RTW_MAT_LDS")) L.mat_lds = std::atoi(ml) != 0 ? L.mat_lds : 0u;
+    const size_t shade_bytes = (size_t)(o_perl - o_mats);
+    L.shade_lds = shade_bytes <= 8192 ? (uint32_t)shade_bytes : 0u;
+    if (const char* sl = std::getenv("RTW_SHADE_LDS")) L.shade_lds = std::atoi(sl) != 0 ? L.shade_lds : 0u;
     const size_t geom_bytes = (size_t)(o_med - o_quad);
     L.geom_lds = (ctx->feat & RTW_F_GEOM) && geom_bytes <= 16384 ? (uint32_t)geom_bytes : 0u;
     if (const char* gl = std::getenv("RTW_GEOM_LDS")) L.geom_lds = std::atoi(gl) != 0 ? L.geom_lds : 0u;

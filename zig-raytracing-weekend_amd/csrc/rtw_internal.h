@@ -71,6 +71,8 @@ struct rtw_launch {
                                  // bit 1: the tail walks the LDS stage too
     uint32_t perlin_lds;         // fused step with the node array in LDS: Perlin tables staged in LDS too
     uint32_t mat_lds;            // compact-LDS fused step: bytes of the material array staged in LDS (0: off)
+    uint32_t shade_lds;          // node-LDS kernels: bytes of materials | textures | image records (contiguous
+                                 // in the scene blob) staged in LDS when small; 0 = read through L1/L2
     uint32_t geom_lds;           // node-LDS step/tail: bytes of quads | members | instances (contiguous in the
                                  // scene blob) staged in LDS too; 0 = read through L1/L2
 };

@@ -191,24 +191,32 @@ __global__ __launch_bounds__(256) void wf_trace(rtw_launch L, rtw_wf W, uint32_t
         extern __shared__ float4 wf_lds_nodes[];
         const uint32_t n4 = 2u * L.n_nodes * L.n_orders;
         for (uint32_t k = threadIdx.x; k < n4; k += 256u) wf_lds_nodes[k] = L.nodes[k];
-        rtw_launch G = L;
-        if constexpr ((FEAT & RTW_F_GEOM) != 0) {
-            if (L.geom_lds) G = stage_geom(L, wf_lds_nodes + n4);
-        }
-        __syncthreads();
-        for (WfIter e(W, it); e.more(); e.next()) {
-            uint32_t slot;
-            if (e.get(W, slot)) {
-                uint32_t depth;
-                const Ray r = wf_load_ray(S, slot, depth);
-                if (depth) {
-                    float t;
-                    const int h = traverse<FEAT>(wf_lds_nodes, G, r, t, cnt, wf_mkey<FEAT>(S, slot));
-                    W.hit[slot] = make_float2(t, __int_as_float(h));
-                    cnt.rays++;
+        auto run = [&](const rtw_launch& G) {  // G: geometry statically in LDS or not
+            for (WfIter e(W, it); e.more(); e.next()) {
+                uint32_t slot;
+                if (e.get(W, slot)) {
+                    uint32_t depth;
+                    const Ray r = wf_load_ray(S, slot, depth);
+                    if (depth) {
+                        float t;
+                        const int h = traverse<FEAT>(wf_lds_nodes, G, r, t, cnt, wf_mkey<FEAT>(S, slot));
+                        W.hit[slot] = make_float2(t, __int_as_float(h));
+                        cnt.rays++;
+                    }
                 }
             }
+        };
+        if constexpr ((FEAT & RTW_F_GEOM) != 0) {
+            if (L.geom_lds) {
+                const rtw_launch G = stage_geom(L, wf_lds_nodes + n4);
+                __syncthreads();
+                run(G);
+                flush_counters(L, cnt, 0);
+                return;
+            }
         }
+        __syncthreads();
+        run(L);
         flush_counters(L, cnt, 0);
         return;
     }
@@ -338,15 +346,24 @@ __global__ __launch_bounds__(1024) void wf_trace_clds(rtw_launch L, rtw_wf W, ui
 // shade: emission / background and Material.scatter; a surviving path's state
 // moves to its slot in the other set; an ending path stores its radiance by id
 template <uint32_t FEAT>
-__global__ __launch_bounds__(256) void wf_shade(rtw_launch L0, rtw_wf W, uint32_t it) {
-    rtw_launch L = L0;
+__device__ __forceinline__ void wf_shade_body(const rtw_launch& L, const rtw_wf& W, uint32_t it);
+
+template <uint32_t FEAT>
+__global__ __launch_bounds__(256) void wf_shade(rtw_launch L, rtw_wf W, uint32_t it) {
     if constexpr ((FEAT & RTW_F_GEOM) != 0) {
-        if (L0.geom_lds) {  // quads / members / instances in LDS (hit records of object scenes)
+        if (L.geom_lds) {  // quads / members / instances in LDS (hit records of object scenes)
             extern __shared__ float4 wf_shade_geom[];
-            L = stage_geom(L0, wf_shade_geom);
+            const rtw_launch G = stage_geom(L, wf_shade_geom);
             __syncthreads();
+            wf_shade_body<FEAT>(G, W, it);
+            return;
         }
     }
+    wf_shade_body<FEAT>(L, W, it);
+}
+
+template <uint32_t FEAT>
+__device__ __forceinline__ void wf_shade_body(const rtw_launch& L, const rtw_wf& W, uint32_t it) {
     const rtw_wf_set& S = W.set[it & 1u];
     const rtw_wf_set& O = W.set[(it + 1u) & 1u];
     for (WfIter e(W, it); e.more(); e.next()) {
@@ -461,14 +478,41 @@ __global__ __launch_bounds__(256) void wf_tail(rtw_launch L, rtw_wf W, uint32_t 
     wf_tail_body<FEAT, false>(L, W, it, nullptr);
 }
 
+// L.shade_lds: the same for the materials | textures | image records (small scenes)
+__device__ __forceinline__ rtw_launch stage_shade(const rtw_launch& L, float4* lds) {
+    const float4* src = reinterpret_cast<const float4*>(L.mats);
+    for (uint32_t k = threadIdx.x; k < L.shade_lds / 16u; k += blockDim.x) lds[k] = src[k];
+    rtw_launch G = L;
+    const char* base = reinterpret_cast<const char*>(L.mats);
+    char* lb = reinterpret_cast<char*>(lds);
+    G.mats = reinterpret_cast<const rtw_dev_material*>(lb);
+    G.texs = reinterpret_cast<const rtw_dev_texture*>(lb + (reinterpret_cast<const char*>(L.texs) - base));
+    G.img_info = reinterpret_cast<const rtw_dev_image*>(lb + (reinterpret_cast<const char*>(L.img_info) - base));
+    return G;
+}
+
 // the 32-B node array(s) staged in LDS (small object scenes: Cornell), + L.geom_lds bytes of geometry
 template <uint32_t FEAT>
 __global__ __launch_bounds__(256) void wf_tail_lds(rtw_launch L, rtw_wf W, uint32_t it) {
     extern __shared__ float4 wf_tail_nodes[];
     const uint32_t n4 = 2u * L.n_nodes * L.n_orders;
     for (uint32_t k = threadIdx.x; k < n4; k += 256u) wf_tail_nodes[k] = L.nodes[k];
+    // then materials, then geometry: one call per combination (statically LDS pointers)
+    const bool sl = L.shade_lds != 0, gl = (FEAT & RTW_F_GEOM) != 0 && L.geom_lds != 0;
+    if (sl && gl) {
+        const rtw_launch G = stage_geom(stage_shade(L, wf_tail_nodes + n4), wf_tail_nodes + n4 + L.shade_lds / 16u);
+        __syncthreads();
+        wf_tail_body<FEAT, false>(G, W, it, nullptr, wf_tail_nodes);
+        return;
+    }
+    if (sl) {
+        const rtw_launch G = stage_shade(L, wf_tail_nodes + n4);
+        __syncthreads();
+        wf_tail_body<FEAT, false>(G, W, it, nullptr, wf_tail_nodes);
+        return;
+    }
     if constexpr ((FEAT & RTW_F_GEOM) != 0) {
-        if (L.geom_lds) {
+        if (gl) {
             const rtw_launch G = stage_geom(L, wf_tail_nodes + n4);
             __syncthreads();
             wf_tail_body<FEAT, false>(G, W, it, nullptr, wf_tail_nodes);
@@ -652,6 +696,30 @@ __global__ __launch_bounds__(1024) void wf_step_clds(rtw_launch L, rtw_wf W, uin
     wf_step_body<FEAT, WALK_CLDS>(L, W, it, wf_clds, coop);
 }
 
+// wf_step's LDS extras by mask (bit 0 Perlin tables, 1 materials/textures, 2 geometry); masks a
+// scene class cannot use compile to nothing
+template <uint32_t FEAT, uint32_t MASK>
+__device__ __forceinline__ void wf_step_staged(const rtw_launch& L, const rtw_wf& W, uint32_t it, float4* nodes,
+                                               uint32_t* coop, float4* extra) {
+    constexpr bool P = (MASK & 1u) && (FEAT & RTW_F_NOISE), S = (MASK & 2u) != 0, G = (MASK & 4u) && (FEAT & RTW_F_GEOM);
+    if constexpr (P || S || G) {
+        rtw_launch Lp = L;
+        if constexpr (P) {  // noise gathers from LDS
+            const uint32_t np4 = L.n_perlin * (RTW_PERLIN_BYTES / 16u);
+            for (uint32_t k = threadIdx.x; k < np4; k += 256u) extra[k] = L.perlin[k];
+            Lp.perlin = extra;
+            extra += np4;
+        }
+        if constexpr (S) {
+            Lp = stage_shade(Lp, extra);
+            extra += L.shade_lds / 16u;
+        }
+        if constexpr (G) Lp = stage_geom(Lp, extra);
+        __syncthreads();
+        wf_step_body<FEAT, WALK_LDS>(Lp, W, it, nodes, coop);
+    }
+}
+
 // the 32-B node array (one ordering) in LDS, or the tree through L1/L2
 template <uint32_t FEAT, bool LDS>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void wf_step(rtw_launch L, rtw_wf W, uint32_t it) {
@@ -661,21 +729,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
     uint32_t* coop = reinterpret_cast<uint32_t*>(wf_lds_nodes + n4) + 64u * (threadIdx.x >> 6);
     if constexpr (LDS) {
         for (uint32_t k = threadIdx.x; k < n4; k += 256u) wf_lds_nodes[k] = L.nodes[k];
-        if constexpr ((FEAT & (RTW_F_NOISE | RTW_F_GEOM)) != 0) {
-            if (L.perlin_lds || L.geom_lds) {  // after the coop scratch: Perlin tables, then geometry
-                float4* extra = wf_lds_nodes + n4 + RTW_WF_COOP_LDS(256u) / 16u;
-                rtw_launch Lp = L;
-                if ((FEAT & RTW_F_NOISE) != 0 && L.perlin_lds) {  // noise gathers from LDS
-                    const uint32_t np4 = L.n_perlin * (RTW_PERLIN_BYTES / 16u);
-                    for (uint32_t k = threadIdx.x; k < np4; k += 256u) extra[k] = L.perlin[k];
-                    Lp.perlin = extra;
-                    extra += np4;
-                }
-                if ((FEAT & RTW_F_GEOM) != 0 && L.geom_lds) Lp = stage_geom(Lp, extra);
-                __syncthreads();
-                wf_step_body<FEAT, WALK_LDS>(Lp, W, it, wf_lds_nodes, coop);
-                return;
-            }
+        // after the coop scratch: Perlin tables, materials, geometry -- one call per staging mask, so
+        // every pointer the body reads is statically LDS or global (no flat loads)
+        const uint32_t mask = (((FEAT & RTW_F_NOISE) && L.perlin_lds) ? 1u : 0u) | (L.shade_lds ? 2u : 0u) |
+                              (((FEAT & RTW_F_GEOM) && L.geom_lds) ? 4u : 0u);
+        float4* extra = wf_lds_nodes + n4 + RTW_WF_COOP_LDS(256u) / 16u;
+        switch (mask) {
+            case 1: return wf_step_staged<FEAT, 1>(L, W, it, wf_lds_nodes, coop, extra);
+            case 2: return wf_step_staged<FEAT, 2>(L, W, it, wf_lds_nodes, coop, extra);
+            case 3: return wf_step_staged<FEAT, 3>(L, W, it, wf_lds_nodes, coop, extra);
+            case 4: return wf_step_staged<FEAT, 4>(L, W, it, wf_lds_nodes, coop, extra);
+            case 5: return wf_step_staged<FEAT, 5>(L, W, it, wf_lds_nodes, coop, extra);
+            case 6: return wf_step_staged<FEAT, 6>(L, W, it, wf_lds_nodes, coop, extra);
+            case 7: return wf_step_staged<FEAT, 7>(L, W, it, wf_lds_nodes, coop, extra);
+            default: break;
         }
         __syncthreads();
         wf_step_body<FEAT, WALK_LDS>(L, W, it, wf_lds_nodes, coop);
@@ -759,8 +826,8 @@ void wf_run_fused(const rtw_launch& L, const rtw_wf& W, hipStream_t st, int n_cu
     const size_t cdyn0 = clds + RTW_WF_COOP_LDS(1024),
                  cdyn = cdyn0 + L.mat_lds <= 160u * 1024u ? cdyn0 + L.mat_lds : cdyn0,
                  ldyn = lds + RTW_WF_COOP_LDS(256) + (L.perlin_lds ? (size_t)L.n_perlin * RTW_PERLIN_BYTES : 0) +
-                        ((FEAT & RTW_F_GEOM) ? L.geom_lds : 0u),
-                 tdyn = lds + ((FEAT & RTW_F_GEOM) ? L.geom_lds : 0u),
+                        ((FEAT & RTW_F_GEOM) ? L.geom_lds : 0u) + L.shade_lds,
+                 tdyn = lds + ((FEAT & RTW_F_GEOM) ? L.geom_lds : 0u) + L.shade_lds,
                  gdyn = RTW_WF_COOP_LDS(256);
     thread_local uint32_t cgrid[2] = {0, 0}, tgrid[2] = {0, 0}, lgrid[2] = {0, 0}, ggrid = 0;
     uint32_t grid = 0;
@@ -908,11 +975,12 @@ void wf_run(const rtw_launch& L, const rtw_wf& W, hipStream_t st, int n_cu, rtw_
         RTW_TIME_BEGIN(T, RTW_K_TAIL)
         if (lds && (L.wf_fuse & 2u)) {  // the node array (+ geometry) in LDS for the tail (smoke +5 %)
             thread_local uint32_t tl[2] = {0, 0};
-            if (tl[1] != tlds) {
-                tl[0] = wf_grid(wf_tail_lds<FEAT>, n_cu, tlds);
-                tl[1] = (uint32_t)tlds;
+            const size_t tdyn = tlds + L.shade_lds;  // wf_tail_lds stages the materials too
+            if (tl[1] != tdyn) {
+                tl[0] = wf_grid(wf_tail_lds<FEAT>, n_cu, tdyn);
+                tl[1] = (uint32_t)tdyn;
             }
-            hipLaunchKernelGGL(wf_tail_lds<FEAT>, dim3(tl[0]), dim3(256), tlds, st, L, W, iters);
+            hipLaunchKernelGGL(wf_tail_lds<FEAT>, dim3(tl[0]), dim3(256), tdyn, st, L, W, iters);
         } else {
             hipLaunchKernelGGL(wf_tail<FEAT>, dim3(g.tail), dim3(256), 0, st, L, W, iters);
         }
