@@ -96,3 +96,15 @@ def test_empty_ranges_leave_the_buffer(rtw, oracle, world, p0, p1, s0, s1):
     buf = np.full((cam.size, 4), 2.5, np.float32)
     got = render(rtw, world, cam, p0, p1, s0, s1, 1, buf.copy())
     assert np.array_equal(got, buf)
+
+
+def test_depth0_after_a_deep_render_on_the_same_context(rtw, world):
+    """The path-state buffer is reused across renders of one context: a depth-0 render
+    after a depth-50 render (same size, the fused single-batch path) must still add zeros
+    (rayColor(r, 0) = 0, camera.zig:183-185), not the previous render's radiance."""
+    deep = rtw.book1_camera(image_width=120, aspect_ratio=1.5, spp=6, max_depth=50).init()
+    got = render(rtw, world, deep, 0, deep.size, 0, 6, 2)
+    assert got[:, :3].max() > 0
+    flat = rtw.book1_camera(image_width=120, aspect_ratio=1.5, spp=6, max_depth=0).init()
+    got0 = render(rtw, world, flat, 0, flat.size, 0, 6, 2)
+    assert (got0[:, :3] == 0).all() and (got0[:, 3] == 6).all()

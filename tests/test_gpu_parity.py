@@ -412,3 +412,51 @@ def test_progressive_and_resume_bit_identical(rtw, book1, tmp_path):
     with pytest.raises(rtw.RtwError):
         bad.resume(str(tmp_path / "c.ckpt"))
     other.close()
+
+
+def test_c3_geometry_multi_batch_and_shards(rtw, oracle, book1, oracle_book1):
+    """BASELINE config 3 (3840x2160, the 8-GPU config) at its own geometry.
+    (1) samples [0, 72) of the full image cross the wavefront batch split: at 8.3 M
+    pixels a 2^29-path batch holds 64 samples, so the render runs as 2 batches (counted
+    by the reduce launches) -- a full-width row strip and 1500 random pixels match the
+    oracle at 1e-5 and every w = 72; (2) 8 row-interleaved shards of 8-row blocks
+    (the C3 sharding, rtw_render_rows_device) reassemble bit-identically to the 1-GPU
+    image (camera.zig:93-116 semantics on every pixel)."""
+    import torch
+    _, world = book1
+    cam = rtw.book1_camera(image_width=3840, aspect_ratio=16 / 9, spp=1024).init()
+    W, H = cam.derived.image_width, cam.derived.image_height
+    assert (W, H) == (3840, 2160)
+    acc = torch.zeros((cam.size, 4), dtype=torch.float32, device="cuda")
+    timing = rtw._abi.RtwKernelTiming()
+    opts = rtw._abi.RtwRenderOpts(0, 0, None, C.pointer(timing))
+    rtw._abi.check(rtw.lib().rtw_render_device(world.handle, C.byref(cam.derived), 0, cam.size, 0, 72, 0,
+                                               acc.data_ptr(), None, C.byref(opts)), "rtw_render_device")
+    assert timing.launches[rtw._abi.RTW_K_REDUCE] >= 2, "expected the render to span several batches"
+    got = acc.cpu().numpy()
+    assert np.isfinite(got).all() and (got[:, 3] == 72).all()
+    rng = np.random.default_rng(33)
+    pix = np.unique(np.concatenate([np.arange(1200 * W, 1201 * W),
+                                    rng.choice(cam.size, 1500, replace=False)])).astype(np.uint32)
+    ocam = oracle.camera(image_width=3840, aspect_ratio=16 / 9, samples_per_pixel=1024, max_depth=50,
+                         background_mode=1)
+    ref = oracle_book1.render_pixels(ocam, 0, pix, 0, 72, threads=os.cpu_count() or 1)
+    ok = close(got[pix, :3], ref[:, :3])
+    assert ok.all(), (pix[np.argwhere(~ok)[:5, 0]], np.abs(got[pix, :3] - ref[:, :3]).max())
+    del acc
+
+    full = torch.zeros((cam.size, 4), dtype=torch.float32, device="cuda")
+    rtw._abi.check(rtw.lib().rtw_render_device(world.handle, C.byref(cam.derived), 0, cam.size, 0, 2, 5,
+                                               full.data_ptr(), None, None), "rtw_render_device")
+    n, rpb = 8, 8
+    d = rtw.distributed
+    cap = d.tile_rows_capacity(H, rpb, n)
+    tiles = torch.zeros((n, cap * W, 4), dtype=torch.float32, device="cuda")
+    for s in range(n):
+        rtw._abi.check(rtw.lib().rtw_render_rows_device(world.handle, C.byref(cam.derived), rpb, n, s, 0, 2, 5,
+                                                        tiles[s].data_ptr(), None, None), "rtw_render_rows_device")
+    src, dst = d.reassembly_index(H, rpb, n)
+    img = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda")
+    img.index_copy_(0, torch.tensor(dst, device="cuda"),
+                    tiles.view(-1, W, 4).index_select(0, torch.tensor(src, device="cuda")))
+    assert torch.equal(img.view(-1, 4), full)

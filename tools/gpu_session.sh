@@ -15,7 +15,7 @@ step() {  # step <name> <timeout> <cmd...>
   case $rc in 0|1) return 0;; *) echo "!! $name ended with $rc: stopping"; exit $rc;; esac
 }
 if [ "${SKIP_TESTS:-0}" != 1 ]; then
-  step pytest_gpu 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider
+  step pytest_gpu 1000 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 240 --timeout-method thread
   step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 fi
 if [ -n "${TUNE_ARGS:-}" ]; then step tune 600 python tools/tune.py ${TUNE_ARGS}; fi

@@ -177,12 +177,16 @@ class RayTraceState:
         cam = _abi.RtwCamera()
         seed, h, done = C.c_uint64(), C.c_uint64(), C.c_uint32()
         b = self.writer.buffer
+        # read into a scratch buffer: a refused checkpoint leaves the caller's accumulator untouched
+        tmp = np.empty_like(b)
         _abi.check(_abi.lib().rtw_checkpoint_read(path.encode(), C.byref(cam), C.byref(seed), C.byref(h),
-                                                  C.byref(done), b.ctypes.data, b.shape[0]), "rtw_checkpoint_read")
+                                                  C.byref(done), tmp.ctypes.data, tmp.shape[0]),
+                   "rtw_checkpoint_read")
         mine = C.c_uint64()
         _abi.check(_abi.lib().rtw_scene_hash(self.world.handle, C.byref(mine)), "rtw_scene_hash")
         if h.value != mine.value or seed.value != self.seed or bytes(cam) != bytes(self.camera.derived):
             raise _abi.RtwError(_abi.RTW_E_INVALID, "resume", "checkpoint is for another scene/camera/seed")
+        b[...] = tmp
         self.writer.update_texture()
         return int(done.value)
 

@@ -317,11 +317,12 @@ int rtw_scene_create(const rtw_scene_desc* d, int device, rtw_ctx** out) {
     {
         // wavefront batch capacity: up to 2^29 paths (BASELINE config 2 = 480M samples in one
         // batch: one drain of long paths per render instead of one per 64M), within ~35 % of
-        // the device's memory (RTW_WF_PATH_BYTES per path)
+        // the device's FREE memory at scene creation (RTW_WF_PATH_BYTES per path); the
+        // allocation halves the batch on failure (run_wavefront)
         size_t free_b = 0, total_b = 0;
         uint64_t cap = 1ull << 29;
-        if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && total_b)
-            cap = std::min<uint64_t>(cap, (uint64_t)(0.35 * (double)total_b) / RTW_WF_PATH_BYTES);
+        if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b)
+            cap = std::min<uint64_t>(cap, (uint64_t)(0.35 * (double)free_b) / RTW_WF_PATH_BYTES);
         ctx->wf_max_paths = std::max<uint64_t>(cap, 1u << 20);
     }
     if (const char* wp = std::getenv("RTW_WF_PATHS")) {
@@ -521,7 +522,7 @@ int run_wavefront(rtw_ctx* ctx, rtw_launch L, hipStream_t stream, rtw_timer* T) 
     const uint32_t spp = L.s1 - L.s0;
     uint64_t n_s = std::max<uint64_t>(1, ctx->wf_max_paths / n_pix);
     if (n_s > spp) n_s = spp;
-    const uint64_t need = n_pix * n_s;
+    uint64_t need = n_pix * n_s;
     if (need > 0x7FFFFFFFull) return fail(RTW_E_INVALID, "wavefront batch too large");
     // stripe capacity: a stripe receives the survivors of nw/STRIPES waves that
     // each take <= ceil(chunks / nw) 64-path chunks (rtw_wavefront.h)
@@ -538,12 +539,21 @@ int run_wavefront(rtw_ctx* ctx, rtw_launch L, hipStream_t stream, rtw_timer* T) 
         }
         ctx->d_wf = nullptr;
         ctx->wf_cap = 0;
-        const uint64_t Q = slots(need);
-        const size_t bytes = 2 * Q * (4 * 16 + 8 + 4) + Q * 8 + need * 16 +
-                             3 * (RTW_WF_STRIPES * RTW_WF_LEN_STRIDE * 4 + 256);
-        HIP_TRY(hipMalloc(&ctx->d_wf, bytes));
+        for (;;) {  // device memory taken since scene creation (other contexts, torch): halve the batch
+            const uint64_t Q = slots(need);
+            const size_t bytes = 2 * Q * (4 * 16 + 8 + 4) + Q * 8 + need * 16 +
+                                 3 * (RTW_WF_STRIPES * RTW_WF_LEN_STRIDE * 4 + 256);
+            const hipError_t e = hipMalloc(&ctx->d_wf, bytes);
+            if (e == hipSuccess) break;
+            if (e != hipErrorOutOfMemory || n_s == 1) return hip_fail(e, "wavefront path state");
+            (void)hipGetLastError();  // clear the sticky OOM before the retry
+            n_s = (n_s + 1) / 2;
+            need = n_pix * n_s;
+            ctx->wf_max_paths = need;  // later renders start from the size that fit
+        }
         ctx->wf_cap = need;
     }
+    if (n_s * n_pix > ctx->wf_cap) n_s = std::max<uint64_t>(1, ctx->wf_cap / n_pix);
     const uint64_t P = ctx->wf_cap, Q = slots(P);
     char* cur = static_cast<char*>(ctx->d_wf);
     auto take = [&](size_t nb) {

@@ -7,6 +7,7 @@
 // Progress/resume: countSamples (main.zig:470-477) and a CRC-checked checkpoint
 // file of the accumulator + the camera, seed, scene hash and samples done.
 #include <hip/hip_runtime.h>
+#include <unistd.h>
 
 #include <cmath>
 #include <cstdio>
@@ -134,7 +135,10 @@ int rtw_checkpoint_write(const char* path, const rtw_camera* cam, uint64_t seed,
                          uint32_t spp_done, const float* accum) {
     if (!path || !cam || !accum) return RTW_E_INVALID;
     crc_init();
-    FILE* f = std::fopen(path, "wb");
+    // write path.tmp, flush it to disk, then rename it over path: a crash mid-write (the case
+    // resume exists for) leaves the previous checkpoint intact
+    const std::string tmp_path = std::string(path) + ".tmp";
+    FILE* f = std::fopen(tmp_path.c_str(), "wb");
     if (!f) return RTW_E_INVALID;
     uint32_t crc = 0xFFFFFFFFu;
     bool ok = true;
@@ -154,7 +158,10 @@ int rtw_checkpoint_write(const char* path, const rtw_camera* cam, uint64_t seed,
     put(accum, n_pix * 16);
     const uint32_t c = crc ^ 0xFFFFFFFFu;
     ok = ok && std::fwrite(&c, 1, 4, f) == 4;
+    ok = ok && std::fflush(f) == 0 && ::fsync(::fileno(f)) == 0;
     ok = (std::fclose(f) == 0) && ok;
+    ok = ok && std::rename(tmp_path.c_str(), path) == 0;
+    if (!ok) std::remove(tmp_path.c_str());
     return ok ? RTW_OK : RTW_E_INVALID;
 }
 

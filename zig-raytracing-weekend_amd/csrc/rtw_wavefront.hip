@@ -854,6 +854,9 @@ void wf_run_fused(const rtw_launch& L, const rtw_wf& W, hipStream_t st, int n_cu
     // zeroed by the kernel two iterations before (wf_step_zero_next)
     (void)hipMemsetAsync(W.len[1], 0, RTW_WF_STRIPES * RTW_WF_LEN_STRIDE * 4, st);
     const uint32_t iters = L.max_depth < W.iters ? L.max_depth : W.iters;
+    // rayColor(depth <= 0) = 0 (camera.zig:183-185): no iteration writes W.ls, which holds the
+    // previous render's radiance, so the reduce must add zeros
+    if (iters == 0) (void)hipMemsetAsync(W.ls, 0, (size_t)W.n_paths * sizeof(float4), st);
     for (uint32_t it = 0; it < iters; it++) {
         RTW_TIME_BEGIN(T, RTW_K_TRACE)
         if constexpr ((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING)) == 0) {
