@@ -1,10 +1,16 @@
-"""The committed bench line (profiles/r1_c2_wavefront_bench.json, written by bench.py on
-an MI355X) carries every field of the driver's contract: the headline metric of
-BASELINE.json on config 2, the dominant kernel's roofline and the CPU baseline."""
+"""The committed bench line (profiles/r2_c2_bench.json, written by bench.py on an
+MI355X) carries every field of the driver's contract: the headline metric of
+BASELINE.json on config 2, the dominant kernel's roofline and the CPU baseline.
+Its roofline fractions are physical (<= 1) and recomputable from profiles/
+(tools/roofline_check.py)."""
 import json
 import os
+import subprocess
+import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BENCH = "r2_c2_bench.json"
+SUMMARY = "r2_c2_timed_summary.txt"
 
 
 def load(name):
@@ -13,7 +19,7 @@ def load(name):
 
 
 def test_c2_bench_line_contract():
-    d = load("r1_c2_wavefront_bench.json")
+    d = load(BENCH)
     base = json.load(open(os.path.join(REPO, "BASELINE.json")))
     assert d["metric"] == base["metric"]
     for k in ("value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
@@ -26,21 +32,32 @@ def test_c2_bench_line_contract():
     r = d["roofline"]
     for k in ("bound", "achieved", "peak", "unit", "frac", "traffic"):
         assert k in r, k
-    assert r["bound"] == "hbm" and r["unit"] == "GB/s" and r["peak"] == 8000.0
+    assert r["bound"] == "valu" and r["unit"] == "Tlane-op/s"
     assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-3
+    assert 0 < r["frac"] <= 1 and 0 < r["hbm"]["frac"] <= 1 and r["hbm"]["peak"] == 8000.0
+    assert 0 < r["valu"]["lane_util"] <= 1
     assert r["traffic"] and r["traffic"] > 0
     c = d["cpu_baseline"]
     for k in ("value", "unit", "cores", "kind", "sample"):
         assert k in c, k
     assert c["kind"] in ("port", "reference") and c["cores"] >= 1 and c["value"] > 0
+    # the reference's 8 threads AND all host cores
+    assert c["legs"]["threads_8"]["threads"] == 8 and c["legs"]["threads_all"]["threads"] == c["cores_all"]
+    assert c["value"] == max(v["value"] for v in c["legs"].values())
+
+
+def test_roofline_recomputes_from_profiles():
+    rc = subprocess.run([sys.executable, os.path.join(REPO, "tools", "roofline_check.py"),
+                         os.path.join(REPO, "profiles", BENCH)], capture_output=True, text=True)
+    assert rc.returncode == 0, rc.stdout + rc.stderr
 
 
 def test_rocprof_summary_agrees_with_bench_events():
-    """profiles/r1_c2_wavefront_timed_summary.txt (rocprofv3 --kernel-trace --stats of the
-    bench command) and the bench's HIP-event average of the dominant kernel agree."""
-    d = load("r1_c2_wavefront_bench.json")
+    """profiles/r2_c2_timed_summary.txt (rocprofv3 --kernel-trace --stats of the bench
+    command) and the bench's HIP-event average of the dominant kernel agree."""
+    d = load(BENCH)
     kernel = d["roofline"]["kernel"]
-    for line in open(os.path.join(REPO, "profiles", "r1_c2_wavefront_timed_summary.txt")):
+    for line in open(os.path.join(REPO, "profiles", SUMMARY)):
         if kernel + "<" in line:
             mean_us = float(line.split()[-3])
             assert abs(mean_us / 1e3 - d["roofline"]["avg_launch_ms"]) <= 0.05 * d["roofline"]["avg_launch_ms"]

@@ -1,0 +1,75 @@
+"""Per-launch VALU issue counters of the bench's kernels from tools/pmc_valu.sh output.
+
+The profiled command is `bench.py --steps 1 --warmup 0`; as in tools/pmc_summary.py
+the LAST n launches of each kernel kind are kept (n = that kind's launches per step
+in the bench line of the same run), i.e. the timed step's launches, and averaged.
+
+Per launch (sums over the launch's waves, rocprofv3 units):
+  insts_valu          SQ_INSTS_VALU          wave-instructions issued to the VALU
+  active_inst_valu    SQ_ACTIVE_INST_VALU    VALU-busy quad-cycles
+  thread_cycles_valu  SQ_THREAD_CYCLES_VALU  active lanes x VALU quad-cycles
+  wave_cycles         SQ_WAVE_CYCLES         resident-wave quad-cycles
+  gui_active          GRBM_GUI_ACTIVE        GPU-busy clocks of the launch
+Derived (unit-free ratios of counters of the same launch):
+  lane_util = thread_cycles_valu / (64 * active_inst_valu)   useful lanes per VALU cycle
+  lane_ops  = insts_valu * 64 * lane_util                    useful lane-instructions
+Writes <dir>/pmc_valu.json {kind: {...}}; bench.py reads the copy in profiles/.
+"""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from pmc_summary import LAUNCH_KEY, kind_of  # noqa: E402
+
+FIELDS = {"SQ_INSTS_VALU": "insts_valu", "SQ_ACTIVE_INST_VALU": "active_inst_valu",
+          "SQ_THREAD_CYCLES_VALU": "thread_cycles_valu", "SQ_WAVE_CYCLES": "wave_cycles", "SQ_WAVES": "waves",
+          "SQ_BUSY_CYCLES": "sq_busy_cycles", "GRBM_GUI_ACTIVE": "gui_active", "GRBM_COUNT": "grbm_count"}
+
+
+def main():
+    d = sys.argv[1]
+    per = defaultdict(lambda: defaultdict(float))
+    names, dur = {}, {}
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            c = r.get("Counter_Name")
+            if c in FIELDS:
+                disp = int(r["Dispatch_Id"])
+                per[disp][FIELDS[c]] += float(r["Counter_Value"])
+                names[disp] = r["Kernel_Name"]
+    launches = {}
+    for line in open(os.path.join(d, "valu.log"), errors="replace"):
+        if line.startswith("{"):
+            try:
+                launches = json.loads(line)["roofline"]["launches"]
+            except (ValueError, KeyError):
+                pass
+    byk = defaultdict(list)
+    for disp in sorted(per):
+        k, short = kind_of(names[disp])
+        if k:
+            byk[k].append((per[disp], short))
+    out = {}
+    for k, v in byk.items():
+        n = launches.get(LAUNCH_KEY.get(k, k[3:]), 0) or len(v)
+        keep = v[-n:]
+        e = {"launches": len(keep), "kernels": sorted({s for _, s in keep})}
+        for f in FIELDS.values():
+            e[f] = sum(c.get(f, 0.0) for c, _ in keep) / max(1, len(keep))
+        if e["active_inst_valu"] > 0:
+            e["lane_util"] = e["thread_cycles_valu"] / (64.0 * e["active_inst_valu"])
+            e["lane_ops"] = e["insts_valu"] * 64.0 * e["lane_util"]
+        out[k] = e
+    json.dump(out, open(os.path.join(d, "pmc_valu.json"), "w"), indent=1, sort_keys=True)
+    for k, e in sorted(out.items(), key=lambda kv: -kv[1]["insts_valu"]):
+        print(f"{k:10s} launches/step {e['launches']:3d}  VALU insts {e['insts_valu']:.4g}  "
+              f"lane_util {e.get('lane_util', 0):.3f}  lane-ops {e.get('lane_ops', 0):.4g}  "
+              f"GUI_ACTIVE {e['gui_active']:.4g}  ({', '.join(e['kernels'])})")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,65 @@
+"""Recompute the roofline fractions of a committed bench line from profiles/.
+
+  python tools/roofline_check.py profiles/r2_c2_bench.json
+
+VALU (the bound): lane-instructions per launch of the dominant kernel
+(profiles/pmc_valu_<config>_<bvh>.json, tools/pmc_valu.sh) / the bench's HIP-event
+average launch time / the non-packed VALU issue peak (bench.py VALU_PEAK_TLOPS).
+HBM: PMC traffic per launch (profiles/pmc_traffic_<config>_<bvh>.json,
+tools/pmc_traffic.sh) / the same launch time / 8 TB/s.
+Prints both and exits non-zero if the line's numbers disagree with the
+recomputation by more than 0.5 % or any fraction exceeds 1.
+"""
+import json
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+
+def bench_line(path):
+    with open(path) as f:
+        return json.loads([ln for ln in f.read().splitlines() if ln.startswith("{")][-1])
+
+
+def recompute(line):
+    import bench
+    r = line["roofline"]
+    launch_s = r["avg_launch_ms"] / 1e3
+    out = {}
+    src = r["valu"]["source"]
+    if src:
+        e = json.load(open(os.path.join(REPO, src)))[r["valu"]["kind"]]
+        out["valu_frac"] = e["lane_ops"] / launch_s / 1e12 / bench.VALU_PEAK_TLOPS
+        out["valu_lane_util"] = e["thread_cycles_valu"] / (64 * e["active_inst_valu"])
+        out["valu_issue_busy"] = e["active_inst_valu"] * 4 / (bench.N_SIMD * launch_s * bench.CLOCK_HZ)
+    hsrc = r["hbm"]["source"]
+    if hsrc:
+        t = json.load(open(os.path.join(REPO, hsrc)))[r["hbm"]["kind"]]["traffic_bytes"]
+        out["hbm_frac"] = t / launch_s / 1e9 / bench.HBM_PEAK_GBS
+    return out
+
+
+def main():
+    line = bench_line(sys.argv[1])
+    r = line["roofline"]
+    got = recompute(line)
+    ok = True
+    pairs = (("valu_frac", r["frac"]), ("hbm_frac", r["hbm"]["frac"]), ("valu_lane_util", r["valu"]["lane_util"]),
+             ("valu_issue_busy", r["valu"]["issue_busy"]))
+    for k, v in pairs:
+        if k not in got:
+            continue
+        good = v is not None and abs(got[k] - v) <= 5e-3 * max(abs(v), 1e-9) + 1e-4
+        ok &= good
+        print(f"{k:16s} line {v}  recomputed {got[k]:.4f}  {'ok' if good else 'MISMATCH'}")
+    for k in ("valu_frac", "hbm_frac"):
+        if k in got and not got[k] <= 1.0:
+            print(f"{k} > 1")
+            ok = False
+    sys.exit(0 if ok else 1)
+
+
+if __name__ == "__main__":
+    main()
