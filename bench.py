@@ -44,6 +44,7 @@ def parse():
                     choices=["c1", "c2", "c3", "c4", "c5", "cornell", "cornell_smoke", "simple_light"])
     ap.add_argument("--spp", type=int, default=0, help="override spp (0 = config's)")
     ap.add_argument("--bvh", default="sah", choices=["sah", "reference"])
+    ap.add_argument("--tuning", default="", help='rtw_tuning fields as JSON, e.g. {"wf_iters": 12} (A/B only)')
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline duration")
     ap.add_argument("--cpu-threads", type=int, default=8, help="reference uses 8 render threads (main.zig:41)")
@@ -74,7 +75,7 @@ def main():
     bvh_mode = {"sah": pkg._abi.RTW_BVH_SAH, "reference": pkg._abi.RTW_BVH_REFERENCE}[args.bvh]
     arr = pkg.flatten(objs, bvh_mode=bvh_mode)
     t0 = time.time()
-    world = pkg.World(arr, device=local_rank)
+    world = pkg.World(arr, device=local_rank, tuning=json.loads(args.tuning) if args.tuning else None)
     build_s = time.time() - t0
     # the reference topology (bvh.zig) defines the algorithmic bytes
     world_ref = pkg.World(pkg.flatten(objs, bvh_mode=pkg._abi.RTW_BVH_REFERENCE), device=local_rank)

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define RTW_ABI_VERSION 2
+#define RTW_ABI_VERSION 3
 
 enum rtw_status {
     RTW_OK = 0,
@@ -267,6 +267,50 @@ int rtw_camera_init(const rtw_camera_params* params, rtw_camera* out);
  * perlin tables to `device`.  Replaces generateWorld's BVHTree.init
  * (src/main.zig:309, src/bvh.zig:22-29). */
 int rtw_scene_create(const rtw_scene_desc* desc, int device, rtw_ctx** out);
+
+/* Implementation choices of a context (ABI 3).  Every setting renders the SAME image,
+ * bit for bit (each one is a different schedule of the same fp32
+ * operations); they exist for A/B measurement and the invariance tests.  Start from
+ * rtw_tuning_defaults() -- the product defaults -- and change fields. */
+enum rtw_kernel_kind {
+    RTW_KERNEL_WAVEFRONT = 0,  /* wavefront path tracer (rtw_wavefront.hip), the product path */
+    RTW_KERNEL_PERSISTENT = 1, /* persistent megakernel (render_persistent_v1), a baseline */
+    RTW_KERNEL_SIMPLE = 2      /* one lane per pixel (render_pixels_v0), a baseline */
+};
+enum {  /* rtw_tuning.lds: what the kernels may stage in LDS when it fits */
+    RTW_LDS_NODES = 1u,        /* the 32-B node array (wavefront trace / fused step / tail) */
+    RTW_LDS_CNODES = 2u,       /* the compact nodes of every octant copy (small static sphere SAH trees) */
+    RTW_LDS_MATERIALS = 4u,    /* materials beside the compact nodes */
+    RTW_LDS_SHADE = 8u,        /* materials | textures | image records of small scenes */
+    RTW_LDS_GEOMETRY = 16u,    /* quads | members | instances of small object scenes */
+    RTW_LDS_PERLIN = 32u,      /* Perlin tables (noise scenes) */
+    RTW_LDS_MEGA_NODES = 64u,  /* the persistent megakernel's node stage */
+    RTW_LDS_ALL = 127u
+};
+enum {  /* rtw_tuning.fuse */
+    RTW_FUSE_STEP = 1u,        /* gen + trace + shade of an iteration in one kernel (trees staged in LDS) */
+    RTW_FUSE_TAIL_LDS = 2u,    /* the tail kernel walks the LDS stage */
+    RTW_FUSE_GLOBAL = 4u       /* the fused step also for trees read through L1/L2 */
+};
+typedef struct rtw_tuning {
+    uint32_t kernel;           /* rtw_kernel_kind (default WAVEFRONT) */
+    uint32_t bvh_orders;       /* 0 = auto (8 octant-ordered copies for SAH sphere scenes, else 1), 1 or 8 */
+    uint32_t sah_max_leaf;     /* spheres per SAH leaf (default 1) */
+    uint32_t compact_nodes;    /* 1 = 16-B fp16 node walk for static sphere SAH trees (default) */
+    uint32_t fast_box;         /* 1 = FMA slab test on the padded SAH boxes (default); 0 = aabb.zig arithmetic */
+    uint32_t fast_reject;      /* 1 = exact sphere fast-reject filter (default) */
+    uint32_t lds;              /* RTW_LDS_* (default RTW_LDS_ALL) */
+    uint32_t fuse;             /* RTW_FUSE_* (default STEP | TAIL_LDS) */
+    uint32_t wf_iters;         /* wavefront iterations before the tail kernel (default 9; 1..64) */
+    uint32_t mega_shade_min;   /* persistent kernel: lanes ready before a shading pass (default 48; 1..64) */
+    uint32_t mega_waves;       /* persistent kernel: launch-bound variant (default 1; 1, 6 or 8) */
+    uint32_t mega_tile_order;  /* persistent kernel: 1 = last tile row first (default) */
+    uint64_t wf_paths;         /* wavefront batch capacity in paths; 0 = auto (2^29 within 35 % of free memory) */
+} rtw_tuning;
+
+void rtw_tuning_defaults(rtw_tuning* out);
+/* rtw_scene_create with explicit tuning (NULL = defaults). */
+int rtw_scene_create_ex(const rtw_scene_desc* desc, int device, const rtw_tuning* tuning, rtw_ctx** out);
 void rtw_scene_destroy(rtw_ctx* ctx);
 
 /* Camera.render for the pixel range [pix_begin, pix_end) (linear index

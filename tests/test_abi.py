@@ -29,13 +29,13 @@ def test_exports_every_header_symbol(rtw):
     for n in names:
         assert hasattr(lib, n), n
     assert set(names) == set(rtw._abi.SIGNATURES), set(names) ^ set(rtw._abi.SIGNATURES)
-    assert lib.rtw_version() == 2
+    assert lib.rtw_version() == 3
 
 
 def test_struct_sizes_match_header(rtw, tmp_path):
     prog = tmp_path / "sizes.c"
     structs = ["rtw_sphere", "rtw_material", "rtw_texture", "rtw_image", "rtw_perlin", "rtw_scene_desc",
-               "rtw_camera_params", "rtw_camera", "rtw_render_opts", "rtw_scene_stats"]
+               "rtw_camera_params", "rtw_camera", "rtw_render_opts", "rtw_scene_stats", "rtw_tuning"]
     prog.write_text('#include <stdio.h>\n#include "rtw_gpu.h"\nint main(){' +
                     "".join(f'printf("%zu\\n", sizeof({s}));' for s in structs) + "return 0;}\n")
     exe = tmp_path / "sizes"
@@ -44,8 +44,20 @@ def test_struct_sizes_match_header(rtw, tmp_path):
     A = rtw._abi
     mine = [A.SPHERE_DT.itemsize, A.MATERIAL_DT.itemsize, A.TEXTURE_DT.itemsize, C.sizeof(A.RtwImage),
             A.PERLIN_DT.itemsize, C.sizeof(A.RtwSceneDesc), C.sizeof(A.RtwCameraParams), C.sizeof(A.RtwCamera),
-            C.sizeof(A.RtwRenderOpts), C.sizeof(A.RtwSceneStats)]
+            C.sizeof(A.RtwRenderOpts), C.sizeof(A.RtwSceneStats), C.sizeof(A.RtwTuning)]
     assert sizes == mine
+
+
+def test_tuning_defaults_and_no_environment_knobs(rtw):
+    """The library is configured only through rtw_tuning (no getenv in the product .so);
+    rtw_tuning_defaults() is the product configuration."""
+    t = rtw._abi.tuning()
+    A = rtw._abi
+    assert (t.kernel, t.bvh_orders, t.sah_max_leaf, t.compact_nodes, t.fast_box, t.fast_reject) == (0, 0, 1, 1, 1, 1)
+    assert t.lds == A.RTW_LDS_ALL and t.fuse == A.RTW_FUSE_STEP | A.RTW_FUSE_TAIL_LDS and t.wf_iters == 9
+    assert t.wf_paths == 0
+    syms = subprocess.check_output(["nm", "-D", "--undefined-only", rtw._abi.LIB_PATH], text=True)
+    assert "getenv" not in syms, "the product library reads the environment"
 
 
 @pytest.mark.parametrize("kw", [dict(image_width=1200, aspect_ratio=1.5, spp=500),

@@ -94,24 +94,23 @@ def test_object_scene_vs_oracle(rtw, oracle, name, mode):
 
 
 @pytest.mark.parametrize("name", ["cornell", "cornell_smoke"])
-def test_object_kernels_bit_identical(rtw, name, monkeypatch):
+def test_object_kernels_bit_identical(rtw, name):
     """v0 / v1 / wavefront perform the same per-path operations: identical images."""
     arr = rtw.flatten(SCENES[name][0](rtw.worlds))
     cam = rtw.Camera(image_width=64, samples_per_pixel=6, max_depth=50, **SCENES[name][1]).init()
     outs = {}
-    for k in ("v0", "v1", "wf"):
-        monkeypatch.setenv("RTW_KERNEL", k)
-        world = rtw.World(arr)
+    for k, kern in (("v0", 2), ("v1", 1), ("wf", 0)):
+        world = rtw.World(arr, tuning={"kernel": kern})
         outs[k] = render_all(rtw, world, cam, 6, 9)
         world.close()
     assert np.array_equal(outs["v0"], outs["v1"]) and np.array_equal(outs["v0"], outs["wf"])
 
 
 @pytest.mark.parametrize("name", ["cornell", "cornell_smoke", "simple_light", "stress"])
-def test_fused_step_bit_identical(rtw, name, monkeypatch):
+def test_fused_step_bit_identical(rtw, name):
     """The fused wavefront step (gen+trace+shade in one kernel; tree in LDS, or through
-    L1/L2 with RTW_WF_FUSE=7; Perlin tables, quads / members / instances, materials /
-    textures in LDS or not) renders exactly what the separate kernels render."""
+    L1/L2 with fuse = STEP|TAIL_LDS|GLOBAL; Perlin tables, quads / members / instances,
+    materials / textures in LDS or not) renders exactly what the separate kernels render."""
     if name == "stress":
         arr = rtw.flatten(rtw.worlds.stress_world(5000, 1))
         kw = dict(aspect_ratio=1.5, vfov=20.0, lookfrom=(13.0, 2.0, 3.0), lookat=(0.0, 0.0, 0.0),
@@ -122,11 +121,8 @@ def test_fused_step_bit_identical(rtw, name, monkeypatch):
     cam = rtw.Camera(image_width=80, samples_per_pixel=6, max_depth=50, **kw).init()
     outs = {}
     for v in ("0111", "3111", "7111", "3011", "3101", "3110"):  # fuse, Perlin / geometry / material LDS
-        monkeypatch.setenv("RTW_WF_FUSE", v[0])
-        monkeypatch.setenv("RTW_PERLIN_LDS", v[1])
-        monkeypatch.setenv("RTW_GEOM_LDS", v[2])
-        monkeypatch.setenv("RTW_SHADE_LDS", v[3])
-        world = rtw.World(arr)
+        lds = 127 & ~((32 if v[1] == "0" else 0) | (16 if v[2] == "0" else 0) | (8 if v[3] == "0" else 0))
+        world = rtw.World(arr, tuning={"fuse": int(v[0]), "lds": lds})
         outs[v] = render_all(rtw, world, cam, 6, 5)
         world.close()
     for k in ("3111", "7111", "3011", "3101", "3110"):

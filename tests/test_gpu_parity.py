@@ -278,7 +278,7 @@ def test_device_counters_equal_reference_traversal(rtw, oracle, book1, oracle_bo
 
 
 @pytest.mark.parametrize("scene", ["book1", "ref_head"])
-def test_persistent_v1_bit_identical_to_v0(rtw, earth_rgba, scene, monkeypatch):
+def test_persistent_v1_bit_identical_to_v0(rtw, earth_rgba, scene):
     """The persistent megakernel (dynamic pixel queue, path regeneration, LDS BVH,
     feature-specialised) and the simple per-pixel kernel perform the same fp32
     operations per pixel in the same order: outputs are bit-identical."""
@@ -287,57 +287,52 @@ def test_persistent_v1_bit_identical_to_v0(rtw, earth_rgba, scene, monkeypatch):
     cam = rtw.book1_camera(image_width=480, aspect_ratio=1.5, spp=6).init()
     outs = {}
     for k in ("v0", "v1", "wf"):
-        monkeypatch.setenv("RTW_KERNEL", k)
-        world = rtw.World(arr)
+        world = rtw.World(arr, tuning={"kernel": KERNELS[k]})
         outs[k] = render_rows(rtw, world, cam, 0, cam.derived.image_height, 0, 6, 21)
         world.close()
     assert np.array_equal(outs["v0"], outs["v1"])
     assert np.array_equal(outs["v0"], outs["wf"])
 
 
-@pytest.mark.parametrize("knob", [("RTW_SHADE_MIN", "1"), ("RTW_SHADE_MIN", "64"), ("RTW_COOP", "0"),
-                                  ("RTW_TILE_ORDER", "0"), ("RTW_POSTPONE", "1"), ("RTW_LDS", "0")])
-def test_v1_knobs_invariant(rtw, book1, knob, monkeypatch):
-    """Megakernel scheduling knobs (ballot threshold, cooperative vs per-lane
-    rejection sampling, tile order, leaf postponement, LDS staging) only move
-    work between lanes: outputs are bit-identical."""
+KERNELS = {"wf": 0, "v1": 1, "v0": 2}   # rtw_kernel_kind
+
+
+@pytest.mark.parametrize("knob", [{"mega_shade_min": 1}, {"mega_shade_min": 64}, {"mega_tile_order": 0},
+                                  {"mega_waves": 8}, {"lds": 127 & ~64}])
+def test_v1_knobs_invariant(rtw, book1, knob):
+    """Megakernel scheduling (rtw_tuning: ballot threshold, tile order, launch
+    bounds, LDS staging) only moves work between lanes: outputs are bit-identical."""
     arr, _ = book1
     cam = rtw.book1_camera(image_width=300, aspect_ratio=1.5, spp=3).init()
-    monkeypatch.setenv("RTW_KERNEL", "v1")
-    w1 = rtw.World(arr)
+    w1 = rtw.World(arr, tuning={"kernel": 1})
     ref = render_rows(rtw, w1, cam, 0, 200, 0, 3, 4)
     w1.close()
-    monkeypatch.setenv(*knob)
-    w2 = rtw.World(arr)
+    w2 = rtw.World(arr, tuning={"kernel": 1, **knob})
     got = render_rows(rtw, w2, cam, 0, 200, 0, 3, 4)
     w2.close()
     assert np.array_equal(ref, got)
 
 
-@pytest.mark.parametrize("knob", [("RTW_WF_ITERS", "1"), ("RTW_WF_ITERS", "50"), ("RTW_WF_PATHS", "4096"),
-                                  ("RTW_REFILL_MIN", "16"), ("RTW_FASTBOX", "0"), ("RTW_WF_LDS", "0"),
-                                  ("RTW_SAH_LEAF", "4"), ("RTW_COMPACT", "0"),
-                                  ("RTW_WF_CLDS", "0"), ("RTW_WF_FUSE", "0"), ("RTW_WF_FUSE", "1"),
-                                  ("RTW_COOP", "0"), ("RTW_COOP", "1"), ("RTW_COOP", "2"),
-                                  ("RTW_MAT_LDS", "0")])
-def test_wavefront_knobs_invariant(rtw, book1, knob, monkeypatch):
-    """Wavefront knobs (bounces before the tail kernel, batch size -> many batches,
-    per-lane refill in trace, FMA vs reference slab test, LDS-staged nodes, SAH
-    leaf runs of up to 4 spheres, 16-B fp16-box nodes vs 32-B nodes, compact nodes in
-    LDS, fused gen+trace+shade kernel vs separate kernels, LDS vs L1/L2 tail) never
-    change a pixel."""
+@pytest.mark.parametrize("knob", [{"wf_iters": 1}, {"wf_iters": 50}, {"wf_paths": 4096}, {"fast_box": 0},
+                                  {"lds": 127 & ~1}, {"sah_max_leaf": 4}, {"compact_nodes": 0}, {"lds": 127 & ~2},
+                                  {"fuse": 0}, {"fuse": 1}, {"lds": 127 & ~4}, {"bvh_orders": 1}])
+def test_wavefront_knobs_invariant(rtw, book1, knob):
+    """Wavefront tuning (rtw_tuning: bounces before the tail kernel, batch size ->
+    many batches, FMA vs reference slab test, LDS-staged nodes, SAH leaf runs of up
+    to 4 spheres, 16-B fp16-box nodes vs 32-B nodes, compact nodes in LDS, fused
+    gen+trace+shade kernel vs separate kernels, LDS vs L1/L2 tail, materials in LDS,
+    one node ordering instead of 8) never changes a pixel."""
     arr, world = book1
     cam = rtw.book1_camera(image_width=300, aspect_ratio=1.5, spp=5).init()
     ref = render_rows(rtw, world, cam, 0, 200, 0, 5, 4)
-    monkeypatch.setenv(*knob)
-    w2 = rtw.World(arr)
+    w2 = rtw.World(arr, tuning=knob)
     got = render_rows(rtw, w2, cam, 0, 200, 0, 5, 4)
     w2.close()
     assert np.array_equal(ref, got)
 
 
 @pytest.mark.parametrize("n,seed", [(20000, 3), (100000, 0)])
-def test_compact_nodes_are_exact(rtw, n, seed, monkeypatch):
+def test_compact_nodes_are_exact(rtw, n, seed):
     """The 16-B node walk (fp16 inner boxes rounded outward, leaves with radius^2)
     visits a superset of the 32-B walk's boxes: identical images on dense stress
     worlds (small spheres far from the origin: the coarsest fp16 boxes), at the
@@ -345,9 +340,8 @@ def test_compact_nodes_are_exact(rtw, n, seed, monkeypatch):
     arr = rtw.flatten(rtw.worlds.stress_world(n, seed), bvh_mode=rtw._abi.RTW_BVH_SAH)
     cam = rtw.book1_camera(image_width=480, aspect_ratio=16 / 9, spp=4).init()
     outs = []
-    for c in ("0", "1"):
-        monkeypatch.setenv("RTW_COMPACT", c)
-        w = rtw.World(arr)
+    for c in (0, 1):
+        w = rtw.World(arr, tuning={"compact_nodes": c})
         outs.append(render_rows(rtw, w, cam, 0, cam.derived.image_height, 0, 4, 6))
         w.close()
     assert np.isfinite(outs[1]).all()
@@ -355,16 +349,15 @@ def test_compact_nodes_are_exact(rtw, n, seed, monkeypatch):
 
 
 @pytest.mark.parametrize("scene", ["book1", "stress"])
-def test_fast_reject_is_exact(rtw, scene, monkeypatch):
+def test_fast_reject_is_exact(rtw, scene):
     """The sphere fast-reject (hardware sqrt/rcp estimate + error margin) never
     changes a result: bit-identical to the always-IEEE path."""
     objs = rtw.worlds.generate_world(0, "book1") if scene == "book1" else rtw.worlds.stress_world(20000, 3)
     arr = rtw.flatten(objs)
     cam = rtw.book1_camera(image_width=600, aspect_ratio=1.5, spp=4).init()
     outs = []
-    for fr in ("0", "1"):
-        monkeypatch.setenv("RTW_FAST_REJECT", fr)
-        w = rtw.World(arr)
+    for fr in (0, 1):
+        w = rtw.World(arr, tuning={"fast_reject": fr})
         outs.append(render_rows(rtw, w, cam, 0, cam.derived.image_height, 0, 4, 5))
         w.close()
     assert np.array_equal(outs[0], outs[1])

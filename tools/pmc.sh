@@ -6,7 +6,7 @@ mkdir -p "$OUT"
 export TMPDIR=/tmp
 SPP=${SPP:-20}
 CFG=${CFG:-c2}
-export TUNE=${TUNE:-'[{"RTW_KERNEL":"v1","RTW_SHADE_MIN":"48"}]'}
+export TUNE=${TUNE:-'[{"kernel": 1}]'}
 if [ "${LIST:-0}" = 1 ]; then
   timeout -k 10 120 rocprofv3 -L > "$OUT/counters.txt" 2>&1 || true
 fi

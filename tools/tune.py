@@ -1,5 +1,6 @@
-"""A/B timing of kernel variants / knobs on BASELINE config 2 geometry (reduced spp).
-Usage: python tools/tune.py [spp] ; knobs via env lists in the script."""
+"""A/B timing of rtw_tuning settings on a config at reduced spp.
+Usage: TUNE='[{"kernel": 1}, {"wf_iters": 12}, {"bvh": "ref"}]' python tools/tune.py [spp] [config]
+Each setting: rtw_tuning fields (include/rtw_gpu.h) plus "bvh" ("sah"/"ref") and "order"."""
 import ctypes as C
 import importlib
 import json
@@ -13,9 +14,7 @@ import torch  # noqa: E402
 pkg = importlib.import_module("zig-raytracing-weekend_amd")
 spp = int(sys.argv[1]) if len(sys.argv) > 1 else 100
 cfg_name = sys.argv[2] if len(sys.argv) > 2 else "c2"
-settings = json.loads(os.environ.get("TUNE", '[{"RTW_KERNEL":"v0"},{"RTW_KERNEL":"v1","RTW_SHADE_MIN":"8"},'
-                                     '{"RTW_KERNEL":"v1","RTW_SHADE_MIN":"16"},{"RTW_KERNEL":"v1","RTW_SHADE_MIN":"32"},'
-                                     '{"RTW_KERNEL":"v1","RTW_SHADE_MIN":"48"}]'))
+settings = json.loads(os.environ.get("TUNE", '[{}, {"kernel": 1}, {"kernel": 2}]'))
 cfg = pkg.configs.CONFIGS[cfg_name]
 arr = pkg.flatten(cfg.objects())
 cam = cfg.camera()
@@ -23,17 +22,12 @@ cam.samples_per_pixel = spp
 cam.init()
 acc = torch.zeros((cam.size, 4), dtype=torch.float32, device="cuda")
 stream = torch.cuda.Stream()
-prev_keys = []
 rounds = int(os.environ.get("TUNE_ROUNDS", "1"))  # round-robin repeats (box noise)
 for st in [s for _ in range(rounds) for s in settings]:
-    st = dict(st)
-    for k in prev_keys + ["RTW_KERNEL", "RTW_SHADE_MIN", "RTW_WAVES"]:
-        os.environ.pop(k, None)
-    arr.bvh_mode = {"ref": 0, "sah": 1}[st.pop("bvh", "sah")]
-    arr.order_dir = tuple(st.pop("order", (0.0, 0.0, 0.0)))
-    os.environ.update(st)
-    prev_keys = list(st.keys())
-    world = pkg.World(arr)
+    tun = dict(st)
+    arr.bvh_mode = {"ref": 0, "sah": 1}[tun.pop("bvh", "sah")]
+    arr.order_dir = tuple(tun.pop("order", (0.0, 0.0, 0.0)))
+    world = pkg.World(arr, tuning=tun or None)
     cnt = torch.zeros(8, dtype=torch.int64, device="cuda")
     torch.cuda.synchronize()  # the render runs on `stream`: the zeroing must be done
     copts = pkg._abi.RtwRenderOpts(spp, 0, cnt.data_ptr())

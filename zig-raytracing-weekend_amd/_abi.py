@@ -25,6 +25,10 @@ RTW_STAT_RAYS, RTW_STAT_NODES, RTW_STAT_LEAVES, RTW_STAT_SAMPLES, RTW_STAT_NAN, 
 RTW_STAT_COUNT = 8
 RTW_K_GEN, RTW_K_TRACE, RTW_K_SHADE, RTW_K_TAIL, RTW_K_REDUCE, RTW_K_MEGA, RTW_K_COUNT = 0, 1, 2, 3, 4, 5, 8
 RTW_K_NAMES = ("gen", "trace", "shade", "tail", "reduce", "mega")
+RTW_KERNEL_WAVEFRONT, RTW_KERNEL_PERSISTENT, RTW_KERNEL_SIMPLE = 0, 1, 2
+RTW_LDS_NODES, RTW_LDS_CNODES, RTW_LDS_MATERIALS, RTW_LDS_SHADE = 1, 2, 4, 8
+RTW_LDS_GEOMETRY, RTW_LDS_PERLIN, RTW_LDS_MEGA_NODES, RTW_LDS_ALL = 16, 32, 64, 127
+RTW_FUSE_STEP, RTW_FUSE_TAIL_LDS, RTW_FUSE_GLOBAL = 1, 2, 4
 
 # numpy record layouts == the C structs (asserted against sizeof in tests)
 SPHERE_DT = np.dtype([("center1", "<f4", 3), ("radius", "<f4"), ("center2", "<f4", 3), ("is_moving", "<u4"),
@@ -99,6 +103,24 @@ class RtwRenderOpts(C.Structure):
                 ("timing", C.POINTER(RtwKernelTiming))]
 
 
+class RtwTuning(C.Structure):
+    _fields_ = [("kernel", C.c_uint32), ("bvh_orders", C.c_uint32), ("sah_max_leaf", C.c_uint32),
+                ("compact_nodes", C.c_uint32), ("fast_box", C.c_uint32), ("fast_reject", C.c_uint32),
+                ("lds", C.c_uint32), ("fuse", C.c_uint32), ("wf_iters", C.c_uint32), ("mega_shade_min", C.c_uint32),
+                ("mega_waves", C.c_uint32), ("mega_tile_order", C.c_uint32), ("wf_paths", C.c_uint64)]
+
+
+def tuning(**fields) -> RtwTuning:
+    """rtw_tuning_defaults() with `fields` overridden (every setting renders the same image)."""
+    t = RtwTuning()
+    lib().rtw_tuning_defaults(C.byref(t))
+    for k, v in fields.items():
+        if not hasattr(t, k):
+            raise KeyError(f"rtw_tuning has no field {k!r}")
+        setattr(t, k, v)
+    return t
+
+
 class RtwSceneStats(C.Structure):
     _fields_ = [("n_nodes", C.c_uint32), ("n_leaves", C.c_uint32), ("n_inner", C.c_uint32), ("depth", C.c_uint32),
                 ("device_bytes", C.c_uint64), ("axis_draws", C.c_uint32), ("_pad", C.c_uint32)]
@@ -114,6 +136,8 @@ SIGNATURES = {
     "rtw_camera_init": (C.c_int, [C.POINTER(RtwCameraParams), C.POINTER(RtwCamera)]),
     "rtw_scene_create": (C.c_int, [C.POINTER(RtwSceneDesc), C.c_int, C.POINTER(C.c_void_p)]),
     "rtw_scene_destroy": (None, [C.c_void_p]),
+    "rtw_tuning_defaults": (None, [C.POINTER(RtwTuning)]),
+    "rtw_scene_create_ex": (C.c_int, [C.POINTER(RtwSceneDesc), C.c_int, C.POINTER(RtwTuning), C.POINTER(C.c_void_p)]),
     "rtw_render": (C.c_int, [C.c_void_p, C.POINTER(RtwCamera), C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
                              C.c_uint64, C.c_void_p, C.c_void_p, PROGRESS_FN, C.c_void_p]),
     "rtw_render_device": (C.c_int, [C.c_void_p, C.POINTER(RtwCamera), C.c_uint32, C.c_uint32, C.c_uint32,

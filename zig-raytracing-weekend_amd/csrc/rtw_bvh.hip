@@ -396,7 +396,7 @@ private:
 // first, so front-most geometry shrinks `closest` early in the fixed walk.
 class SahBuilder {
 public:
-    SahBuilder(const rtw_scene_desc& d, const Geometry& g, std::vector<rtw_node>& out)
+    SahBuilder(const rtw_scene_desc& d, const Geometry& g, std::vector<rtw_node>& out, uint32_t max_leaf)
         : geo_(g), nodes_(out), objs_(g.objects()) {
         const size_t n = objs_.size();
         cent_.resize(n);
@@ -406,8 +406,7 @@ public:
         for (size_t i = 0; i < n; i++) idx_[i] = (uint32_t)i;
         for (int k = 0; k < 3; k++) dir_[k] = d.order_dir[k];
         if (dir_[0] == 0 && dir_[1] == 0 && dir_[2] == 0) dir_[1] = -1;
-        if (const char* e = std::getenv("RTW_SAH_LEAF")) max_leaf_ = (size_t)std::max(1, std::atoi(e));
-        if (const char* e = std::getenv("RTW_SAH_CI")) ci_ = (float)std::atof(e);
+        max_leaf_ = std::max<size_t>(1, max_leaf);
     }
     // orders = 1: one pre-order with children front-to-back along order_dir;
     // orders = 8: one pre-order per ray-direction octant (bit k set = negative
@@ -577,13 +576,14 @@ private:
 }  // namespace
 
 int rtw_build_bvh(const rtw_scene_desc& desc, std::vector<rtw_node>& nodes, rtw_geometry& geom,
-                  uint32_t* depth, uint32_t* axis_draws, float* box_pad, float* extent, uint32_t orders) {
+                  uint32_t* depth, uint32_t* axis_draws, float* box_pad, float* extent, uint32_t orders,
+                  uint32_t sah_max_leaf) {
     if (box_pad) *box_pad = 0;
     if (extent) *extent = 0;
     Geometry geo(desc, geom);
     if (int rc = geo.build()) return rc;
     if (desc.bvh_mode == RTW_BVH_SAH) {
-        SahBuilder b(desc, geo, nodes);
+        SahBuilder b(desc, geo, nodes, sah_max_leaf);
         b.build(orders);
         if (depth) *depth = b.depth();
         if (axis_draws) *axis_draws = 0;

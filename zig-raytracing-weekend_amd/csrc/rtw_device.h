@@ -748,56 +748,6 @@ __device__ __forceinline__ int traverse(const float4* __restrict__ nodes, const 
     return hit_with_order(hit, oct);
 }
 
-// traverse() with leaf postponement (Aila & Laine 2009 "while-while"): a lane
-// that reaches a leaf parks it and the wave keeps stepping inner nodes for the
-// others until leaf_min/64 of the walking lanes hold one; then every parked leaf
-// is tested in one pass, so a wave step runs either the box or the sphere code,
-// not both.  Leaves are tested in walk order per lane; boxes passed meanwhile
-// saw a larger `closest` (a superset of visits, the same closest hit).
-// Must be called by the whole wave (ballots); `walking` = this lane has a ray.
-template <uint32_t FEAT>
-__device__ __forceinline__ int traverse_postponed(const float4* __restrict__ nodes, const rtw_launch& L, const Ray& r,
-                                                  bool walking, float& t_out, Counters& cnt, uint64_t mkey = 0) {
-    const uint32_t oct = order_of(L, r);
-    nodes = order_base(nodes, L, oct);
-    const RayTrav rt = ray_trav(r, L.fast_box != 0);
-    float closest = kInf;
-    int hit = -1, pend = -1;
-    uint32_t i = 0;
-    const uint32_t n = L.n_nodes;
-    bool active = walking;
-    for (;;) {
-        if (active && pend < 0 && i < n) {
-            float4 A, B;
-            load_node(nodes, i, A, B);
-            const uint32_t w = fbits(A.w);
-            if (w & RTW_LEAF_BIT) {
-                pend = (int)i;
-                i = w & RTW_SKIP_MASK;
-            } else {
-                cnt.nodes++;
-                i = box_next(r, rt, A, B, i, closest, L.fast_box != 0);
-            }
-        }
-        if (active && pend < 0 && i >= n) active = false;
-        const uint64_t walk = __ballot(active);
-        if (!walk) break;
-        const uint32_t n_walk = (uint32_t)__popcll(walk);
-        const uint32_t n_park = (uint32_t)__popcll(__ballot(active && pend >= 0));
-        if (n_park && (n_park == n_walk || n_park * 64u >= n_walk * L.leaf_min)) {
-            if (active && pend >= 0) {
-                float4 A, B;
-                load_node(nodes, (uint32_t)pend, A, B);
-                leaf_test<FEAT>(L, r, rt, A, B, (uint32_t)pend, closest, hit, cnt, mkey);
-                pend = -1;
-                if (i >= n) active = false;
-            }
-        }
-    }
-    t_out = closest;
-    return hit_with_order(hit, oct);
-}
-
 __device__ __forceinline__ f3 background(const rtw_launch& L, const Ray& r) {
     if (L.bg_mode == RTW_BG_GRADIENT) {  // camera.zig:204-206
         f3 ud = unit_vector(r.d);
@@ -983,16 +933,11 @@ __device__ __forceinline__ bool shade(const float4* __restrict__ nodes, const rt
 }
 
 // ---------------------------------------------------------------------------
-// Wave-cooperative rejection sampling (vec3.randomInUnitSphere D=3 /
-// randomInUnitDisk D=2, vec3.zig:40-45, 59-64).  The sequential loop runs until
-// the slowest lane of the wave accepts (E[max] ~ 6 iterations for 48 lanes at
-// p = 0.52).  Render-domain draws are counter-based (rtw_path_float: one Weyl
-// step each), so candidate j of a lane is draws j*D+1 .. j*D+D after its current
-// state: every round, all 64 lanes evaluate candidates of the still-unresolved
-// lanes (64/n helpers each, consecutive j), and each lane takes its FIRST
-// accepted candidate -- exactly the sequential result and stream position.
-// Must be called with every lane of the wave converged (helpers are idle
-// lanes); `slot` is 64 u32 of per-wave LDS scratch.
+// Rejection sampling of vec3.randomInUnitSphere (D = 3) / randomInUnitDisk
+// (D = 2) (vec3.zig:40-45, 59-64): the reference's per-lane loop, each lane
+// drawing from its own counter-based stream.  (A wave-cooperative form that
+// evaluated the unresolved lanes' candidates on idle lanes gave the same draws
+// but measured -3 % on C2: removed)
 // ---------------------------------------------------------------------------
 template <int D>
 __device__ __forceinline__ void seq_reject(rtw_rng& rng, float (&out)[D]) {
@@ -1011,76 +956,10 @@ __device__ __forceinline__ void seq_reject(rtw_rng& rng, float (&out)[D]) {
     }
 }
 
-template <int D>
-__device__ __forceinline__ void coop_reject(bool active, rtw_rng& rng, float (&out)[D], uint32_t* slot,
-                                            bool coop = true) {
-    if (!coop) {  // A/B knob (RTW_COOP=0): plain per-lane loop, same results
-        if (active) seq_reject<D>(rng, out);
-        return;
-    }
-    const uint32_t lane = __lane_id();
-    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
-    uint64_t pend = __ballot(active);
-    if (!pend) return;
-    const uint64_t s0 = rng.s;
-    uint32_t base = 0;
-    while (pend) {
-        const uint32_t n = (uint32_t)__popcll(pend);
-        const uint32_t k = 64u / n;
-        const bool me = (pend >> lane) & 1ull;
-        const uint32_t rank = (uint32_t)__popcll(pend & lt);
-        if (me) slot[rank] = lane;
-        __builtin_amdgcn_wave_barrier();
-        const uint32_t tr = lane / k;
-        const bool helper = tr < n;
-        const uint32_t tl = helper ? slot[tr] : lane;
-        const uint32_t ts_lo = __shfl((uint32_t)s0, (int)tl), ts_hi = __shfl((uint32_t)(s0 >> 32), (int)tl);
-        const uint32_t tj = (uint32_t)__shfl((int)base, (int)tl) + (lane - tr * k);
-        float v[D];
-        bool acc = false;
-        if (helper) {
-            rtw_rng c;
-            c.s = (((uint64_t)ts_hi << 32) | ts_lo) + (uint64_t)(tj * (uint32_t)D) * RTW_GOLDEN;
-#pragma unroll
-            for (int d = 0; d < D; d++) v[d] = rtw_path_range(c, -1, 1);
-            float ls;
-            if constexpr (D == 3) ls = v[0] * v[0] + v[1] * v[1] + v[2] * v[2];
-            else ls = v[0] * v[0] + v[1] * v[1];  // + 0*0 of the disk's z (exact)
-            acc = ls < 1.0f;
-        } else {
-#pragma unroll
-            for (int d = 0; d < D; d++) v[d] = 0.0f;
-        }
-        const uint64_t accb = __ballot(acc);
-        const uint32_t off = me ? rank * k : 0u;
-        const uint64_t m = (k >= 64u) ? ~0ull : ((1ull << k) - 1ull);
-        const uint64_t a = me ? ((accb >> off) & m) : 0ull;
-        const uint32_t fa = a ? (uint32_t)__builtin_ctzll(a) : 64u;
-        const int src = (int)((me && fa < 64u) ? off + fa : lane);
-        float got[D];
-#pragma unroll
-        for (int d = 0; d < D; d++) got[d] = __shfl(v[d], src);
-        bool done = !me;
-        if (me) {
-            if (fa < 64u) {
-#pragma unroll
-                for (int d = 0; d < D; d++) out[d] = got[d];
-                rng.s = s0 + (uint64_t)((base + fa + 1u) * (uint32_t)D) * RTW_GOLDEN;
-                done = true;
-            } else {
-                base += k;
-            }
-        }
-        __builtin_amdgcn_wave_barrier();  // slot[] is rewritten next round
-        pend = __ballot(!done);
-    }
-}
-
-// Camera.getRay for every lane of the wave (`active` lanes get a ray), the
-// defocus disk's rejection loop wave-cooperatively (coop_reject): the same draws
-// in the same order as get_ray.  Must be called with the wave converged.
-__device__ __forceinline__ Ray get_ray_wave(const rtw_launch& L, bool active, uint32_t i, uint32_t j, rtw_rng& rng,
-                                            uint32_t* slot) {
+// Camera.getRay for every lane of the wave (`active` lanes get a ray): the same
+// draws in the same order as get_ray, the disk's rejection loop outside the
+// per-lane branch (one loop for the wave).
+__device__ __forceinline__ Ray get_ray_wave(const rtw_launch& L, bool active, uint32_t i, uint32_t j, rtw_rng& rng) {
     const f3 du = ld3(L.du), dv = ld3(L.dv);
     f3 pixel_sample = mk(0, 0, 0);
     if (active) {
@@ -1092,7 +971,7 @@ __device__ __forceinline__ Ray get_ray_wave(const rtw_launch& L, bool active, ui
     f3 origin = ld3(L.center);
     if (L.defocus_angle > 0) {
         float dsk[2] = {0.0f, 0.0f};
-        coop_reject<2>(active, rng, dsk, slot, (L.coop & 2u) != 0);
+        if (active) seq_reject<2>(rng, dsk);
         origin = (origin + ld3(L.disk_u) * splat(dsk[0])) + ld3(L.disk_v) * splat(dsk[1]);
     }
     Ray r;

@@ -135,8 +135,39 @@ int rtw_camera_init(const rtw_camera_params* p, rtw_camera* c) {
     return RTW_OK;
 }
 
+void rtw_tuning_defaults(rtw_tuning* t) {
+    if (!t) return;
+    std::memset(t, 0, sizeof *t);
+    t->kernel = RTW_KERNEL_WAVEFRONT;
+    t->bvh_orders = 0;
+    t->sah_max_leaf = 1;
+    t->compact_nodes = 1;
+    t->fast_box = 1;
+    t->fast_reject = 1;
+    t->lds = RTW_LDS_ALL;
+    t->fuse = RTW_FUSE_STEP | RTW_FUSE_TAIL_LDS;
+    t->wf_iters = 9;  // C2 at 9/12/16/24 iterations: 7.02/7.00/6.92/6.78x at 8 ranks; 1 GPU flat
+    t->mega_shade_min = 48;  // tuned on C2: 8..64 -> 48 best
+    t->mega_waves = 1;
+    t->mega_tile_order = 1;
+    t->wf_paths = 0;
+}
+
 int rtw_scene_create(const rtw_scene_desc* d, int device, rtw_ctx** out) {
+    return rtw_scene_create_ex(d, device, nullptr, out);
+}
+
+int rtw_scene_create_ex(const rtw_scene_desc* d, int device, const rtw_tuning* tuning, rtw_ctx** out) {
     if (!d || !out) return fail(RTW_E_INVALID, "null scene desc");
+    rtw_tuning tu;
+    rtw_tuning_defaults(&tu);
+    if (tuning) tu = *tuning;
+    if (tu.kernel > RTW_KERNEL_SIMPLE) return fail(RTW_E_INVALID, "tuning.kernel out of range");
+    if (tu.bvh_orders != 0 && tu.bvh_orders != 1 && tu.bvh_orders != 8) return fail(RTW_E_INVALID, "tuning.bvh_orders must be 0, 1 or 8");
+    if (tu.wf_iters < 1 || tu.wf_iters > RTW_WF_MAX_ITERS) return fail(RTW_E_INVALID, "tuning.wf_iters out of range");
+    if (tu.mega_shade_min < 1 || tu.mega_shade_min > 64) return fail(RTW_E_INVALID, "tuning.mega_shade_min out of range");
+    if (tu.mega_waves != 1 && tu.mega_waves != 6 && tu.mega_waves != 8) return fail(RTW_E_INVALID, "tuning.mega_waves must be 1, 6 or 8");
+    if (tu.wf_paths && tu.wf_paths < 4096) return fail(RTW_E_INVALID, "tuning.wf_paths must be 0 or >= 4096");
     *out = nullptr;
     if ((d->n_spheres && !d->spheres) || (d->objects ? d->n_objects : d->n_spheres) == 0)
         return fail(RTW_E_INVALID, "scene has no objects");
@@ -173,8 +204,9 @@ int rtw_scene_create(const rtw_scene_desc* d, int device, rtw_ctx** out) {
     // lanes walking different orders stop executing them together (Cornell: -31 % with 8 orders).
     const bool objects = d->n_quads || d->n_instances || d->n_media;
     uint32_t orders = (d->bvh_mode == RTW_BVH_SAH && !objects) ? 8u : 1u;
-    if (const char* o = std::getenv("RTW_ORDERS")) orders = (d->bvh_mode == RTW_BVH_SAH && std::atoi(o) == 8) ? 8u : 1u;
-    int rc = rtw_build_bvh(*d, ctx->nodes_host, geom, &depth, &draws, &ctx->box_pad, &ctx->extent, orders);
+    if (tu.bvh_orders) orders = (d->bvh_mode == RTW_BVH_SAH && tu.bvh_orders == 8) ? 8u : 1u;
+    int rc = rtw_build_bvh(*d, ctx->nodes_host, geom, &depth, &draws, &ctx->box_pad, &ctx->extent, orders,
+                           tu.sah_max_leaf);
     if (rc != RTW_OK) {
         delete ctx;
         return fail(rc, "BVH build failed (bad object graph or bvh_mode)");
@@ -184,12 +216,11 @@ int rtw_scene_create(const rtw_scene_desc* d, int device, rtw_ctx** out) {
         return fail(RTW_E_INVALID, "scenes with instances are limited to 2^24 BVH nodes");
     }
     const std::vector<float>& cvec = geom.cvec;
-    // compact 16-B walk for static sphere SAH trees (rtw_compact_nodes); RTW_COMPACT=0 disables
+    // compact 16-B walk for static sphere SAH trees (rtw_compact_nodes)
     std::vector<rtw_cnode> cnodes;
     {
-        bool want = d->bvh_mode == RTW_BVH_SAH && !objects && ctx->box_pad > 0;
+        bool want = d->bvh_mode == RTW_BVH_SAH && !objects && ctx->box_pad > 0 && tu.compact_nodes;
         for (uint32_t i = 0; want && i < d->n_spheres; i++) want = !d->spheres[i].is_moving;
-        if (const char* c = std::getenv("RTW_COMPACT")) want = want && std::atoi(c) != 0;
         if (want && !rtw_compact_nodes(ctx->nodes_host, orders, cnodes)) cnodes.clear();
     }
 
@@ -312,8 +343,7 @@ int rtw_scene_create(const rtw_scene_desc* d, int device, rtw_ctx** out) {
     ctx->feat = scene_features(d) | geom.feat;
     L.feat = ctx->feat;
     L.work_counter = ctx->d_work;
-    if (const char* kv = std::getenv("RTW_KERNEL"))
-        ctx->variant = (std::strcmp(kv, "v0") == 0) ? 0 : (std::strcmp(kv, "v1") == 0) ? 1 : 2;
+    ctx->variant = tu.kernel == RTW_KERNEL_WAVEFRONT ? 2 : tu.kernel == RTW_KERNEL_PERSISTENT ? 1 : 0;
     {
         // wavefront batch capacity: up to 2^29 paths (BASELINE config 2 = 480M samples in one
         // batch: one drain of long paths per render instead of one per 64M), within ~35 % of
@@ -323,80 +353,43 @@ int rtw_scene_create(const rtw_scene_desc* d, int device, rtw_ctx** out) {
         uint64_t cap = 1ull << 29;
         if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b)
             cap = std::min<uint64_t>(cap, (uint64_t)(0.35 * (double)free_b) / RTW_WF_PATH_BYTES);
-        ctx->wf_max_paths = std::max<uint64_t>(cap, 1u << 20);
+        ctx->wf_max_paths = tu.wf_paths ? tu.wf_paths : std::max<uint64_t>(cap, 1u << 20);
     }
-    if (const char* wp = std::getenv("RTW_WF_PATHS")) {
-        long long v = std::atoll(wp);
-        if (v >= 4096) ctx->wf_max_paths = (uint64_t)v;
-    }
-    if (const char* wi = std::getenv("RTW_WF_ITERS")) {
-        int v = std::atoi(wi);
-        ctx->wf_iters = (uint32_t)(v < 1 ? 1 : (v > RTW_WF_MAX_ITERS ? RTW_WF_MAX_ITERS : v));
-    }
+    ctx->wf_iters = tu.wf_iters;
     {
         int n_cu = 0;
         if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || n_cu < 1)
             n_cu = 256;
         ctx->n_cu = n_cu;
     }
-    if (const char* sm = std::getenv("RTW_SHADE_MIN")) {
-        int v = std::atoi(sm);
-        ctx->shade_min = (uint32_t)(v < 1 ? 1 : (v > 64 ? 64 : v));
-    }
-    L.shade_min = ctx->shade_min;
-    L.waves = 1;
-    L.tile_order = 1;
-    L.fast_reject = 1;  // (an unfiltered variant measured +-0 on C2 and -20 % on C4: its codegen slowed the L1/L2 walk)
-    L.coop = 0;   // wave-cooperative rejection sampling: exact but no gain measured on C2
-    if (const char* cp = std::getenv("RTW_COOP")) L.coop = (uint32_t)std::atoi(cp);
-    if (const char* fr = std::getenv("RTW_FAST_REJECT")) L.fast_reject = (uint32_t)std::atoi(fr);
-    if (const char* to = std::getenv("RTW_TILE_ORDER")) L.tile_order = (uint32_t)std::atoi(to);
-    if (const char* wv = std::getenv("RTW_WAVES")) L.waves = (uint32_t)std::atoi(wv);
-    L.use_lds = orders == 1 ? 1 : 0;  // the octant copies do not fit the megakernel's LDS stage
-    if (const char* ul = std::getenv("RTW_LDS")) L.use_lds = orders == 1 ? (uint32_t)std::atoi(ul) : 0;
+    L.shade_min = tu.mega_shade_min;
+    L.waves = tu.mega_waves;
+    L.tile_order = tu.mega_tile_order ? 1u : 0u;
+    // (an unfiltered variant measured +-0 on C2 and -20 % on C4: its codegen slowed the L1/L2 walk)
+    L.fast_reject = tu.fast_reject ? 1u : 0u;
+    L.use_lds = orders == 1 && (tu.lds & RTW_LDS_MEGA_NODES) ? 1u : 0u;  // the octant copies do not fit the megakernel's stage
     // wavefront trace: node array staged in LDS when one ordering fits (object scenes,
     // reference trees; +2 % on Cornell); the 8 octant copies of SAH sphere trees do not
-    L.wf_lds = 1;
+    L.wf_lds = (tu.lds & RTW_LDS_NODES) ? 1u : 0u;
     // small static sphere SAH trees: the compact nodes of all 8 orders in LDS (C2: +1 %)
-    L.wf_clds = 1;
-    if (const char* cl = std::getenv("RTW_WF_CLDS")) L.wf_clds = (uint32_t)std::atoi(cl);
-    if (const char* wl = std::getenv("RTW_WF_LDS")) L.wf_lds = (uint32_t)std::atoi(wl);
+    L.wf_clds = (tu.lds & RTW_LDS_CNODES) ? 1u : 0u;
     // compact LDS stage: gen, trace and shade of an iteration fused in one kernel
     // (the ray/hit hand-off through HBM disappears), tail on the LDS stage
-    L.wf_fuse = 3;
-    if (const char* fu = std::getenv("RTW_WF_FUSE")) L.wf_fuse = (uint32_t)std::atoi(fu);
+    L.wf_fuse = tu.fuse;
     // Perlin tables (7 KiB each) staged in LDS by the fused step when at most 4 (noise scenes)
-    L.perlin_lds = (ctx->feat & RTW_F_NOISE) && d->n_perlins <= 4 ? 1u : 0u;
-    if (const char* pl = std::getenv("RTW_PERLIN_LDS")) L.perlin_lds = L.perlin_lds && std::atoi(pl) != 0;
-    // quads, instance member lists and instances of small object scenes (Cornell: ~2 KiB) staged in LDS
-    // with the node array: the member loop's loads stop waiting on L1
+    L.perlin_lds = (ctx->feat & RTW_F_NOISE) && d->n_perlins <= 4 && (tu.lds & RTW_LDS_PERLIN) ? 1u : 0u;
     // materials of sphere scenes staged in LDS by the compact-LDS fused step when they fit beside the
     // nodes (wf_run_fused checks the total): hit_prep's material load stops waiting on L1/L2
-    L.mat_lds = (uint32_t)((d->n_materials * sizeof(rtw_dev_material) + 15) & ~size_t(15));
-    if (const char* ml = std::getenv("RTW_MAT_LDS")) L.mat_lds = std::atoi(ml) != 0 ? L.mat_lds : 0u;
+    L.mat_lds = (tu.lds & RTW_LDS_MATERIALS) ? (uint32_t)((d->n_materials * sizeof(rtw_dev_material) + 15) & ~size_t(15)) : 0u;
     const size_t shade_bytes = (size_t)(o_perl - o_mats);
-    L.shade_lds = shade_bytes <= 8192 ? (uint32_t)shade_bytes : 0u;
-    if (const char* sl = std::getenv("RTW_SHADE_LDS")) L.shade_lds = std::atoi(sl) != 0 ? L.shade_lds : 0u;
+    L.shade_lds = shade_bytes <= 8192 && (tu.lds & RTW_LDS_SHADE) ? (uint32_t)shade_bytes : 0u;
+    // quads, instance member lists and instances of small object scenes (Cornell: ~2 KiB) staged in LDS
+    // with the node array: the member loop's loads stop waiting on L1
     const size_t geom_bytes = (size_t)(o_med - o_quad);
-    L.geom_lds = (ctx->feat & RTW_F_GEOM) && geom_bytes <= 16384 ? (uint32_t)geom_bytes : 0u;
-    if (const char* gl = std::getenv("RTW_GEOM_LDS")) L.geom_lds = std::atoi(gl) != 0 ? L.geom_lds : 0u;
-    // SAH trees: FMA slab test on the padded boxes + leaf postponement (both only
-    // enlarge the set of visited nodes; reference trees keep the exact aabb.zig walk)
-    const bool sah = ctx->box_pad > 0;
-    L.fast_box = sah ? 1 : 0;
-    L.postpone = 0;  // measured: no gain in v1; wavefront trace: see RTW_POSTPONE A/B
-    L.leaf_min = 32;
-    L.refill_min = 0;
-    if (const char* rm = std::getenv("RTW_REFILL_MIN")) {
-        int v = std::atoi(rm);
-        L.refill_min = (uint32_t)(v < 0 ? 0 : (v > 64 ? 64 : v));
-    }
-    if (const char* fb = std::getenv("RTW_FASTBOX")) L.fast_box = sah && std::atoi(fb) != 0;
-    if (const char* pp = std::getenv("RTW_POSTPONE")) L.postpone = (uint32_t)std::atoi(pp);
-    if (const char* lm = std::getenv("RTW_LEAF_MIN")) {
-        int v = std::atoi(lm);
-        L.leaf_min = (uint32_t)(v < 1 ? 1 : (v > 64 ? 64 : v));
-    }
+    L.geom_lds = (ctx->feat & RTW_F_GEOM) && geom_bytes <= 16384 && (tu.lds & RTW_LDS_GEOMETRY) ? (uint32_t)geom_bytes : 0u;
+    // SAH trees: FMA slab test on the padded boxes (only enlarges the set of visited nodes;
+    // reference trees keep the exact aabb.zig walk)
+    L.fast_box = ctx->box_pad > 0 && tu.fast_box ? 1u : 0u;
     ctx->grid = rtw_persistent_grid(ctx->feat, (uint32_t)n_nodes, (int)L.waves, L.use_lds != 0);
 
     ctx->stats.n_nodes = (uint32_t)n_nodes;
@@ -829,17 +822,6 @@ int rtw_debug_sample(rtw_ctx* ctx, const rtw_camera* cam, uint64_t seed, uint32_
     HIP_TRY(hipGetLastError());
     float tmp[32];
     HIP_TRY(hipMemcpyAsync(tmp, ctx->d_dbg, sizeof tmp, hipMemcpyDeviceToHost, ctx->stream));
-    if (const char* dbg = std::getenv("RTW_DEBUG_FILTER")) {
-        (void)dbg;
-        if (tmp[8] != 0)
-            std::fprintf(stderr, "filter miss: node %g hb %.9g c %.9g disc %.9g sq %.9g sa %.9g a %.9g rcp %.9g r1 %.9g r2 %.9g q1 %.9g q2 %.9g e %.9g\n",
-                         tmp[9], tmp[10], tmp[11], tmp[12], tmp[13], tmp[14], tmp[15], tmp[16], tmp[17], tmp[18], tmp[19], tmp[20], tmp[21]);
-        else
-            std::fprintf(stderr, "filter ok\n");
-        if (tmp[22] != 0)
-            std::fprintf(stderr, "closest mismatch at bounce %g: trav hit %g t %.9g brute hit %g t %.9g origin %.9g %.9g %.9g\n",
-                         tmp[23], tmp[24], tmp[25], tmp[26], tmp[27], tmp[28], tmp[29], tmp[30]);
-    }
     HIP_TRY(hipStreamSynchronize(ctx->stream));
     out[0] = tmp[0];
     out[1] = tmp[1];

@@ -58,12 +58,8 @@ struct rtw_launch {
     uint32_t waves;              // launch-bound variant (min waves per SIMD): 1, 6 or 8
     uint32_t tile_order;         // 1 = last tile row first (default), 0 = first row first
     uint32_t use_lds;            // 1 = stage the BVH in LDS when it fits (default), 0 = read nodes from L1/L2
-    uint32_t coop;               // wave-cooperative rejection sampling: bit 0 unit sphere (shading), bit 1 disk (camera; v1: any bit)
     uint32_t fast_reject;        // 1 = exact sphere fast-reject filter (default), 0 = always the IEEE path
     uint32_t fast_box;           // 1 = FMA slab test on padded boxes (SAH trees only), 0 = aabb.zig arithmetic
-    uint32_t postpone;           // 1 = postpone leaf tests until leaf_min/64 of the walking lanes hold one
-    uint32_t leaf_min;           // postponement threshold in 1/64ths of the walking lanes
-    uint32_t refill_min;         // wavefront trace: refill idle lanes once >= refill_min are idle (0 = off)
     uint32_t n_orders;           // 1, or 8 octant-ordered copies of the node array (SAH sphere scenes)
     uint32_t wf_lds;             // wavefront trace: stage the node array(s) in LDS when they fit
     uint32_t wf_clds;            // wavefront trace: stage the compact nodes (all orders) in LDS when they fit
@@ -94,7 +90,7 @@ struct rtw_launch {
 #define RTW_F_ALL 127u
 
 // max nodes staged in LDS by the persistent kernel (48 KiB)
-#define RTW_LDS_NODES 1536
+#define RTW_MEGA_LDS_NODES_MAX 1536
 
 struct rtw_kernel_info {
     int blocks_per_cu;
@@ -166,7 +162,7 @@ bool rtw_compact_nodes(const std::vector<rtw_node>& nodes, uint32_t orders, std:
 
 int rtw_build_bvh(const rtw_scene_desc& desc, std::vector<rtw_node>& nodes, rtw_geometry& geom,
                   uint32_t* depth, uint32_t* axis_draws, float* box_pad = nullptr, float* extent = nullptr,
-                  uint32_t orders = 1);
+                  uint32_t orders = 1, uint32_t sah_max_leaf = 1);
 
 // One scene on one device (the opaque rtw_ctx of include/rtw_gpu.h).
 struct rtw_ctx {
@@ -183,12 +179,11 @@ struct rtw_ctx {
     uint32_t* d_work = nullptr;    // persistent-kernel work counter (zeroed before each launch)
     uint32_t feat = 0;             // RTW_F_* scene features
     int grid = 0;                  // resident blocks of the persistent kernel
-    int variant = 2;               // 2 = wavefront v2 (default), 1 = persistent v1, 0 = simple v0 (RTW_KERNEL)
-    uint32_t shade_min = 48;       // RTW_SHADE_MIN (tuned on C2: 8..64 -> 48 best)
+    int variant = 2;               // 2 = wavefront v2 (default), 1 = persistent v1, 0 = simple v0 (rtw_tuning.kernel)
     void* d_wf = nullptr;          // wavefront path state (rtw_wavefront.h), wf_cap paths
     uint64_t wf_cap = 0;
-    uint64_t wf_max_paths = 1u << 26;  // RTW_WF_PATHS: paths per wavefront batch (x RTW_WF_PATH_BYTES); set at scene creation
-    uint32_t wf_iters = 9;         // RTW_WF_ITERS: wavefront bounces before the tail kernel
+    uint64_t wf_max_paths = 1u << 26;  // paths per wavefront batch (x RTW_WF_PATH_BYTES); set at scene creation
+    uint32_t wf_iters = 9;         // wavefront bounces before the tail kernel (rtw_tuning.wf_iters)
     int n_cu = 256;                // compute units of the device (wavefront grids)
     std::vector<hipEvent_t> ev_pool;  // recycled timing events
     uint64_t scene_hash = 0;       // FNV-1a 64 of the uploaded scene image

@@ -57,7 +57,7 @@ __global__ __launch_bounds__(256) void render_pixels_v0(rtw_launch L) {
 //  * traversal runs node steps until >= shade_min lanes have finished their
 //    walk (ballot popcount), then shades only those lanes: the wave's shading
 //    pass is shared by many lanes instead of one;
-//  * the BVH (<= RTW_LDS_NODES nodes) is staged once per block in LDS.
+//  * the BVH (<= RTW_MEGA_LDS_NODES_MAX nodes) is staged once per block in LDS.
 // ---------------------------------------------------------------------------
 enum : uint32_t { ST_TRAV = 0, ST_SHADE = 1, ST_NEWSAMPLE = 2, ST_NEWPIXEL = 3, ST_DONE = 4 };
 
@@ -90,8 +90,6 @@ __global__ __launch_bounds__(256, WAVES) void render_persistent_v1(rtw_launch L)
     const uint32_t lane = __lane_id();
     const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     const uint32_t n_nodes = L.n_nodes;
-    __shared__ uint32_t coop_slots[4][64];  // per-wave scratch of coop_reject (1 KiB, multiple of 16 B)
-    uint32_t* const coop_slot = coop_slots[threadIdx.x >> 6];
 
     // wave-uniform queue state
     uint32_t q_cur = 0, q_end = 0;
@@ -111,7 +109,6 @@ __global__ __launch_bounds__(256, WAVES) void render_persistent_v1(rtw_launch L)
     uint32_t depth = 0, ti = 0;
     float closest = kInf;
     int hit = -1;
-    int pend = -1;  // parked leaf (leaf postponement), -1 = none
     const float4* nb = nodes;  // this lane's node array (octant copy, order_base)
     uint32_t oct = 0;
     Counters cnt;
@@ -176,7 +173,7 @@ __global__ __launch_bounds__(256, WAVES) void render_persistent_v1(rtw_launch L)
         STAMP(t1) STAMP_ADD(c_assign, t0, t1)
 
         // ---- 2. start a new sample: getRay (camera.zig:169-180).  Jitter draws
-        // per lane, the defocus-disk rejection loop wave-cooperatively, then time.
+        // per lane, the defocus-disk rejection loop, then time.
         {
             const bool starting = st == ST_NEWSAMPLE;
             f3 pixel_sample = mk(0, 0, 0);
@@ -190,7 +187,7 @@ __global__ __launch_bounds__(256, WAVES) void render_persistent_v1(rtw_launch L)
             }
             float dsk[2] = {0.0f, 0.0f};
             const bool defocus = L.defocus_angle > 0;
-            if (defocus) coop_reject<2>(starting, rng, dsk, coop_slot, L.coop != 0);
+            if (defocus && starting) seq_reject<2>(rng, dsk);
             if (starting) {
                 f3 origin = ld3(L.center);
                 if (defocus) origin = (origin + ld3(L.disk_u) * splat(dsk[0])) + ld3(L.disk_v) * splat(dsk[1]);
@@ -226,45 +223,11 @@ __global__ __launch_bounds__(256, WAVES) void render_persistent_v1(rtw_launch L)
                 if (!trav) break;
                 if (popc64(__ballot(st == ST_SHADE)) >= want) break;
                 // RTW_STEPS node steps per readiness check (amortises the ballot/branch bookkeeping)
-                if (L.postpone) {
-                    // Leaf postponement (Aila & Laine 2009 "while-while"): a lane that
-                    // reaches a leaf parks it and waits; inner steps run for the others
-                    // until leaf_min/64 of the walking lanes hold one, then all parked
-                    // leaves are tested in one pass -- the wave no longer executes both
-                    // the box and the sphere code on every step.  Leaves are still
-                    // tested in walk order per lane; boxes passed meanwhile saw a
-                    // larger `closest` (superset of visits, same closest hit).
-                    if (st == ST_TRAV && pend < 0) {
-                        float4 A, B;
-                        load_node(nb, ti, A, B);
-                        const uint32_t w = fbits(A.w);
-                        if (w & RTW_LEAF_BIT) {
-                            pend = (int)ti;
-                            ti = w & RTW_SKIP_MASK;
-                        } else {
-                            cnt.nodes++;
-                            ti = box_next(ray, rt, A, B, ti, closest, L.fast_box != 0);
-                            if (ti >= n_nodes) st = ST_SHADE;
-                        }
-                    }
-                    const uint32_t n_walk = popc64(__ballot(st == ST_TRAV));
-                    const uint32_t n_park = popc64(__ballot(st == ST_TRAV && pend >= 0));
-                    if (n_park && (n_park == n_walk || n_park * 64u >= n_walk * L.leaf_min)) {
-                        if (st == ST_TRAV && pend >= 0) {
-                            float4 A, B;
-                            load_node(nb, (uint32_t)pend, A, B);
-                            leaf_test<FEAT>(L, ray, rt, A, B, (uint32_t)pend, closest, hit, cnt, rng.s);
-                            pend = -1;
-                            if (ti >= n_nodes) st = ST_SHADE;
-                        }
-                    }
-                } else {
 #pragma unroll
-                    for (int u = 0; u < RTW_STEPS; u++) {
-                        if (st == ST_TRAV) {
-                            ti = trav_step<FEAT>(nb, L, ray, rt, ti, closest, hit, cnt, rng.s);
-                            if (ti >= n_nodes) st = ST_SHADE;
-                        }
+                for (int u = 0; u < RTW_STEPS; u++) {
+                    if (st == ST_TRAV) {
+                        ti = trav_step<FEAT>(nb, L, ray, rt, ti, closest, hit, cnt, rng.s);
+                        if (ti >= n_nodes) st = ST_SHADE;
                     }
                 }
 #if defined(RTW_STAMPS)
@@ -278,7 +241,7 @@ __global__ __launch_bounds__(256, WAVES) void render_persistent_v1(rtw_launch L)
 #endif
 
         // ---- 4. shade lanes whose walk is complete: hit record per lane, the
-        // randomUnitVector rejection loop wave-cooperatively, then the material.
+        // randomUnitVector rejection loop of the lanes that need it, then the material.
         {
             const bool shading = st == ST_SHADE;
             HitPrep hp;
@@ -288,7 +251,7 @@ __global__ __launch_bounds__(256, WAVES) void render_persistent_v1(rtw_launch L)
                 need_uv = needs_unit_vector<FEAT>(hp.m.kind);
             }
             float ruv3[3] = {0.0f, 0.0f, 0.0f};
-            coop_reject<3>(need_uv, rng, ruv3, coop_slot, L.coop != 0);
+            if (need_uv) seq_reject<3>(rng, ruv3);
             if (shading) {
                 bool cont = false;
                 if (hit == -1) {
@@ -471,7 +434,7 @@ void rtw_launch_render(const rtw_launch& L, void* stream, int variant, int grid)
         hipLaunchKernelGGL(render_pixels_v0, g, block, 0, st, L);
         return;
     }
-    const bool lds = L.n_nodes <= RTW_LDS_NODES && L.use_lds;
+    const bool lds = L.n_nodes <= RTW_MEGA_LDS_NODES_MAX && L.use_lds;
     const int w = (int)L.waves;
     switch (pick_feat(L.feat)) {
     case 0u:
@@ -491,7 +454,7 @@ int rtw_persistent_grid(uint32_t feat, uint32_t n_nodes, int waves, bool use_lds
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
     if (n_cu <= 0) n_cu = 256;
-    const bool lds = n_nodes <= RTW_LDS_NODES && use_lds;
+    const bool lds = n_nodes <= RTW_MEGA_LDS_NODES_MAX && use_lds;
     const size_t bytes = (size_t)n_nodes * 32;
     int b;
     switch (pick_feat(feat)) {

@@ -220,83 +220,6 @@ __global__ __launch_bounds__(256) void wf_trace(rtw_launch L, rtw_wf W, uint32_t
         flush_counters(L, cnt, 0);
         return;
     }
-    if (L.refill_min) {
-        // per-lane refill: a lane whose walk is done takes the wave's next ray
-        // once refill_min lanes are idle (the refill stalls the wave on the loads)
-        const uint32_t lane = __lane_id();
-        const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-        const bool fast = L.fast_box != 0;
-        uint32_t cursor = 0, slot = 0, ti = 0;
-        uint64_t mkey = 0;
-        const float4* nb = L.nodes;
-        uint32_t oct = 0;
-        bool active = false, exhausted = false;
-        Ray r;
-        r.o = r.d = mk(0, 0, 0);
-        r.time = 0;
-        RayTrav rt = ray_trav(r, false);
-        float closest = kInf;
-        int hit = -1;
-        for (;;) {
-            const uint64_t idle = __ballot(!active);
-            const uint32_t n_idle = (uint32_t)__popcll(idle);
-            if (!exhausted && (n_idle >= L.refill_min || n_idle == 64)) {
-                const uint32_t m = cursor + (uint32_t)__popcll(idle & lt);
-                cursor += n_idle;
-                bool end = false;
-                uint32_t q = 0;
-                const bool ok = wf_nth(W, it, m, q, end);
-                exhausted = __ballot(end && !active) == idle;  // every idle lane ran past the list
-                if (!active && ok) {
-                    uint32_t depth;
-                    r = wf_load_ray(S, q, depth);
-                    if (depth) {
-                        slot = q;
-                        mkey = wf_mkey<FEAT>(S, q);
-                        oct = order_of(L, r);
-                        nb = order_base(L.nodes, L, oct);
-                        rt = ray_trav(r, fast);
-                        ti = 0;
-                        closest = kInf;
-                        hit = -1;
-                        active = true;
-                        cnt.rays++;
-                    }
-                }
-            }
-            if (!__ballot(active)) {
-                if (exhausted) break;
-                continue;
-            }
-            if (active) {
-                ti = trav_step<FEAT>(nb, L, r, rt, ti, closest, hit, cnt, mkey);
-                if (ti >= L.n_nodes) {
-                    W.hit[slot] = make_float2(closest, __int_as_float(hit_with_order(hit, oct)));
-                    active = false;
-                }
-            }
-        }
-        flush_counters(L, cnt, 0);
-        return;
-    }
-    if (L.postpone) {
-        for (WfIter e(W, it); e.more(); e.next()) {
-            uint32_t slot, depth = 0;
-            Ray r;
-            r.o = r.d = mk(0, 0, 0);
-            r.time = 0;
-            if (e.get(W, slot)) r = wf_load_ray(S, slot, depth);
-            float t;
-            const int h = traverse_postponed<FEAT>(L.nodes, L, r, depth != 0, t, cnt,
-                                                   depth ? wf_mkey<FEAT>(S, slot) : 0);
-            if (depth) {
-                W.hit[slot] = make_float2(t, __int_as_float(h));
-                cnt.rays++;
-            }
-        }
-        flush_counters(L, cnt, 0);
-        return;
-    }
     for (WfIter e(W, it); e.more(); e.next()) {
         uint32_t slot;
         if (e.get(W, slot)) {
@@ -538,9 +461,6 @@ __global__ __launch_bounds__(1024) void wf_tail_clds(rtw_launch L, rtw_wf W, uin
     wf_tail_body<FEAT, true>(L, W, it, wf_clds);
 }
 
-// dynamic LDS of the fused kernels: tree stage + 64 u32 of coop_reject scratch per wave
-#define RTW_WF_COOP_LDS(threads) ((threads) / 64u * 256u)
-
 // Where the fused step's walk reads the tree:
 //   WALK_CLDS   the compact nodes of every octant copy staged in LDS (small static sphere SAH trees, C2)
 //   WALK_LDS    the 32-B node array of one ordering staged in LDS (small object scenes: Cornell)
@@ -571,8 +491,7 @@ __device__ __forceinline__ int wf_walk(const rtw_launch& L, const void* lds, con
 // previous iteration, or by the host for it = 0) and zeroes len[(it+2)%3],
 // iteration it-1's input, for the next iteration.
 template <uint32_t FEAT, int WALK>
-__device__ __forceinline__ void wf_step_body(const rtw_launch& L, const rtw_wf& W, uint32_t it, const void* lds,
-                                             uint32_t* coop_slot) {
+__device__ __forceinline__ void wf_step_body(const rtw_launch& L, const rtw_wf& W, uint32_t it, const void* lds) {
     const rtw_wf_set& S = W.set[it & 1u];
     const rtw_wf_set& O = W.set[(it + 1u) & 1u];
     Counters cnt;
@@ -596,7 +515,7 @@ __device__ __forceinline__ void wf_step_body(const rtw_launch& L, const rtw_wf& 
                 else W.ls[slot] = make_float4(0, 0, 0, 0);  // rayColor(r, 0) = 0
             }
             if constexpr ((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM)) == 0) {
-                r = get_ray_wave(L, live, x + L.pixel_offset, y + L.pixel_offset, rng, coop_slot);
+                r = get_ray_wave(L, live, x + L.pixel_offset, y + L.pixel_offset, rng);
             } else {
                 if (live) r = get_ray(L, x + L.pixel_offset, y + L.pixel_offset, rng);
             }
@@ -613,7 +532,7 @@ __device__ __forceinline__ void wf_step_body(const rtw_launch& L, const rtw_wf& 
         Ray sc;
         if constexpr ((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM)) == 0) {
             // sphere scenes: hit record, then the randomUnitVector draw of every lane
-            // that needs one (wave-cooperatively with RTW_COOP=1), then the material --
+            // that needs one (one rejection loop for the wave), then the material --
             // measured faster than the nested form below (C2 +6 %, C5 +3 %)
             HitPrep hp;
             bool hitp = false, need_uv = false;
@@ -630,7 +549,7 @@ __device__ __forceinline__ void wf_step_body(const rtw_launch& L, const rtw_wf& 
                 }
             }
             float uv3[3] = {0.0f, 0.0f, 0.0f};
-            coop_reject<3>(need_uv, rng, uv3, coop_slot, (L.coop & 1u) != 0);
+            if (need_uv) seq_reject<3>(rng, uv3);
             if (hitp) {
                 const f3 ruv = need_uv ? unit_vector(mk(uv3[0], uv3[1], uv3[2])) : mk(0, 0, 0);
                 f3 att;
@@ -681,26 +600,24 @@ __global__ __launch_bounds__(1024) void wf_step_clds(rtw_launch L, rtw_wf W, uin
     wf_step_zero_next(W, it);
     extern __shared__ uint4 wf_clds[];
     stage_clds(L, wf_clds);
-    // per-wave coop_reject scratch after the nodes (the host adds RTW_WF_COOP_LDS(1024) bytes)
-    uint32_t* coop = reinterpret_cast<uint32_t*>(wf_clds + L.n_nodes * L.n_orders) + 64u * (threadIdx.x >> 6);
-    if (L.mat_lds) {  // the materials after the coop scratch (the host checked that they fit)
-        uint4* ml = wf_clds + L.n_nodes * L.n_orders + RTW_WF_COOP_LDS(1024u) / 16u;
+    if (L.mat_lds) {  // the materials after the nodes (the host checked that they fit)
+        uint4* ml = wf_clds + L.n_nodes * L.n_orders;
         const uint4* src = reinterpret_cast<const uint4*>(L.mats);
         for (uint32_t k = threadIdx.x; k < L.mat_lds / 16u; k += 1024u) ml[k] = src[k];
         __syncthreads();
         rtw_launch Lm = L;
         Lm.mats = reinterpret_cast<const rtw_dev_material*>(ml);
-        wf_step_body<FEAT, WALK_CLDS>(Lm, W, it, wf_clds, coop);
+        wf_step_body<FEAT, WALK_CLDS>(Lm, W, it, wf_clds);
         return;
     }
-    wf_step_body<FEAT, WALK_CLDS>(L, W, it, wf_clds, coop);
+    wf_step_body<FEAT, WALK_CLDS>(L, W, it, wf_clds);
 }
 
 // wf_step's LDS extras by mask (bit 0 Perlin tables, 1 materials/textures, 2 geometry); masks a
 // scene class cannot use compile to nothing
 template <uint32_t FEAT, uint32_t MASK>
 __device__ __forceinline__ void wf_step_staged(const rtw_launch& L, const rtw_wf& W, uint32_t it, float4* nodes,
-                                               uint32_t* coop, float4* extra) {
+                                               float4* extra) {
     constexpr bool P = (MASK & 1u) && (FEAT & RTW_F_NOISE), S = (MASK & 2u) != 0, G = (MASK & 4u) && (FEAT & RTW_F_GEOM);
     if constexpr (P || S || G) {
         rtw_launch Lp = L;
@@ -716,7 +633,7 @@ __device__ __forceinline__ void wf_step_staged(const rtw_launch& L, const rtw_wf
         }
         if constexpr (G) Lp = stage_geom(Lp, extra);
         __syncthreads();
-        wf_step_body<FEAT, WALK_LDS>(Lp, W, it, nodes, coop);
+        wf_step_body<FEAT, WALK_LDS>(Lp, W, it, nodes);
     }
 }
 
@@ -726,28 +643,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
     wf_step_zero_next(W, it);
     extern __shared__ float4 wf_lds_nodes[];
     const uint32_t n4 = LDS ? 2u * L.n_nodes * L.n_orders : 0u;
-    uint32_t* coop = reinterpret_cast<uint32_t*>(wf_lds_nodes + n4) + 64u * (threadIdx.x >> 6);
     if constexpr (LDS) {
         for (uint32_t k = threadIdx.x; k < n4; k += 256u) wf_lds_nodes[k] = L.nodes[k];
-        // after the coop scratch: Perlin tables, materials, geometry -- one call per staging mask, so
+        // after the nodes: Perlin tables, materials, geometry -- one call per staging mask, so
         // every pointer the body reads is statically LDS or global (no flat loads)
         const uint32_t mask = (((FEAT & RTW_F_NOISE) && L.perlin_lds) ? 1u : 0u) | (L.shade_lds ? 2u : 0u) |
                               (((FEAT & RTW_F_GEOM) && L.geom_lds) ? 4u : 0u);
-        float4* extra = wf_lds_nodes + n4 + RTW_WF_COOP_LDS(256u) / 16u;
+        float4* extra = wf_lds_nodes + n4;
         switch (mask) {
-            case 1: return wf_step_staged<FEAT, 1>(L, W, it, wf_lds_nodes, coop, extra);
-            case 2: return wf_step_staged<FEAT, 2>(L, W, it, wf_lds_nodes, coop, extra);
-            case 3: return wf_step_staged<FEAT, 3>(L, W, it, wf_lds_nodes, coop, extra);
-            case 4: return wf_step_staged<FEAT, 4>(L, W, it, wf_lds_nodes, coop, extra);
-            case 5: return wf_step_staged<FEAT, 5>(L, W, it, wf_lds_nodes, coop, extra);
-            case 6: return wf_step_staged<FEAT, 6>(L, W, it, wf_lds_nodes, coop, extra);
-            case 7: return wf_step_staged<FEAT, 7>(L, W, it, wf_lds_nodes, coop, extra);
+            case 1: return wf_step_staged<FEAT, 1>(L, W, it, wf_lds_nodes, extra);
+            case 2: return wf_step_staged<FEAT, 2>(L, W, it, wf_lds_nodes, extra);
+            case 3: return wf_step_staged<FEAT, 3>(L, W, it, wf_lds_nodes, extra);
+            case 4: return wf_step_staged<FEAT, 4>(L, W, it, wf_lds_nodes, extra);
+            case 5: return wf_step_staged<FEAT, 5>(L, W, it, wf_lds_nodes, extra);
+            case 6: return wf_step_staged<FEAT, 6>(L, W, it, wf_lds_nodes, extra);
+            case 7: return wf_step_staged<FEAT, 7>(L, W, it, wf_lds_nodes, extra);
             default: break;
         }
         __syncthreads();
-        wf_step_body<FEAT, WALK_LDS>(L, W, it, wf_lds_nodes, coop);
+        wf_step_body<FEAT, WALK_LDS>(L, W, it, wf_lds_nodes);
     } else {
-        wf_step_body<FEAT, WALK_GLOBAL>(L, W, it, nullptr, coop);
+        wf_step_body<FEAT, WALK_GLOBAL>(L, W, it, nullptr);
     }
 }
 
@@ -818,17 +734,17 @@ const WfGrids<FEAT>& wf_grids(int n_cu) {
 //   clds > 0: compact nodes of all orders in LDS (wf_step_clds, 1024 threads)
 //   lds  > 0: the 32-B node array in LDS (wf_step<FEAT, true>)
 //   else    : the tree through L1/L2 (wf_step<FEAT, false>)
-// dynamic LDS of the fused kernels: tree stage + 64 u32 of coop_reject scratch per wave
+// dynamic LDS of the fused kernels: tree stage + what is staged after it
 
 template <uint32_t FEAT>
 void wf_run_fused(const rtw_launch& L, const rtw_wf& W, hipStream_t st, int n_cu, size_t clds, size_t lds,
                   rtw_timer* T) {
-    const size_t cdyn0 = clds + RTW_WF_COOP_LDS(1024),
+    const size_t cdyn0 = clds,
                  cdyn = cdyn0 + L.mat_lds <= 160u * 1024u ? cdyn0 + L.mat_lds : cdyn0,
-                 ldyn = lds + RTW_WF_COOP_LDS(256) + (L.perlin_lds ? (size_t)L.n_perlin * RTW_PERLIN_BYTES : 0) +
+                 ldyn = lds + (L.perlin_lds ? (size_t)L.n_perlin * RTW_PERLIN_BYTES : 0) +
                         ((FEAT & RTW_F_GEOM) ? L.geom_lds : 0u) + L.shade_lds,
                  tdyn = lds + ((FEAT & RTW_F_GEOM) ? L.geom_lds : 0u) + L.shade_lds,
-                 gdyn = RTW_WF_COOP_LDS(256);
+                 gdyn = 0;
     thread_local uint32_t cgrid[2] = {0, 0}, tgrid[2] = {0, 0}, lgrid[2] = {0, 0}, ggrid = 0;
     uint32_t grid = 0;
     if constexpr ((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING)) == 0) {
@@ -903,7 +819,7 @@ void wf_run_fused(const rtw_launch& L, const rtw_wf& W, hipStream_t st, int n_cu
 template <uint32_t FEAT>
 void wf_run(const rtw_launch& L, const rtw_wf& W, hipStream_t st, int n_cu, rtw_timer* T) {
     const WfGrids<FEAT>& g = wf_grids<FEAT>(n_cu);
-    if ((L.wf_fuse & 1u) && !L.refill_min && !L.postpone) {
+    if (L.wf_fuse & 1u) {
         size_t fclds = 0, flds = 0;
         // (textured scenes keep the 32-B node stage: it leaves LDS for the Perlin tables and the
         // 1024-thread compact kernel would spill at its 128-VGPR cap -- C5 -20 % measured)
@@ -926,20 +842,16 @@ void wf_run(const rtw_launch& L, const rtw_wf& W, hipStream_t st, int n_cu, rtw_
     RTW_TIME_END(T)
     const uint32_t iters = L.max_depth < W.iters ? L.max_depth : W.iters;
     const size_t lds_need = (size_t)L.n_nodes * L.n_orders * 32u;
-    const size_t lds = (L.wf_lds && !L.refill_min && !L.postpone && lds_need <= RTW_WF_LDS_MAX)
+    const size_t lds = (L.wf_lds && lds_need <= RTW_WF_LDS_MAX)
                            ? (lds_need + 511u) / 512u * 512u : 0;
     const size_t tlds = lds ? lds + ((FEAT & RTW_F_GEOM) ? L.geom_lds : 0u) : 0;  // + quads/members/instances
     const uint32_t lds_grid = lds ? wf_lds_grid<FEAT>(n_cu, tlds) : 0;
     // compact nodes of every octant copy in LDS (small static sphere trees)
-    const size_t clds = (L.cnodes && L.fast_box && L.wf_clds && !L.refill_min && !L.postpone)
+    const size_t clds = (L.cnodes && L.fast_box && L.wf_clds)
                             ? (size_t)L.n_nodes * L.n_orders * 16u : 0;
     thread_local uint32_t clds_grid_cache[2] = {0, 0};
     uint32_t clds_grid = 0;
-    static const uint32_t clds_threads = [] {  // DIAGNOSTIC: RTW_CLDS_THREADS (occupancy of the LDS walk)
-        const char* e = std::getenv("RTW_CLDS_THREADS");
-        const int t = e ? std::atoi(e) : 1024;
-        return (uint32_t)((t == 256 || t == 512) ? t : 1024);
-    }();
+    constexpr uint32_t clds_threads = 1024;  // one block per CU shares the stage (256 / 512: slower)
     if constexpr ((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING)) == 0) {
         if (clds && clds <= RTW_WF_CLDS_MAX) {
             if (!clds_grid_cache[0] || clds_grid_cache[1] != clds) {
@@ -949,9 +861,6 @@ void wf_run(const rtw_launch& L, const rtw_wf& W, hipStream_t st, int n_cu, rtw_
             clds_grid = clds_grid_cache[0];
         }
     }
-    const char* op = std::getenv("RTW_TRACE_OCC_PAD");
-    const size_t occ_pad = op ? (size_t)std::atoi(op) : 0;
-    const uint32_t pad_grid = occ_pad ? wf_grid(wf_trace<FEAT, false>, n_cu, occ_pad) : 0;
     for (uint32_t it = 0; it < iters; it++) {
         RTW_TIME_BEGIN(T, RTW_K_TRACE)
         if constexpr ((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING)) == 0) {
@@ -963,8 +872,6 @@ void wf_run(const rtw_launch& L, const rtw_wf& W, hipStream_t st, int n_cu, rtw_
         }
         if (lds)
             hipLaunchKernelGGL((wf_trace<FEAT, true>), dim3(lds_grid), dim3(256), tlds, st, L, W, it);
-        else if (occ_pad)  // DIAGNOSTIC: occupancy sweep (dynamic LDS limits resident blocks)
-            hipLaunchKernelGGL((wf_trace<FEAT, false>), dim3(pad_grid), dim3(256), occ_pad, st, L, W, it);
         else
             hipLaunchKernelGGL((wf_trace<FEAT, false>), dim3(g.trace), dim3(256), 0, st, L, W, it);
         RTW_TIME_END(T)

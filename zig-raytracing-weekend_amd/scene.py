@@ -470,13 +470,18 @@ class World:
 
     Owns an ``rtw_ctx`` (one GPU).  ``Hittable{.tree = ...}`` in the reference."""
 
-    def __init__(self, arrays: SceneArrays, device: int = 0):
+    def __init__(self, arrays: SceneArrays, device: int = 0, tuning: Optional[dict] = None):
+        """tuning: rtw_tuning fields to override (A/B measurement; every setting renders the same image)."""
         L = _abi.lib()
         self.arrays = arrays
         self.device = device
         self._desc = arrays.desc()
         h = C.c_void_p()
-        _abi.check(L.rtw_scene_create(C.byref(self._desc), device, C.byref(h)), "rtw_scene_create")
+        if tuning:
+            t = _abi.tuning(**tuning)
+            _abi.check(L.rtw_scene_create_ex(C.byref(self._desc), device, C.byref(t), C.byref(h)), "rtw_scene_create_ex")
+        else:
+            _abi.check(L.rtw_scene_create(C.byref(self._desc), device, C.byref(h)), "rtw_scene_create")
         self.handle = h
 
     def close(self):
