@@ -38,6 +38,9 @@ ROWS_PER_BLOCK = 8   # row blocks interleaved over ranks: C2 at 8 GPUs 6.97x pre
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--single-process", action="store_true",
+                    help="drive the N GPUs from this one process through the C ABI (rtw_multi: shard renders + one "
+                         "grouped RCCL send/recv); the default without torchrun when --gpus > 1")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="c2",
@@ -60,9 +63,10 @@ def main():
     world_size = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world_size != args.gpus:
-        if world_size == 1 and args.gpus > 1:
-            raise SystemExit("--gpus N > 1 must be launched with torchrun --nproc-per-node N")
+    single = args.single_process or (world_size == 1 and args.gpus > 1)
+    if world_size > 1 and (single or world_size != args.gpus):
+        raise SystemExit("torchrun: --gpus must equal the number of ranks and excludes --single-process")
+    n_shards = args.gpus if single else world_size
     torch.cuda.set_device(local_rank)
     distributed = world_size > 1
     if distributed:
@@ -75,7 +79,11 @@ def main():
     bvh_mode = {"sah": pkg._abi.RTW_BVH_SAH, "reference": pkg._abi.RTW_BVH_REFERENCE}[args.bvh]
     arr = pkg.flatten(objs, bvh_mode=bvh_mode)
     t0 = time.time()
-    world = pkg.World(arr, device=local_rank, tuning=json.loads(args.tuning) if args.tuning else None)
+    tun = json.loads(args.tuning) if args.tuning else None
+    world = pkg.World(arr, device=local_rank, tuning=tun)
+    # single-process multi-GPU: one context per device + the RCCL communicators of rtw_multi
+    worlds = [world] + [pkg.World(arr, device=k, tuning=tun) for k in range(1, n_shards)] if single else [world]
+    multi = pkg.distributed.MultiDeviceRender(worlds, ROWS_PER_BLOCK) if single else None
     build_s = time.time() - t0
     # the reference topology (bvh.zig) defines the algorithmic bytes
     world_ref = pkg.World(pkg.flatten(objs, bvh_mode=pkg._abi.RTW_BVH_REFERENCE), device=local_rank)
@@ -88,9 +96,11 @@ def main():
 
     stream = torch.cuda.Stream()          # explicit stream: the kernels and the timing events share it
     torch.cuda.set_stream(stream)
-    shard = pkg.distributed.ShardedRender(world, cam, rank, world_size, ROWS_PER_BLOCK)
+    # the shard this process renders (single-process mode: device 0's, for the counted and timing passes)
+    shard = pkg.distributed.ShardedRender(world, cam, rank, n_shards, ROWS_PER_BLOCK)
     my_rows = shard.rows
-    assert my_rows == L.rtw_shard_rows(H, ROWS_PER_BLOCK, world_size, rank)
+    assert my_rows == L.rtw_shard_rows(H, ROWS_PER_BLOCK, n_shards, rank)
+    frame = torch.zeros((W * H, 4), dtype=torch.float32, device="cuda") if single else None
 
     def render_step(counters=None, w=None, timing=None):
         if w is not None:
@@ -100,7 +110,15 @@ def main():
             shard.world = saved
 
     def gather_step():
-        shard.gather()
+        if not single:
+            shard.gather()
+
+    def frame_step():
+        # one whole frame: every shard rendered + gathered (single-process: rtw_render_multi_device)
+        if single:
+            multi.render_device(cam, 0, spp, frame.data_ptr(), seed=0, stream=stream, fresh=True, sync=False)
+        else:
+            render_step()
 
     # ---- algorithmic bytes of one step: counted pass on the reference topology (the device
     # walk of a reference-topology tree visits exactly the nodes bvh.zig's recursion visits)
@@ -120,7 +138,7 @@ def main():
     alg_bytes = NODE_BYTES * (nodes + leaves) + 32 * pixels
 
     for _ in range(args.warmup):
-        render_step()
+        frame_step()
         gather_step()
     torch.cuda.synchronize()
 
@@ -133,7 +151,10 @@ def main():
     t_start = time.perf_counter()
     for k in range(args.steps):
         ev[k][0].record(stream)
-        render_step(timing=timings[k])
+        if single:
+            frame_step()
+        else:
+            render_step(timing=timings[k])
         ev[k][1].record(stream)
         gather_step()
     torch.cuda.synchronize()
@@ -141,11 +162,19 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t_start
     kernel_ms = [a.elapsed_time(b) for a, b in ev]
+    if single:  # per-kernel HIP events of device 0's shard, rendered alone after the timed region
+        for k in range(args.steps):
+            render_step(timing=timings[k])
+        torch.cuda.synchronize()
     if distributed:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
+    if single:
+        multi.close()
+        for w in worlds[1:]:
+            w.close()
     total_samples = W * H * spp * args.steps
     value = total_samples / elapsed / 1e6
     render_s = sum(kernel_ms) / len(kernel_ms) / 1e3          # whole render call (all kernels) per step
@@ -229,7 +258,7 @@ def main():
                        if args.config == "c2" else f"Msamples/s (pixel·spp) on {cfg.description}"),
             "value": round(value, 3),
             "unit": "Msamples/s",
-            "n_gpus": world_size,
+            "n_gpus": n_shards,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 3),
@@ -240,8 +269,10 @@ def main():
             "data": "synthetic: seeded %s scene (%d world objects), counter-based RNG seed 0" % (args.config, len(objs)),
             "config": {"workload": cfg.description, "config_id": args.config, "width": W, "height": H,
                        "spp": spp, "max_depth": cam.max_depth, "objects": len(objs), "bvh_nodes": stats["n_nodes"],
-                       "bvh_depth": stats["depth"], "parallelism": f"row-interleaved tiles x{world_size}"
-                       + (" + RCCL gather" if distributed else ""), "rows_per_block": ROWS_PER_BLOCK},
+                       "bvh_depth": stats["depth"], "parallelism": f"row-interleaved tiles x{n_shards}"
+                       + (" + RCCL gather" if distributed else "")
+                       + (" (one process, rtw_multi: grouped RCCL send/recv)" if single else ""),
+                       "rows_per_block": ROWS_PER_BLOCK},
             "roofline": roofline,
             "cpu_baseline": cpu,
             "nan_samples": nan_count,

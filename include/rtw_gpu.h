@@ -339,6 +339,39 @@ int rtw_render_rows_device(rtw_ctx* ctx, const rtw_camera* cam, uint32_t rows_pe
                            uint32_t shard, uint32_t spp_begin, uint32_t spp_end, uint64_t seed,
                            float* d_tile, void* stream, const rtw_render_opts* opts);
 uint32_t rtw_shard_rows(uint32_t height, uint32_t rows_per_block, uint32_t n_shards, uint32_t shard);
+/* Image row of row `tile_row` of a shard's compact tile (>= height: padding; 0xFFFFFFFF: bad spec).
+ * The same function places rows in the render kernels and the multi-GPU gather. */
+uint32_t rtw_shard_image_row(uint32_t rows_per_block, uint32_t n_shards, uint32_t shard, uint32_t tile_row);
+
+/* ---------------------------------------------------------------------------
+ * Multi-GPU frame in one process (the north star's "8-GPU tile shard
+ * + one RCCL gather" behind the FFI).  Replaces startRender's 8-thread split
+ * (src/main.zig:314-326) of Camera.render (src/camera.zig:93-116) with N devices:
+ * device k renders the row blocks b with b % N == k (rtw_render_rows_device) into
+ * a compact tile; one grouped RCCL send/recv moves every tile to device 0, where
+ * the rows are scattered into the frame.  Unless RTW_RENDER_FRESH, the frame's
+ * current rows are first scattered to the devices the same way, so progressive
+ * calls accumulate exactly as on one device: the result is bit-identical to
+ * rtw_render_device for any N (counter-based RNG keyed by seed, pixel, sample).
+ * ------------------------------------------------------------------------- */
+typedef struct rtw_multi rtw_multi;
+/* ctxs[k]: one context per device, each from rtw_scene_create(desc, device_k) with the
+ * same desc; ctxs[0]'s device holds the frame.  Creates the RCCL communicators
+ * (ncclCommInitAll) once.  The contexts must outlive the rtw_multi and must not be
+ * rendered on by other callers during an rtw_render_multi* call. */
+int rtw_multi_create(rtw_ctx* const* ctxs, uint32_t n, rtw_multi** out);
+void rtw_multi_destroy(rtw_multi* m);
+enum { RTW_RENDER_FRESH = 2u };  /* rtw_render_multi_device: start the range from zero, do not read d_accum */
+/* d_accum: float4[W*H] on ctxs[0]'s device; stream: a hipStream_t of that device or NULL.
+ * opts: spp_batch and flags (RTW_RENDER_NO_SYNC, RTW_RENDER_FRESH) are honoured; counters
+ * and timing must be NULL. */
+int rtw_render_multi_device(rtw_multi* m, const rtw_camera* cam, uint32_t rows_per_block, uint32_t spp_begin,
+                            uint32_t spp_end, uint64_t seed, float* d_accum, void* stream,
+                            const rtw_render_opts* opts);
+/* Same on a caller-owned HOST float4[W*H] (ColorAndSamples), blocking; cancel is polled
+ * before the render starts. */
+int rtw_render_multi(rtw_multi* m, const rtw_camera* cam, uint32_t rows_per_block, uint32_t spp_begin,
+                     uint32_t spp_end, uint64_t seed, float* accum, const volatile int32_t* cancel);
 
 /* SharedStateImageWriter texel update: u8(256*clamp(sqrt(rgb/w),0,0.999)), alpha 255
  * (src/camera.zig:58-65, src/color.zig:43-62). Host, n pixels. */

@@ -30,6 +30,36 @@ def test_shard_rows_match_library(rtw):
                 assert sorted(dst) == list(range(H))
 
 
+def test_shard_image_row_matches_reassembly(rtw):
+    """The library's one row map (rtw_shard_image_row: render kernels and the multi-GPU
+    pack/unpack) equals the reassembly index of the gather, and places every image row
+    exactly once across the shards' tiles."""
+    L = rtw.lib()
+    d = rtw.distributed
+    for H in (1, 15, 17, 800, 2160):
+        for rpb in (1, 8, 16):
+            for n in (1, 2, 3, 8):
+                cap = d.tile_rows_capacity(H, rpb, n)
+                src, dst = d.reassembly_index(H, rpb, n)
+                got = {}
+                for s in range(n):
+                    for r in range(cap):
+                        y = L.rtw_shard_image_row(rpb, n, s, r)
+                        if y < H:
+                            assert y not in got.values()
+                            got[s * cap + r] = y
+                assert got == dict(zip(src, dst))
+                assert sorted(got.values()) == list(range(H))
+    assert L.rtw_shard_image_row(8, 2, 2, 0) == 0xFFFFFFFF
+
+
+def test_multi_create_rejects_bad_args(rtw):
+    import ctypes as C
+    h = C.c_void_p()
+    assert rtw.lib().rtw_multi_create(None, 0, C.byref(h)) == rtw._abi.RTW_E_INVALID
+    assert rtw.lib().rtw_multi_create(None, 1, None) == rtw._abi.RTW_E_INVALID
+
+
 def _free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))

@@ -21,6 +21,7 @@ RTW_BG_CONSTANT, RTW_BG_GRADIENT = 0, 1
 RTW_BVH_REFERENCE, RTW_BVH_SAH = 0, 1
 RTW_PPM_WRITECOLOR, RTW_PPM_STDOUT = 0, 1
 RTW_RENDER_NO_SYNC = 1
+RTW_RENDER_FRESH = 2
 RTW_STAT_RAYS, RTW_STAT_NODES, RTW_STAT_LEAVES, RTW_STAT_SAMPLES, RTW_STAT_NAN, RTW_STAT_TAIL_RAYS = 0, 1, 2, 3, 4, 5
 RTW_STAT_COUNT = 8
 RTW_K_GEN, RTW_K_TRACE, RTW_K_SHADE, RTW_K_TAIL, RTW_K_REDUCE, RTW_K_MEGA, RTW_K_COUNT = 0, 1, 2, 3, 4, 5, 8
@@ -146,6 +147,13 @@ SIGNATURES = {
                                          C.c_uint32, C.c_uint32, C.c_uint64, C.c_void_p, C.c_void_p,
                                          C.POINTER(RtwRenderOpts)]),
     "rtw_shard_rows": (C.c_uint32, [C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32]),
+    "rtw_shard_image_row": (C.c_uint32, [C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32]),
+    "rtw_multi_create": (C.c_int, [C.POINTER(C.c_void_p), C.c_uint32, C.POINTER(C.c_void_p)]),
+    "rtw_multi_destroy": (None, [C.c_void_p]),
+    "rtw_render_multi_device": (C.c_int, [C.c_void_p, C.POINTER(RtwCamera), C.c_uint32, C.c_uint32, C.c_uint32,
+                                          C.c_uint64, C.c_void_p, C.c_void_p, C.POINTER(RtwRenderOpts)]),
+    "rtw_render_multi": (C.c_int, [C.c_void_p, C.POINTER(RtwCamera), C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint64,
+                                   C.c_void_p, C.c_void_p]),
     "rtw_texture_from_accum": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p]),
     "rtw_texture_from_accum_device": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p]),
     "rtw_encode_ppm": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_void_p, C.c_size_t,

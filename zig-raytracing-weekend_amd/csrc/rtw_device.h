@@ -1009,8 +1009,7 @@ __device__ f3 sample_radiance(const float4* __restrict__ nodes, const rtw_launch
 
 __device__ __forceinline__ bool map_row(const rtw_launch& L, uint32_t r, uint32_t& y) {
     if (L.n_shards) {
-        const uint32_t blk = r / L.rpb;
-        y = (blk * L.n_shards + L.shard) * L.rpb + r % L.rpb;
+        y = rtw_tile_row_image(L.rpb, L.n_shards, L.shard, r);
     } else {
         y = r;
     }

@@ -38,6 +38,8 @@ int hip_fail(hipError_t e, const char* where) {
 
 }  // namespace
 
+void rtw_set_error(const char* msg) { g_err = msg ? msg : ""; }
+
 // struct rtw_ctx: see rtw_internal.h
 
 namespace {
@@ -734,6 +736,11 @@ uint32_t rtw_shard_rows(uint32_t H, uint32_t rpb, uint32_t n_shards, uint32_t sh
         rows += (H - y0 < rpb) ? H - y0 : rpb;
     }
     return rows;
+}
+
+uint32_t rtw_shard_image_row(uint32_t rpb, uint32_t n_shards, uint32_t shard, uint32_t tile_row) {
+    if (!rpb || !n_shards || shard >= n_shards) return 0xFFFFFFFFu;
+    return rtw_tile_row_image(rpb, n_shards, shard, tile_row);
 }
 
 int rtw_render_rows_device(rtw_ctx* ctx, const rtw_camera* cam, uint32_t rpb, uint32_t n_shards, uint32_t shard,

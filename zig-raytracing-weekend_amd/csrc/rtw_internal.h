@@ -99,6 +99,7 @@ struct rtw_kernel_info {
 int rtw_persistent_grid(uint32_t feat, uint32_t n_nodes, int waves, bool use_lds);
 
 void rtw_launch_render(const rtw_launch& L, void* stream, int variant, int grid);
+void rtw_set_error(const char* msg);  // the thread's rtw_last_error() message (rtw_host.hip)
 void rtw_launch_debug_rng(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t n, float* d_out, void* stream);
 void rtw_launch_debug_sample(const rtw_launch& L, uint32_t pixel, uint32_t sample, float* d_out, void* stream);
 

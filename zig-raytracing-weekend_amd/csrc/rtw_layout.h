@@ -15,6 +15,7 @@
 // Moving spheres keep center_vec = center2 - center1 in a side array indexed by
 // sphere id (only read when the moving flag is set).
 #pragma once
+#include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #define RTW_LEAF_BIT 0x80000000u
@@ -100,3 +101,11 @@ struct rtw_dev_image {
 
 // Per perlin table: ranvec as float4[256] (4 KiB) then perm_x|perm_y|perm_z as uint32[3][256]
 #define RTW_PERLIN_BYTES (256 * 16 + 3 * 256 * 4)
+
+// Row-interleaved shards (multi-GPU): row r of shard `shard`'s compact
+// tile is image row ((r / rpb) * n_shards + shard) * rpb + r % rpb (>= H: padding).
+// One definition for the render kernels (map_row), the multi-GPU pack/unpack and the
+// host (rtw_shard_image_row).
+__host__ __device__ inline uint32_t rtw_tile_row_image(uint32_t rpb, uint32_t n_shards, uint32_t shard, uint32_t r) {
+    return ((r / rpb) * n_shards + shard) * rpb + r % rpb;
+}

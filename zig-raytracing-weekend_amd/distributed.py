@@ -104,3 +104,50 @@ def gather_tiles(tile, image, gather_list, src, dst, W: int, world_size: int, ra
             image.index_copy_(0, dst, allt.index_select(0, src))
     else:
         image.index_copy_(0, dst, tile.view(-1, W, 4).index_select(0, src))
+
+
+class MultiDeviceRender:
+    """One process driving N devices through the C ABI (rtw_multi_*, csrc/rtw_multi.hip):
+    the same row-interleaved shards as ShardedRender, rendered concurrently on each
+    device's context, then ONE grouped RCCL send/recv of the tiles to device 0 and a
+    row scatter into the frame there.  worlds[k] is a World on device k (same scene);
+    worlds[0]'s device holds the frame.  Bit-identical to a 1-GPU render for any N."""
+
+    def __init__(self, worlds, rows_per_block: int = 8):
+        self.worlds = list(worlds)
+        self.rpb = rows_per_block
+        n = len(self.worlds)
+        handles = (C.c_void_p * n)(*[w.handle.value for w in self.worlds])
+        h = C.c_void_p()
+        _abi.check(_abi.lib().rtw_multi_create(handles, n, C.byref(h)), "rtw_multi_create")
+        self.handle = h
+
+    def render_device(self, cam, spp_begin: int, spp_end: int, d_accum: int, seed: int = 0, stream=None,
+                      fresh: bool = False, sync: bool = True, spp_batch: int = 0) -> None:
+        """Frame float4[W*H] at device pointer d_accum (worlds[0]'s device): rgb += samples
+        [spp_begin, spp_end), w = spp_end (fresh: the range starts from zero)."""
+        flags = (0 if sync else _abi.RTW_RENDER_NO_SYNC) | (_abi.RTW_RENDER_FRESH if fresh else 0)
+        opts = _abi.RtwRenderOpts(spp_batch, flags, None, None)
+        rc = _abi.lib().rtw_render_multi_device(self.handle, C.byref(cam.derived), self.rpb, spp_begin, spp_end,
+                                                seed, d_accum,
+                                                C.c_void_p(stream.cuda_stream if stream is not None else 0),
+                                                C.byref(opts))
+        _abi.check(rc, "rtw_render_multi_device")
+
+    def render_host(self, cam, spp_begin: int, spp_end: int, accum, seed: int = 0) -> None:
+        """Same on a host numpy float32 [W*H, 4] buffer (blocking)."""
+        assert accum.dtype.name == "float32" and accum.flags.c_contiguous and accum.size == cam.size * 4
+        rc = _abi.lib().rtw_render_multi(self.handle, C.byref(cam.derived), self.rpb, spp_begin, spp_end, seed,
+                                         accum.ctypes.data, None)
+        _abi.check(rc, "rtw_render_multi")
+
+    def close(self) -> None:
+        if getattr(self, "handle", None) and self.handle.value:
+            _abi.lib().rtw_multi_destroy(self.handle)
+            self.handle = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
