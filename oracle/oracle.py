@@ -92,6 +92,7 @@ def lib() -> C.CDLL:
             "oracle_path_floats": (None, [u64, u32, u32, u32, vp]),
             "oracle_aabb_hit": (C.c_int, [vp, vp, vp, C.c_float, C.c_float]),
             "oracle_sphere_uv": (None, [vp, vp]),
+            "oracle_libm": (None, [C.c_int, vp, vp, vp, u64]),
             "oracle_pow": (C.c_float, [C.c_float, C.c_float]),
             "oracle_reflect": (None, [vp, vp, vp]),
             "oracle_refract": (None, [vp, vp, C.c_float, vp]),

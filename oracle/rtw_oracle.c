@@ -18,6 +18,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include "zig_libm.h"  /* std.math.acos/atan2, @sin, @log as the Zig toolchain computes them */
+
 #define GOLDEN 0x9E3779B97F4A7C15ULL
 #define PI_F 3.1415926535897932385f                 /* rtweekend.zig:4 */
 #define INF_F (__builtin_inff())
@@ -341,12 +343,24 @@ static inline void set_face_normal(hit_record_t* rec, const ray3* r, v3 outward)
 
 /* objects.zig:101-114 */
 static void get_sphere_uv(v3 p, float* u, float* v) {
-    float theta = acosf(-p.e[1]);
-    float phi = atan2f(-p.e[2], p.e[0]) + PI_F;
+    float theta = zig_acosf(-p.e[1]);
+    float phi = zig_atan2f(-p.e[2], p.e[0]) + PI_F;
     *u = phi / (2 * PI_F);
     *v = theta / PI_F;
 }
 void oracle_sphere_uv(const float p[3], float uv[2]) { get_sphere_uv(vload(p), &uv[0], &uv[1]); }
+/* the restated transcendentals over arrays (tests): fn 0 acos, 1 atan2(y = a, x = b), 2 sin, 3 log, 4 atan */
+void oracle_libm(int fn, const float* a, const float* b, float* out, uint64_t n) {
+    for (uint64_t i = 0; i < n; i++) {
+        switch (fn) {
+            case 0: out[i] = zig_acosf(a[i]); break;
+            case 1: out[i] = zig_atan2f(a[i], b[i]); break;
+            case 2: out[i] = zig_sinf(a[i]); break;
+            case 3: out[i] = zig_logf(a[i]); break;
+            default: out[i] = zig_atanf(a[i]); break;
+        }
+    }
+}
 
 typedef struct {
     v3 center1, center_vec;
@@ -538,7 +552,7 @@ static v3 texture_value(const o_scene_desc* d, uint32_t ti, float u, float v, v3
         const o_perlin* pl = &d->perlins[t->perlin];
         v3 s = mul(splat(t->scale), p);
         COUNT(noise);
-        return splat(0.5f * (1 + sinf(s.e[2] + 10 * oracle_perlin_turb(pl, s.e, 7))));
+        return splat(0.5f * (1 + zig_sinf(s.e[2] + 10 * oracle_perlin_turb(pl, s.e, 7))));
     }
     }
     return V(0, 0, 0);
@@ -855,7 +869,7 @@ static int medium_hit(const world_t* w, uint32_t mi, const ray3* r, interval_t r
     if (rec_1.t < 0) rec_1.t = 0;
     float ray_length = vlength(r->direction);
     float distance_inside_boundary = (rec_2.t - rec_1.t) * ray_length;
-    float hit_distance = m->neg_inv_density * logf(oracle_medium_draw(rng ? rng->s : 0, mi));
+    float hit_distance = m->neg_inv_density * zig_logf(oracle_medium_draw(rng ? rng->s : 0, mi));
     if (hit_distance > distance_inside_boundary) return 0;
     rec->t = rec_1.t + hit_distance / ray_length;
     rec->p = ray_at(r, rec->t);

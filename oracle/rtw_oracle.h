@@ -153,6 +153,7 @@ void oracle_path_floats(uint64_t seed, uint32_t a, uint32_t b, uint32_t n, float
 /* Known-answer hooks */
 int oracle_aabb_hit(const float box[6], const float origin[3], const float dir[3], float tmin, float tmax);
 void oracle_sphere_uv(const float p[3], float uv[2]);
+void oracle_libm(int fn, const float* a, const float* b, float* out, uint64_t n);
 float oracle_pow(float x, float y);
 void oracle_reflect(const float v[3], const float n[3], float out[3]);
 void oracle_refract(const float uv[3], const float n[3], float e, float out[3]);

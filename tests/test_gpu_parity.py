@@ -6,9 +6,10 @@ direction is computed with the same fp32 operations as the oracle
 identical; only the radiance product is re-associated (iterative L += T*e vs
 the reference's recursive e + a*(...)), bounded by max_depth * 2^-24 relative
 per sample.  Tests assert |gpu - oracle| <= 1e-5 * max(1, |oracle|) per
-channel for the untextured scenes.  The textured scene uses device
-acosf/atan2f/sinf (ocml) against glibc, so a texel index or noise value may
-differ by 1 ulp: there >= 99.5 % of pixels must meet 1e-4 and the image mean 1e-4.
+channel for every pixel, textured scenes included: the sphere UV's acos/atan2 and
+the noise's sin are the Zig toolchain's algorithms restated on both sides
+(csrc/rtw_libm.h, oracle/zig_libm.h; tests/test_libm.py), so texel indices and
+noise values are bit-identical too.
 """
 import ctypes as C
 import os
@@ -116,9 +117,8 @@ def test_golden_crop_ref_head_moving(rtw, earth_rgba):
     world = rtw.World(rtw.flatten(rtw.worlds.generate_world(0, "ref_head", imgs)))
     cam = rtw.book1_camera(image_width=320, aspect_ratio=16 / 9, spp=8, max_depth=50).init()
     buf = render_rows(rtw, world, cam, 0, 180, 0, 8, 3)
-    ok = close(buf[:, :3], ref[:, :3], 1e-4)
-    assert ok.all(axis=1).mean() >= 0.995
-    assert abs(buf[:, :3].mean() - ref[:, :3].mean()) <= 1e-4 * abs(ref[:, :3].mean())
+    ok = close(buf[:, :3], ref[:, :3])
+    assert ok.all(), (ok.all(axis=1).mean(), np.abs(buf[:, :3] - ref[:, :3]).max())
 
 
 def test_sky_rows_vs_reference_image2(rtw, book1):
@@ -225,9 +225,8 @@ def test_textured_c5_crop(rtw, oracle, earth_rgba):
     pix = np.arange(y0 * 1920, y1 * 1920, dtype=np.uint32)
     ref = ow.render_pixels(ocam, 1, pix, 0, 4, threads=os.cpu_count() or 1)
     got = buf[pix]
-    ok = close(got[:, :3], ref[:, :3], 1e-4).all(axis=1)
-    assert ok.mean() >= 0.995, ok.mean()
-    assert abs(got[:, :3].mean() - ref[:, :3].mean()) <= 1e-4 * abs(ref[:, :3].mean())
+    ok = close(got[:, :3], ref[:, :3]).all(axis=1)
+    assert ok.all(), (ok.mean(), np.abs(got[:, :3] - ref[:, :3]).max())
 
 
 def test_stress_100k_crop(rtw, oracle):

@@ -18,6 +18,7 @@
 #include "../../include/rtw_gpu.h"
 #include "rtw_internal.h"
 #include "rtw_layout.h"
+#include "rtw_libm.h"
 #include "rtw_rng.h"
 
 #pragma clang fp contract(off)
@@ -205,8 +206,8 @@ __device__ float perlin_noise(const float4* tab, f3 p) {  // perlin.zig:117-162 
 }
 
 __device__ __forceinline__ void sphere_uv(f3 p, float& u, float& v) {  // objects.zig:101-114
-    float theta = acosf(-p.y);
-    float phi = atan2f(-p.z, p.x) + kPi;
+    float theta = rtw_acosf(-p.y);  // std.math.acos / atan2 as Zig computes them (rtw_libm.h)
+    float phi = rtw_atan2f(-p.z, p.x) + kPi;
     u = phi / (2 * kPi);
     v = theta / kPi;
 }
@@ -262,7 +263,7 @@ __device__ f3 texture_value(const rtw_launch& L, uint32_t ti, const HitUV& uv, f
                 tp = tp * splat(2);
             }
             float turb = __builtin_fabsf(accum);
-            return splat(0.5f * (1 + sinf(s.z + 10 * turb)));
+            return splat(0.5f * (1 + rtw_sinf(s.z + 10 * turb)));  // @sin: rtw_libm.h
         }
     }
     return ld3(t.even);  // RTW_TEX_SOLID (textures.zig:43-45)
@@ -484,7 +485,7 @@ __device__ __forceinline__ bool medium_t(const rtw_launch& L, uint32_t idx, cons
     if (t1 < 0) t1 = 0;
     const float ray_length = __builtin_sqrtf(length_squared(r.d));
     const float inside = (t2 - t1) * ray_length;
-    const float hit_distance = m.neg_inv_density * logf(rtw_medium_u(mkey, idx));
+    const float hit_distance = m.neg_inv_density * rtw_logf(rtw_medium_u(mkey, idx));  // @log: rtw_libm.h
     if (hit_distance > inside) return false;
     t = t1 + RTW_DIV(hit_distance, ray_length);
     return true;
