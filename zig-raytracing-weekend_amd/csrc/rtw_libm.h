@@ -21,6 +21,9 @@
 #pragma once
 #include <stdint.h>
 #include <string.h>
+#ifndef __cplusplus
+#include <stdbool.h>
+#endif
 
 #if defined(__HIPCC__)
 #define RTW_LIBM_FN __host__ __device__ static inline
@@ -50,7 +53,9 @@ RTW_LIBM_FN float rtw_lm_acos_r(float z) {
     return p / q;
 }
 
-// acos.zig acos32 (musl acosf)
+// acos.zig acos32 (musl acosf).  The three ranges are evaluated with selects (the wave
+// would execute every branch its lanes take): each result is the same fp32 expression
+// of the source, so the selected value is bit-identical to the branchy form.
 RTW_LIBM_FN float rtw_acosf(float x) {
     const float pio2_hi = 1.5707962513e+00f, pio2_lo = 7.5497894159e-08f;
     const uint32_t hx = rtw_lm_bits(x);
@@ -59,70 +64,63 @@ RTW_LIBM_FN float rtw_acosf(float x) {
         if (ix == 0x3F800000u) return (hx >> 31) ? 2.0f * pio2_hi + 0x1.0p-120f : 0.0f;
         return rtw_lm_float(0x7FC00000u);
     }
-    if (ix < 0x3F000000u) {  // |x| < 0.5
-        if (ix <= 0x32800000u) return pio2_hi + 0x1.0p-120f;  // |x| < 2^-26
-        return pio2_hi - (x - (pio2_lo - x * rtw_lm_acos_r(x * x)));
-    }
-    if (hx >> 31) {  // x < -0.5
-        const float z = (1.0f + x) * 0.5f;
-        const float s = __builtin_sqrtf(z);
-        const float w = rtw_lm_acos_r(z) * s - pio2_lo;
-        return 2.0f * (pio2_hi - (s + w));
-    }
+    const bool small = ix < 0x3F000000u;       // |x| < 0.5
+    const bool neg = (hx >> 31) != 0;          // (big) x < -0.5
+    const float zb = neg ? (1.0f + x) * 0.5f : (1.0f - x) * 0.5f;
+    const float z = small ? x * x : zb;
+    const float r = rtw_lm_acos_r(z);
+    const float s = __builtin_sqrtf(zb);
+    // |x| < 0.5
+    const float v_small = (ix <= 0x32800000u) ? pio2_hi + 0x1.0p-120f : pio2_hi - (x - (pio2_lo - x * r));
+    // x < -0.5
+    const float v_neg = 2.0f * (pio2_hi - (s + (r * s - pio2_lo)));
     // x > 0.5
-    const float z = (1.0f - x) * 0.5f;
-    const float s = __builtin_sqrtf(z);
     const float df = rtw_lm_float(rtw_lm_bits(s) & 0xFFFFF000u);
-    const float c = (z - df * df) / (s + df);
-    const float w = rtw_lm_acos_r(z) * s + c;
-    return 2.0f * (df + w);
+    const float c = (zb - df * df) / (s + df);
+    const float v_pos = 2.0f * (df + (r * s + c));
+    return small ? v_small : (neg ? v_neg : v_pos);
 }
 
-// atan.zig atan32 (musl atanf)
+// atan.zig atan32 (musl atanf).  The argument reduction's five forms are one quotient
+// (a*x + b) / (c*x + d) with per-range constants that reproduce each form's fp32
+// operations exactly (2x and 0*x, 1*x, x + 0 are exact for these finite x), so no lane
+// diverges; the result is bit-identical to the branchy source.
 RTW_LIBM_FN float rtw_atanf(float x_) {
-    const float atanhi[4] = {4.6364760399e-01f, 7.8539812565e-01f, 9.8279368877e-01f, 1.5707962513e+00f};
-    const float atanlo[4] = {5.0121582440e-09f, 3.7748947079e-08f, 3.4473217170e-08f, 7.5497894159e-08f};
-    const float aT[5] = {3.3333328366e-01f, -1.9999158382e-01f, 1.4253635705e-01f, -1.0648017377e-01f,
-                         6.1687607318e-02f};
-    float x = x_;
-    uint32_t ix = rtw_lm_bits(x);
+    const float aT0 = 3.3333328366e-01f, aT1 = -1.9999158382e-01f, aT2 = 1.4253635705e-01f,
+                aT3 = -1.0648017377e-01f, aT4 = 6.1687607318e-02f;
+    uint32_t ix = rtw_lm_bits(x_);
     const uint32_t sign = ix >> 31;
     ix &= 0x7FFFFFFFu;
-    int id;
     if (ix >= 0x4C800000u) {  // |x| >= 2^26
-        if (ix > 0x7F800000u) return x;  // nan
-        const float z = atanhi[3] + 0x1.0p-120f;
+        if (ix > 0x7F800000u) return x_;  // nan
+        const float z = 1.5707962513e+00f + 0x1.0p-120f;
         return sign ? -z : z;
     }
-    if (ix < 0x3EE00000u) {  // |x| < 0.4375
-        if (ix < 0x39800000u) return x;  // |x| < 2^-12
-        id = -1;
-    } else {
-        x = __builtin_fabsf(x);
-        if (ix < 0x3F980000u) {  // |x| < 1.1875
-            if (ix < 0x3F300000u) {  // 7/16 <= |x| < 11/16
-                id = 0;
-                x = (2.0f * x - 1.0f) / (2.0f + x);
-            } else {  // 11/16 <= |x| < 19/16
-                id = 1;
-                x = (x - 1.0f) / (x + 1.0f);
-            }
-        } else {
-            if (ix < 0x401C0000u) {  // |x| < 2.4375
-                id = 2;
-                x = (x - 1.5f) / (1.0f + 1.5f * x);
-            } else {  // 2.4375 <= |x| < 2^26
-                id = 3;
-                x = -1.0f / x;
-            }
-        }
-    }
+    if (ix < 0x39800000u) return x_;  // |x| < 2^-12
+    // id: -1 |x| < 0.4375, 0 < 11/16, 1 < 19/16, 2 < 2.4375, 3 beyond
+    const int id = ix < 0x3EE00000u ? -1 : ix < 0x3F300000u ? 0 : ix < 0x3F980000u ? 1 : ix < 0x401C0000u ? 2 : 3;
+    const float ax = id < 0 ? x_ : __builtin_fabsf(x_);
+    //            num = a*x + b           den = c*x + d
+    // id -1:     1*x + 0                 0*x + 1        -> x
+    // id  0:     2*x - 1                 1*x + 2        -> (2x - 1) / (2 + x)
+    // id  1:     1*x - 1                 1*x + 1        -> (x - 1) / (x + 1)
+    // id  2:     1*x - 1.5               1.5*x + 1      -> (x - 1.5) / (1 + 1.5x)
+    // id  3:     0*x - 1                 1*x + 0        -> -1 / x
+    const float ka = id == 0 ? 2.0f : (id == 3 ? 0.0f : 1.0f);
+    const float kb = id < 0 ? 0.0f : (id == 2 ? -1.5f : (id == 0 || id == 1 || id == 3 ? -1.0f : 0.0f));
+    const float kc = id < 0 ? 0.0f : (id == 2 ? 1.5f : 1.0f);
+    const float kd = id < 0 ? 1.0f : (id == 0 ? 2.0f : (id == 3 ? 0.0f : 1.0f));
+    const float x = (ka * ax + kb) / (kc * ax + kd);
     const float z = x * x;
     const float w = z * z;
-    const float s1 = z * (aT[0] + w * (aT[2] + w * aT[4]));
-    const float s2 = w * (aT[1] + w * aT[3]);
+    const float s1 = z * (aT0 + w * (aT2 + w * aT4));
+    const float s2 = w * (aT1 + w * aT3);
+    const float hi = id == 0 ? 4.6364760399e-01f : id == 1 ? 7.8539812565e-01f : id == 2 ? 9.8279368877e-01f
+                                                                                      : 1.5707962513e+00f;
+    const float lo = id == 0 ? 5.0121582440e-09f : id == 1 ? 3.7748947079e-08f : id == 2 ? 3.4473217170e-08f
+                                                                                      : 7.5497894159e-08f;
     if (id < 0) return x - x * (s1 + s2);
-    const float zz = atanhi[id] - ((x * (s1 + s2) - atanlo[id]) - x);
+    const float zz = hi - ((x * (s1 + s2) - lo) - x);
     return sign ? -zz : zz;
 }
 
@@ -213,41 +211,69 @@ RTW_LIBM_FN int rtw_lm_rem_pio2f(float x, double* y) {
     return n;
 }
 
-// sin.zig sinf (musl)
+// sin.zig sinf (musl).  The five argument ranges and the medium-size reduction give
+// (y, kernel, sign) with the source's exact double operations (x + c == x - (-c) and
+// -(a + b) == (-a) + (-b) in IEEE arithmetic); both kernels are evaluated and selected,
+// so the wave runs one path: bit-identical to the branchy source.
 RTW_LIBM_FN float rtw_sinf(float x) {
     const double s1pio2 = 1 * 1.57079632679489661923, s2pio2 = 2 * 1.57079632679489661923,
                  s3pio2 = 3 * 1.57079632679489661923, s4pio2 = 4 * 1.57079632679489661923;
     uint32_t ix = rtw_lm_bits(x);
-    const uint32_t sign = ix >> 31;
+    const bool sign = (ix >> 31) != 0;
     ix &= 0x7FFFFFFFu;
-    if (ix <= 0x3F490FDAu) {  // |x| ~<= pi/4
-        if (ix < 0x39800000u) return x;  // |x| < 2^-12
-        return rtw_lm_sindf(x);
-    }
-    if (ix <= 0x407B53D1u) {  // |x| ~<= 5*pi/4
-        if (ix <= 0x4016CBE3u) {  // |x| ~<= 3*pi/4
-            if (sign) return -rtw_lm_cosdf((double)x + s1pio2);
-            return rtw_lm_cosdf((double)x - s1pio2);
-        }
-        return rtw_lm_sindf(sign ? -((double)x + s2pio2) : -((double)x - s2pio2));
-    }
-    if (ix <= 0x40E231D5u) {  // |x| ~<= 9*pi/4
-        if (ix <= 0x40AFEDDFu) {  // |x| ~<= 7*pi/4
-            if (sign) return rtw_lm_cosdf((double)x + s3pio2);
-            return -rtw_lm_cosdf((double)x - s3pio2);
-        }
-        return rtw_lm_sindf(sign ? (double)x + s4pio2 : (double)x - s4pio2);
-    }
+    if (ix < 0x39800000u) return x;  // |x| < 2^-12 (and +-0)
     if (ix >= 0x7F800000u) return x - x;  // sin(inf or nan) = nan
     if (ix >= 0x4DC90FDBu) return rtw_lm_float(0x7FC00000u);  // beyond the medium-size reduction
+    const double xd = (double)x;
     double y;
-    const int n = rtw_lm_rem_pio2f(x, &y);
-    switch (n & 3) {
-        case 0: return rtw_lm_sindf(y);
-        case 1: return rtw_lm_cosdf(y);
-        case 2: return rtw_lm_sindf(-y);
-        default: return -rtw_lm_cosdf(y);
+    bool use_cos, neg_out = false;
+    if (ix <= 0x40E231D5u) {  // |x| ~<= 9*pi/4: one subtraction of a multiple of pi/2
+        double off;
+        bool neg_in = false;
+        if (ix <= 0x3F490FDAu) {  // |x| ~<= pi/4: sin(x)
+            off = 0.0;
+            use_cos = false;
+        } else if (ix <= 0x4016CBE3u) {  // ~<= 3pi/4: sign ? -cos(x + pi/2) : cos(x - pi/2)
+            off = sign ? -s1pio2 : s1pio2;
+            use_cos = true;
+            neg_out = sign;
+        } else if (ix <= 0x407B53D1u) {  // ~<= 5pi/4: sin(-(x -+ pi))
+            off = sign ? -s2pio2 : s2pio2;
+            use_cos = false;
+            neg_in = true;
+        } else if (ix <= 0x40AFEDDFu) {  // ~<= 7pi/4: sign ? cos(x + 3pi/2) : -cos(x - 3pi/2)
+            off = sign ? -s3pio2 : s3pio2;
+            use_cos = true;
+            neg_out = !sign;
+        } else {  // ~<= 9pi/4: sin(x -+ 2pi)
+            off = sign ? -s4pio2 : s4pio2;
+            use_cos = false;
+        }
+        y = (ix <= 0x3F490FDAu) ? xd : xd - off;
+        if (neg_in) y = -y;
+    } else {
+        const int n = rtw_lm_rem_pio2f(x, &y);
+        use_cos = (n & 1) != 0;
+        neg_out = (n & 3) == 3;
+        if ((n & 3) == 2) y = -y;
     }
+    // __sindf and __cosdf as one evaluation with selected operands, each step the same IEEE
+    // double operation as in the kernel it stands for:
+    //   sin: (y + s*(S1 + z*S2)) + (s*w)*(S3 + z*S4),   s = z*y
+    //   cos: ((1 + z*C0) + w*C1) + (w*z)*(C2 + z*C3)
+    const double S1 = -0x15555554cbac77.0p-55, S2 = 0x111110896efbb2.0p-59, S3 = -0x1a00f9e2cae774.0p-65,
+                 S4 = 0x16cd878c3b46a7.0p-71;
+    const double C0 = -0x1ffffffd0c5e81.0p-54, C1 = 0x155553e1053a42.0p-57, C2 = -0x16c087e80f1e27.0p-62,
+                 C3 = 0x199342e0ee5069.0p-68;
+    const double z = y * y;
+    const double w = z * z;
+    const double sz = z * y;
+    const double a = use_cos ? 1.0 + z * C0 : y;
+    const double b = use_cos ? w : sz;
+    const double c = use_cos ? C1 : S1 + z * S2;
+    const double r = (use_cos ? C2 : S3) + z * (use_cos ? C3 : S4);
+    const float v = (float)((a + b * c) + (w * (use_cos ? z : sz)) * r);
+    return neg_out ? -v : v;
 }
 
 // log.zig logf (FreeBSD e_logf.c as ported by musl / Zig compiler_rt)
