@@ -216,7 +216,8 @@ def main():
         "unit": "Tlane-op/s",
         "frac": round(achieved_valu / VALU_PEAK_TLOPS, 4) if achieved_valu is not None else None,
         "traffic": traffic,
-        "kernel": knames.get(dom, dom),
+        # the dominant kernel's instantiation as the committed PMC pass of this config recorded it
+        "kernel": (valu["kernels"][0] if valu and valu.get("kernels") else knames.get(dom, dom)),
         "fused_step": fused,
         "avg_launch_ms": round(dom_launch_s * 1e3, 4),
         "launches_per_step": kcalls[dom] / args.steps,
