@@ -8,6 +8,8 @@ import os
 import subprocess
 import sys
 
+import pytest
+
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 BENCH = "r2_c2_bench.json"
 SUMMARY = "r2_c2_timed_summary.txt"
@@ -46,10 +48,16 @@ def test_c2_bench_line_contract():
     assert c["value"] == max(v["value"] for v in c["legs"].values())
 
 
-def test_roofline_recomputes_from_profiles():
-    rc = subprocess.run([sys.executable, os.path.join(REPO, "tools", "roofline_check.py"),
-                         os.path.join(REPO, "profiles", BENCH)], capture_output=True, text=True)
+@pytest.mark.parametrize("config", ["c2", "c3", "c4", "c5", "cornell", "cornell_smoke", "simple_light"])
+def test_roofline_recomputes_from_profiles(config):
+    """Every committed round-2 bench line: VALU and HBM fractions <= 1 and recomputable from
+    the PMC passes in profiles/ and the line's HIP-event launch time."""
+    line = os.path.join(REPO, "profiles", f"r2_{config}_bench.json")
+    rc = subprocess.run([sys.executable, os.path.join(REPO, "tools", "roofline_check.py"), line],
+                        capture_output=True, text=True)
     assert rc.returncode == 0, rc.stdout + rc.stderr
+    r = load(f"r2_{config}_bench.json")["roofline"]
+    assert r["bound"] == "valu" and 0 < r["frac"] <= 1 and 0 < r["hbm"]["frac"] <= 1
 
 
 def test_rocprof_summary_agrees_with_bench_events():
