@@ -265,7 +265,11 @@ int rtw_camera_init(const rtw_camera_params* params, rtw_camera* out);
 /* Builds the BVH (bvh_mode) on the host, flattens it to 32-byte depth-first
  * nodes with skip links, and uploads nodes / materials / textures / images /
  * perlin tables to `device`.  Replaces generateWorld's BVHTree.init
- * (src/main.zig:309, src/bvh.zig:22-29). */
+ * (src/main.zig:309, src/bvh.zig:22-29).
+ * device = RTW_DEVICE_CPU makes a HOST context (no GPU needed): rtw_render on it runs the
+ * same per-sample code as the GPU on host threads (bit-identical images); the device-buffer
+ * and multi-GPU entry points refuse it (RTW_E_INVALID). */
+#define RTW_DEVICE_CPU (-1)
 int rtw_scene_create(const rtw_scene_desc* desc, int device, rtw_ctx** out);
 
 /* Implementation choices of a context (ABI 3).  Every setting renders the SAME image,
@@ -305,6 +309,8 @@ typedef struct rtw_tuning {
     uint32_t mega_shade_min;   /* persistent kernel: lanes ready before a shading pass (default 48; 1..64) */
     uint32_t mega_waves;       /* persistent kernel: launch-bound variant (default 1; 1, 6 or 8) */
     uint32_t mega_tile_order;  /* persistent kernel: 1 = last tile row first (default) */
+    uint32_t cpu_threads;      /* host context (RTW_DEVICE_CPU): render threads, 0 = every available core */
+    uint32_t _pad0;
     uint64_t wf_paths;         /* wavefront batch capacity in paths; 0 = auto (2^29 within 35 % of free memory) */
 } rtw_tuning;
 

@@ -30,6 +30,7 @@ RTW_KERNEL_WAVEFRONT, RTW_KERNEL_PERSISTENT, RTW_KERNEL_SIMPLE = 0, 1, 2
 RTW_LDS_NODES, RTW_LDS_CNODES, RTW_LDS_MATERIALS, RTW_LDS_SHADE = 1, 2, 4, 8
 RTW_LDS_GEOMETRY, RTW_LDS_PERLIN, RTW_LDS_MEGA_NODES, RTW_LDS_ALL = 16, 32, 64, 127
 RTW_FUSE_STEP, RTW_FUSE_TAIL_LDS, RTW_FUSE_GLOBAL = 1, 2, 4
+RTW_DEVICE_CPU = -1
 
 # numpy record layouts == the C structs (asserted against sizeof in tests)
 SPHERE_DT = np.dtype([("center1", "<f4", 3), ("radius", "<f4"), ("center2", "<f4", 3), ("is_moving", "<u4"),
@@ -108,7 +109,8 @@ class RtwTuning(C.Structure):
     _fields_ = [("kernel", C.c_uint32), ("bvh_orders", C.c_uint32), ("sah_max_leaf", C.c_uint32),
                 ("compact_nodes", C.c_uint32), ("fast_box", C.c_uint32), ("fast_reject", C.c_uint32),
                 ("lds", C.c_uint32), ("fuse", C.c_uint32), ("wf_iters", C.c_uint32), ("mega_shade_min", C.c_uint32),
-                ("mega_waves", C.c_uint32), ("mega_tile_order", C.c_uint32), ("wf_paths", C.c_uint64)]
+                ("mega_waves", C.c_uint32), ("mega_tile_order", C.c_uint32), ("cpu_threads", C.c_uint32),
+                ("_pad0", C.c_uint32), ("wf_paths", C.c_uint64)]
 
 
 def tuning(**fields) -> RtwTuning:

@@ -1,0 +1,60 @@
+// rtw_cpu.hip -- the host backend of the C ABI (rtw_scene_create(desc, RTW_DEVICE_CPU, ...)):
+// Camera.render (src/camera.zig:93-116) on host threads, for machines without a GPU and for the
+// reference's own CPU configuration (BASELINE config 1: 400x225, 10 spp, the 8-thread path of
+// src/main.zig:314-326).
+//
+// Not a fallback: a context is a host context only when the caller asks for one, and a GPU
+// context never runs here.  Each sample is sample_radiance() of rtw_device.h -- the very
+// function the GPU's v0 kernel runs per lane, compiled for the host -- so a host render is
+// bit-identical to the GPU's (same fp32 operations: correctly rounded division and sqrt, the
+// restated pow / acos / atan2 / sin / log, the counter-based RNG; a host context walks the
+// exact aabb.zig slab test and the IEEE sphere test, which the GPU's fast paths reproduce
+// bit for bit).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <thread>
+#include <vector>
+
+#include "rtw_device.h"
+
+int rtw_cpu_render(const rtw_launch& L, uint32_t pix_begin, uint32_t pix_end, float* accum, uint32_t threads,
+                   const volatile int32_t* cancel) {
+    const uint32_t n = pix_end - pix_begin;
+    if (threads == 0) threads = std::max(1u, std::thread::hardware_concurrency());
+    threads = std::min<uint32_t>(threads, std::max(1u, n));
+    std::atomic<bool> stopped{false};
+    // contiguous chunks, as startRender's Tasks (main.zig:318-324); samples in order per pixel
+    auto work = [&](uint32_t t) {
+        const uint32_t a = pix_begin + (uint32_t)((uint64_t)n * t / threads);
+        const uint32_t b = pix_begin + (uint32_t)((uint64_t)n * (t + 1) / threads);
+        Counters cnt;
+        for (uint32_t i = a; i < b; i++) {
+            if (cancel && *cancel) {  // polled per pixel, as Camera.render polls `running` (camera.zig:107)
+                stopped = true;
+                return;
+            }
+            const uint32_t x = i % L.W, y = i / L.W;
+            float* px = accum + 4 * (size_t)i;
+            float r = px[0], g = px[1], bl = px[2];
+            for (uint32_t s = L.s0; s < L.s1; s++) {
+                const f3 c = sample_radiance<RTW_F_ALL>(L.nodes, L, i, x + L.pixel_offset, y + L.pixel_offset, s,
+                                                        cnt);
+                r += c.x;
+                g += c.y;
+                bl += c.z;
+            }
+            px[0] = r;
+            px[1] = g;
+            px[2] = bl;
+            px[3] = (float)L.s1;  // writeColor: number_of_samples (camera.zig:56)
+        }
+    };
+    std::vector<std::thread> pool;
+    pool.reserve(threads);
+    for (uint32_t t = 1; t < threads; t++) pool.emplace_back(work, t);
+    work(0);
+    for (std::thread& th : pool) th.join();
+    return stopped ? RTW_E_CANCELLED : RTW_OK;
+}

@@ -35,6 +35,19 @@
 #define RTW_DIV(a, b) ((a) / (b))
 #endif
 
+// Every building block below is host + device (RTW_DHD): the CPU backend (rtw_cpu.hip) runs
+// the same per-sample path (sample_radiance) as the GPU's v0 kernel.  The hardware estimates
+// (v_rcp_f32 / v_sqrt_f32) exist only on the device; on the host they are never consulted --
+// a host context has fast_reject = fast_box = 0 and no compact nodes.
+#define RTW_DHD __host__ __device__ __forceinline__
+#if defined(__HIP_DEVICE_COMPILE__)
+#define RTW_RCP_EST(x) __builtin_amdgcn_rcpf(x)
+#define RTW_SQRT_EST(x) __builtin_amdgcn_sqrtf(x)
+#else
+#define RTW_RCP_EST(x) (1.0f / (x))
+#define RTW_SQRT_EST(x) __builtin_sqrtf(x)
+#endif
+
 namespace {
 
 constexpr float kPi = 3.1415926535897932385f;  // rtweekend.zig:4
@@ -43,37 +56,38 @@ constexpr float kInf = __builtin_inff();
 struct f3 {
     float x, y, z;
 };
-__device__ __forceinline__ f3 mk(float x, float y, float z) { return f3{x, y, z}; }
-__device__ __forceinline__ f3 operator+(f3 a, f3 b) { return f3{a.x + b.x, a.y + b.y, a.z + b.z}; }
-__device__ __forceinline__ f3 operator-(f3 a, f3 b) { return f3{a.x - b.x, a.y - b.y, a.z - b.z}; }
-__device__ __forceinline__ f3 operator*(f3 a, f3 b) { return f3{a.x * b.x, a.y * b.y, a.z * b.z}; }
-__device__ __forceinline__ f3 operator-(f3 a) { return f3{-a.x, -a.y, -a.z}; }
-__device__ __forceinline__ f3 splat(float s) { return f3{s, s, s}; }
-__device__ __forceinline__ f3 divs(f3 a, float s) { return f3{RTW_DIV(a.x, s), RTW_DIV(a.y, s), RTW_DIV(a.z, s)}; }
-__device__ __forceinline__ float dot(f3 u, f3 v) { return u.x * v.x + u.y * v.y + u.z * v.z; }
-__device__ __forceinline__ f3 cross(f3 u, f3 v) {  // vec3.zig:31-33
+RTW_DHD f3 mk(float x, float y, float z) { return f3{x, y, z}; }
+RTW_DHD f3 operator+(f3 a, f3 b) { return f3{a.x + b.x, a.y + b.y, a.z + b.z}; }
+RTW_DHD f3 operator-(f3 a, f3 b) { return f3{a.x - b.x, a.y - b.y, a.z - b.z}; }
+RTW_DHD f3 operator*(f3 a, f3 b) { return f3{a.x * b.x, a.y * b.y, a.z * b.z}; }
+RTW_DHD f3 operator-(f3 a) { return f3{-a.x, -a.y, -a.z}; }
+RTW_DHD f3 splat(float s) { return f3{s, s, s}; }
+RTW_DHD f3 divs(f3 a, float s) { return f3{RTW_DIV(a.x, s), RTW_DIV(a.y, s), RTW_DIV(a.z, s)}; }
+RTW_DHD float dot(f3 u, f3 v) { return u.x * v.x + u.y * v.y + u.z * v.z; }
+RTW_DHD f3 cross(f3 u, f3 v) {  // vec3.zig:31-33
     return f3{u.y * v.z - u.z * v.y, u.z * v.x - u.x * v.z, u.x * v.y - u.y * v.x};
 }
-__device__ __forceinline__ float length_squared(f3 u) { return u.x * u.x + u.y * u.y + u.z * u.z; }
-__device__ __forceinline__ f3 unit_vector(f3 v) { return divs(v, __builtin_sqrtf(length_squared(v))); }
-__device__ __forceinline__ f3 ld3(const float* p) { return f3{p[0], p[1], p[2]}; }
-__device__ __forceinline__ bool near_zero(f3 u) {  // vec3.zig:19-22
+RTW_DHD float length_squared(f3 u) { return u.x * u.x + u.y * u.y + u.z * u.z; }
+RTW_DHD f3 unit_vector(f3 v) { return divs(v, __builtin_sqrtf(length_squared(v))); }
+RTW_DHD f3 ld3(const float* p) { return f3{p[0], p[1], p[2]}; }
+RTW_DHD bool near_zero(f3 u) {  // vec3.zig:19-22
     const float s = 1e-8f;
     return __builtin_fabsf(u.x) < s && __builtin_fabsf(u.y) < s && __builtin_fabsf(u.z) < s;
 }
-__device__ __forceinline__ f3 reflect(f3 v, f3 n) { return v - n * splat(dot(v, n) * 2); }  // vec3.zig:77-79
-__device__ __forceinline__ f3 refract(f3 uv, f3 n, float e) {                             // vec3.zig:81-86
+RTW_DHD f3 reflect(f3 v, f3 n) { return v - n * splat(dot(v, n) * 2); }  // vec3.zig:77-79
+RTW_DHD f3 refract(f3 uv, f3 n, float e) {                             // vec3.zig:81-86
     float c = dot(-uv, n);
     float cos_theta = c < 1.0f ? c : 1.0f;
     f3 perp = splat(e) * (uv + n * splat(cos_theta));
     f3 par = n * splat(-__builtin_sqrtf(__builtin_fabsf(1.0f - length_squared(perp))));
     return perp + par;
 }
-__device__ __forceinline__ uint32_t fbits(float f) { return __float_as_uint(f); }
+RTW_DHD uint32_t fbits(float f) { return __builtin_bit_cast(uint32_t, f); }
+RTW_DHD float ubits(uint32_t u) { return __builtin_bit_cast(float, u); }
 
 // ---- RNG helpers (rtweekend.zig / vec3.zig samplers) ----
-__device__ __forceinline__ float rnd(rtw_rng& r) { return rtw_path_float(r); }  // render-domain draw
-__device__ __forceinline__ f3 random_unit_vector(rtw_rng& r) {  // vec3.zig:59-68
+RTW_DHD float rnd(rtw_rng& r) { return rtw_path_float(r); }  // render-domain draw
+RTW_DHD f3 random_unit_vector(rtw_rng& r) {  // vec3.zig:59-68
 #if defined(RTW_ABLATE_REJECT)
     {   // timing ablation only: one candidate, no rejection loop (wrong distribution)
         float x = rtw_path_range(r, -1, 1), y = rtw_path_range(r, -1, 1), z = rtw_path_range(r, -1, 1);
@@ -91,7 +105,7 @@ __device__ __forceinline__ f3 random_unit_vector(rtw_rng& r) {  // vec3.zig:59-6
 
 // Zig std.math.pow(f32, x, 5) via frexp-significand square-and-multiply +
 // scalbn (restated; identical fp32 operations to the CPU restatement).
-__device__ __forceinline__ float scalbn_f(float x, int n) {
+RTW_DHD float scalbn_f(float x, int n) {
     float y = x;
     if (n > 127) {
         y *= 1.7014118346046923e38f; n -= 127;
@@ -100,9 +114,9 @@ __device__ __forceinline__ float scalbn_f(float x, int n) {
         y *= 1.1754943508222875e-38f * 16777216.0f; n += 126 - 24;
         if (n < -126) { y *= 1.1754943508222875e-38f * 16777216.0f; n += 126 - 24; if (n < -126) n = -126; }
     }
-    return y * __uint_as_float((uint32_t)(0x7f + n) << 23);
+    return y * ubits((uint32_t)(0x7f + n) << 23);
 }
-__device__ __forceinline__ float frexp_sig(float x, int* e) {
+RTW_DHD float frexp_sig(float x, int* e) {
     uint32_t u = fbits(x);
     int ee = (int)((u >> 23) & 0xFF);
     int extra = 0;
@@ -114,9 +128,9 @@ __device__ __forceinline__ float frexp_sig(float x, int* e) {
         extra = -64;
     }
     *e = ee - 126 + extra;
-    return __uint_as_float((u & 0x807FFFFFu) | 0x3F000000u);
+    return ubits((u & 0x807FFFFFu) | 0x3F000000u);
 }
-__device__ __forceinline__ float pow5(float x) {
+RTW_DHD float pow5(float x) {
     if (x == 1) return 1;
     if (x == 0) return x;  // pow(+-0, odd int > 0) = +-0
     if (!(x == x)) return x;
@@ -131,7 +145,7 @@ __device__ __forceinline__ float pow5(float x) {
     a1 *= x1; ae += xe;
     return scalbn_f(a1, ae);
 }
-__device__ __forceinline__ float reflectance(float cosine, float ref_idx) {  // material.zig:101-106
+RTW_DHD float reflectance(float cosine, float ref_idx) {  // material.zig:101-106
     float r0 = (1 - ref_idx) / (1 + ref_idx);
     r0 = r0 * r0;
     return r0 + (1 - r0) * pow5(1 - cosine);
@@ -143,7 +157,7 @@ struct Ray {
 };
 
 // Camera.getRay (camera.zig:156-180)
-__device__ __forceinline__ Ray get_ray(const rtw_launch& L, uint32_t i, uint32_t j, rtw_rng& rng) {
+RTW_DHD Ray get_ray(const rtw_launch& L, uint32_t i, uint32_t j, rtw_rng& rng) {
     const f3 du = ld3(L.du), dv = ld3(L.dv);
     f3 pixel_center = (ld3(L.pixel00) + du * splat((float)i)) + dv * splat((float)j);
     float px = -0.5f + rnd(rng);
@@ -169,7 +183,7 @@ __device__ __forceinline__ Ray get_ray(const rtw_launch& L, uint32_t i, uint32_t
 }
 
 // Texture.value (textures.zig:22-123)
-__device__ float perlin_noise(const float4* tab, f3 p) {  // perlin.zig:117-162 + perlin_interp 30-53
+__host__ __device__ float perlin_noise(const float4* tab, f3 p) {  // perlin.zig:117-162 + perlin_interp 30-53
     const uint32_t* perm = reinterpret_cast<const uint32_t*>(tab + 256);
     float u = p.x - __builtin_floorf(p.x);
     float v = p.y - __builtin_floorf(p.y);
@@ -205,7 +219,7 @@ __device__ float perlin_noise(const float4* tab, f3 p) {  // perlin.zig:117-162 
     return accum;
 }
 
-__device__ __forceinline__ void sphere_uv(f3 p, float& u, float& v) {  // objects.zig:101-114
+RTW_DHD void sphere_uv(f3 p, float& u, float& v) {  // objects.zig:101-114
     float theta = rtw_acosf(-p.y);  // std.math.acos / atan2 as Zig computes them (rtw_libm.h)
     float phi = rtw_atan2f(-p.z, p.x) + kPi;
     u = phi / (2 * kPi);
@@ -222,7 +236,7 @@ struct HitUV {
 };
 
 template <uint32_t FEAT>
-__device__ f3 texture_value(const rtw_launch& L, uint32_t ti, const HitUV& uv, f3 p) {
+__host__ __device__ f3 texture_value(const rtw_launch& L, uint32_t ti, const HitUV& uv, f3 p) {
     const rtw_dev_texture& t = L.texs[ti];
     const uint32_t kind = t.kind;
     if constexpr ((FEAT & RTW_F_CHECKER) != 0) {
@@ -280,19 +294,19 @@ __device__ f3 texture_value(const rtw_launch& L, uint32_t ti, const HitUV& uv, f
 // so several divisions by one d (a ray's |d|^2, a sphere radius, a vector length)
 // share y.  sqrt_refined: for x in [2^-96, 2^128) finite, the compiler's IEEE sqrt
 // is v_sqrt_f32 then a +-1 ulp correction by the signs of fma residuals.
-__device__ __forceinline__ float rcp_refined(float d, float y0) {
+RTW_DHD float rcp_refined(float d, float y0) {
     const float e = __builtin_fmaf(-d, y0, 1.0f);
     return __builtin_fmaf(e, y0, y0);
 }
-__device__ __forceinline__ float div_shared(float x, float d, float y) {
+RTW_DHD float div_shared(float x, float d, float y) {
     const float q0 = x * y;
     const float r0 = __builtin_fmaf(-d, q0, x);
     const float q1 = __builtin_fmaf(r0, y, q0);
     const float r1 = __builtin_fmaf(-d, q1, x);
     return __builtin_fmaf(r1, y, q1);
 }
-__device__ __forceinline__ float sqrt_refined(float x, float s /* v_sqrt_f32(x) */) {
-    const float sdn = __uint_as_float(__float_as_uint(s) - 1u), sup = __uint_as_float(__float_as_uint(s) + 1u);
+RTW_DHD float sqrt_refined(float x, float s /* v_sqrt_f32(x) */) {
+    const float sdn = ubits(fbits(s) - 1u), sup = ubits(fbits(s) + 1u);
     const float rdn = __builtin_fmaf(-sdn, s, x), rup = __builtin_fmaf(-sup, s, x);
     const float r = (rdn <= 0.0f) ? sdn : s;
     return (rup > 0.0f) ? sup : r;
@@ -310,14 +324,14 @@ struct RayTrav {
     float rcp_a; // hardware 1/a estimate for the sphere fast-reject (0 disables it)
     float ya;    // rcp_refined(a) for div_shared (0: a outside [2^-40, 2^40], IEEE division)
 };
-__device__ __forceinline__ RayTrav ray_trav(const Ray& r, bool fast_box) {
+RTW_DHD RayTrav ray_trav(const Ray& r, bool fast_box) {
     RayTrav t;
     if (fast_box) {
         // |inv| <= 1e30 keeps every product finite (no inf*0 / inf-inf); a zero
         // component gives slabs of +-1e30 * (P - o), i.e. still +-"infinite"
         // given the >= E*2^-19 box pad
         auto ci = [](float d) {
-            return __builtin_fmaxf(__builtin_fminf(__builtin_amdgcn_rcpf(d), 1e30f), -1e30f);
+            return __builtin_fmaxf(__builtin_fminf(RTW_RCP_EST(d), 1e30f), -1e30f);
         };
         t.inv = mk(ci(r.d.x), ci(r.d.y), ci(r.d.z));
         t.oinv = mk(-(r.o.x * t.inv.x), -(r.o.y * t.inv.y), -(r.o.z * t.inv.z));
@@ -327,7 +341,7 @@ __device__ __forceinline__ RayTrav ray_trav(const Ray& r, bool fast_box) {
     }
     t.a = length_squared(r.d);
     // fast-reject only where every intermediate below stays normal and finite
-    t.rcp_a = (t.a > 1e-30f && t.a < 1e30f) ? __builtin_amdgcn_rcpf(t.a) : 0.0f;
+    t.rcp_a = (t.a > 1e-30f && t.a < 1e30f) ? RTW_RCP_EST(t.a) : 0.0f;
     t.ya = (t.a >= 0x1p-40f && t.a <= 0x1p40f) ? rcp_refined(t.a, t.rcp_a) : 0.0f;
     return t;
 }
@@ -339,10 +353,10 @@ constexpr float kTmin = 0.001f;  // camera.zig:187
 // Translate/RotateY instances of a HittableList, ConstantMedium.  Same fp32
 // operations in the same order as objects.zig (and the CPU restatement).
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ float4 ldg4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+RTW_DHD float4 ldg4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 
 // Sphere.hit t only (objects.zig:116-136), open interval (tmin, tmax)
-__device__ __forceinline__ bool sphere_t(f3 center, float radius, const Ray& r, float tmin, float tmax, float& t) {
+RTW_DHD bool sphere_t(f3 center, float radius, const Ray& r, float tmin, float tmax, float& t) {
     const f3 oc = r.o - center;
     const float a = length_squared(r.d);
     const float half_b = dot(oc, r.d);
@@ -360,7 +374,7 @@ __device__ __forceinline__ bool sphere_t(f3 center, float radius, const Ray& r, 
 }
 
 template <uint32_t FEAT>
-__device__ __forceinline__ f3 member_sphere_center(const rtw_launch& L, const rtw_dev_sphere& s, uint32_t idx,
+RTW_DHD f3 member_sphere_center(const rtw_launch& L, const rtw_dev_sphere& s, uint32_t idx,
                                                    float time) {
     f3 c = ld3(s.c1);
     if constexpr ((FEAT & RTW_F_MOVING) != 0) {
@@ -373,7 +387,7 @@ __device__ __forceinline__ f3 member_sphere_center(const rtw_launch& L, const rt
 }
 
 // Quad.hit t only (objects.zig:222-255), closed interval [tmin, tmax]
-__device__ __forceinline__ bool quad_t(const rtw_dev_quad& q, const Ray& r, float tmin, float tmax, float& t) {
+RTW_DHD bool quad_t(const rtw_dev_quad& q, const Ray& r, float tmin, float tmax, float& t) {
     const f3 n = ld3(q.n);
     const float denom = dot(n, r.d);
     if (__builtin_fabsf(denom) < 1e-8f) return false;
@@ -390,7 +404,7 @@ __device__ __forceinline__ bool quad_t(const rtw_dev_quad& q, const Ray& r, floa
 
 // world ray -> object space of an instance: the outermost transform first
 // (Translate.hit objects.zig:314-317, RotateY.hit :401-411)
-__device__ __forceinline__ Ray inst_to_object(const rtw_dev_instance* __restrict__ in, Ray r) {
+RTW_DHD Ray inst_to_object(const rtw_dev_instance* __restrict__ in, Ray r) {
     for (int k = (int)in->n_xf - 1; k >= 0; k--) {
         const float4 x = ldg4(in->xf[k]);
         if (fbits(x.x) == RTW_XF_TRANSLATE) {
@@ -408,7 +422,7 @@ __device__ __forceinline__ Ray inst_to_object(const rtw_dev_instance* __restrict
 }
 
 // object-space point/normal -> world: innermost transform first (RotateY.hit :419-435, Translate.hit :325-326)
-__device__ __forceinline__ void inst_to_world(const rtw_dev_instance* __restrict__ in, f3& p, f3& n) {
+RTW_DHD void inst_to_world(const rtw_dev_instance* __restrict__ in, f3& p, f3& n) {
     for (uint32_t k = 0; k < in->n_xf; k++) {
         const float4 x = ldg4(in->xf[k]);
         if (fbits(x.x) == RTW_XF_TRANSLATE) {
@@ -426,7 +440,7 @@ __device__ __forceinline__ void inst_to_world(const rtw_dev_instance* __restrict
 
 // HittableList.hit over the members in object space (objects.zig:281-289)
 template <uint32_t FEAT>
-__device__ __forceinline__ bool list_t(const rtw_launch& L, const rtw_dev_instance* __restrict__ in, const Ray& ro,
+RTW_DHD bool list_t(const rtw_launch& L, const rtw_dev_instance* __restrict__ in, const Ray& ro,
                                        float tmin, float tmax, float& t, uint32_t& sub) {
     bool any = false;
     float closest = tmax;
@@ -454,7 +468,7 @@ __device__ __forceinline__ bool list_t(const rtw_launch& L, const rtw_dev_instan
 
 // Hittable.hit of a sphere / quad / instance reference (a medium boundary)
 template <uint32_t FEAT>
-__device__ __forceinline__ bool boundary_t(const rtw_launch& L, uint32_t ref, const Ray& r, float tmin, float tmax,
+RTW_DHD bool boundary_t(const rtw_launch& L, uint32_t ref, const Ray& r, float tmin, float tmax,
                                            float& t) {
     const uint32_t idx = RTW_REF_INDEX(ref);
     switch (RTW_REF_KIND(ref)) {
@@ -473,7 +487,7 @@ __device__ __forceinline__ bool boundary_t(const rtw_launch& L, uint32_t ref, co
 
 // ConstantMedium.hit (objects.zig:470-507); the draw is keyed by (mkey, medium)
 template <uint32_t FEAT>
-__device__ __forceinline__ bool medium_t(const rtw_launch& L, uint32_t idx, const Ray& r, float tmin, float tmax,
+RTW_DHD bool medium_t(const rtw_launch& L, uint32_t idx, const Ray& r, float tmin, float tmax,
                                          uint64_t mkey, float& t) {
     const rtw_dev_medium m = L.media[idx];
     float t1, t2;
@@ -494,7 +508,7 @@ __device__ __forceinline__ bool medium_t(const rtw_launch& L, uint32_t idx, cons
 // A non-sphere leaf tested with (0.001, closest): updates closest / hit
 // (hit = node | member << 24 for an instance's list member)
 template <uint32_t FEAT>
-__device__ __forceinline__ void object_leaf(const rtw_launch& L, const Ray& r, uint32_t kind, uint32_t idx, uint32_t node,
+RTW_DHD void object_leaf(const rtw_launch& L, const Ray& r, uint32_t kind, uint32_t idx, uint32_t node,
                                          float& closest, int& hit, uint64_t mkey) {
     float t;
     uint32_t sub = 0;
@@ -516,17 +530,19 @@ __device__ __forceinline__ void object_leaf(const rtw_launch& L, const Ray& r, u
 // Node i of the pre-order walk: two 16-B loads issued together (both halves are
 // needed on either path; a split load would put a second memory round trip on
 // the inner-node path).
-__device__ __forceinline__ void load_node(const float4* __restrict__ nodes, uint32_t i, float4& A, float4& B) {
+RTW_DHD void load_node(const float4* __restrict__ nodes, uint32_t i, float4& A, float4& B) {
     A = nodes[2 * i];
     B = nodes[2 * i + 1];
+#if defined(__HIP_DEVICE_COMPILE__)
     asm volatile("" ::"v"(A.x), "v"(A.y), "v"(A.z), "v"(A.w), "v"(B.x), "v"(B.y), "v"(B.z), "v"(B.w));
+#endif
 }
 
 // Leaf: Sphere.hit (objects.zig:116-136) on the open interval (0.001, closest),
 // no box test (bvh.zig:123-125).  Updates closest/hit.
 // Sphere.hit (objects.zig:116-136) of a sphere at `center` with rr = radius * radius
 // (the reference's product, evaluated by the caller or on the host) on (0.001, closest).
-__device__ __forceinline__ void sphere_leaf(const rtw_launch& L, const Ray& r, const RayTrav& rt, f3 center, float rr,
+RTW_DHD void sphere_leaf(const rtw_launch& L, const Ray& r, const RayTrav& rt, f3 center, float rr,
                                             uint32_t i, float& closest, int& hit) {
     const f3 oc = r.o - center;
     const float half_b = dot(oc, r.d);
@@ -548,7 +564,7 @@ __device__ __forceinline__ void sphere_leaf(const rtw_launch& L, const Ray& r, c
         // The exact roots satisfy r1 <= r2 (a > 0), so one of them lies in (tmin, closest)
         // only if r2 > tmin and r1 < closest: with |r - q| <= e, only if q2 + e > tmin and
         // q1 - e < closest (a necessary condition; non-short-circuit & and |, no branches).
-        sa = __builtin_amdgcn_sqrtf(disc);
+        sa = RTW_SQRT_EST(disc);
         const float e = (__builtin_fabsf(half_b) + sa) * rt.rcp_a * 3.8146973e-06f;
         const float q1 = (-half_b - sa) * rt.rcp_a;
         const float q2 = (-half_b + sa) * rt.rcp_a;
@@ -586,7 +602,7 @@ __device__ __forceinline__ void sphere_leaf(const rtw_launch& L, const Ray& r, c
 }
 
 template <uint32_t FEAT>
-__device__ __forceinline__ void leaf_test(const rtw_launch& L, const Ray& r, const RayTrav& rt, float4 A, float4 B,
+RTW_DHD void leaf_test(const rtw_launch& L, const Ray& r, const RayTrav& rt, float4 A, float4 B,
                                           uint32_t i, float& closest, int& hit, Counters& cnt, uint64_t mkey = 0) {
     cnt.leaves++;
     if constexpr ((FEAT & RTW_F_GEOM) != 0) {
@@ -615,7 +631,7 @@ __device__ __forceinline__ void leaf_test(const rtw_launch& L, const Ray& r, con
 //  fast (SAH trees): t = fma(P, inv, -o*inv) with min/max instead of swaps, on
 //    boxes padded by E*2^-19 -- conservative (never rejects a box the exact test
 //    on the unpadded box accepts), so the closest hit is unchanged.
-__device__ __forceinline__ uint32_t box_next(const Ray& r, const RayTrav& rt, float4 A, float4 B, uint32_t i,
+RTW_DHD uint32_t box_next(const Ray& r, const RayTrav& rt, float4 A, float4 B, uint32_t i,
                                              float closest, bool fast) {
     const uint32_t w = fbits(A.w);
     if (fast) {
@@ -642,7 +658,7 @@ __device__ __forceinline__ uint32_t box_next(const Ray& r, const RayTrav& rt, fl
 // One node of the stackless pre-order walk of the reference BVH
 // (bvh.zig:122-136).  Returns the next node index.
 template <uint32_t FEAT>
-__device__ __forceinline__ uint32_t trav_step(const float4* __restrict__ nodes, const rtw_launch& L, const Ray& r,
+RTW_DHD uint32_t trav_step(const float4* __restrict__ nodes, const rtw_launch& L, const Ray& r,
                                               const RayTrav& rt, uint32_t i, float& closest, int& hit,
                                               Counters& cnt, uint64_t mkey = 0) {
     float4 A, B;
@@ -663,14 +679,14 @@ __device__ __forceinline__ uint32_t trav_step(const float4* __restrict__ nodes, 
 // slower: more node visits and no gain in coherence).  The copy is recorded in
 // the hit id (bits 24..26; such scenes have no instance members there) so
 // shading finds the leaf.
-__device__ __forceinline__ uint32_t order_of(const rtw_launch& L, const Ray& r) {
+RTW_DHD uint32_t order_of(const rtw_launch& L, const Ray& r) {
     if (L.n_orders <= 1) return 0;
     return (r.d.x < 0 ? 1u : 0u) | (r.d.y < 0 ? 2u : 0u) | (r.d.z < 0 ? 4u : 0u);
 }
-__device__ __forceinline__ const float4* order_base(const float4* nodes, const rtw_launch& L, uint32_t oct) {
+RTW_DHD const float4* order_base(const float4* nodes, const rtw_launch& L, uint32_t oct) {
     return nodes + (size_t)oct * 2u * L.n_nodes;
 }
-__device__ __forceinline__ int hit_with_order(int hit, uint32_t oct) {
+RTW_DHD int hit_with_order(int hit, uint32_t oct) {
     return hit < 0 ? hit : (int)((uint32_t)hit | (oct << RTW_HIT_NODE_BITS));
 }
 
@@ -679,12 +695,12 @@ __device__ __forceinline__ int hit_with_order(int hit, uint32_t oct) {
 // rounded outward, consumed by v_fma_mix_f32 (exact f16->f32, one rounding:
 // the same t = fma(P, inv, -o*inv) as box_next's fast test on a superset box);
 // leaves carry center and radius^2.  Same visits-superset argument: same hit.
-__device__ __forceinline__ float h_lo(uint32_t w) { return (float)__builtin_bit_cast(_Float16, (unsigned short)(w & 0xFFFFu)); }
-__device__ __forceinline__ float h_hi(uint32_t w) { return (float)__builtin_bit_cast(_Float16, (unsigned short)(w >> 16)); }
+RTW_DHD float h_lo(uint32_t w) { return (float)__builtin_bit_cast(_Float16, (unsigned short)(w & 0xFFFFu)); }
+RTW_DHD float h_hi(uint32_t w) { return (float)__builtin_bit_cast(_Float16, (unsigned short)(w >> 16)); }
 
 // `base`: L.cnodes, or their copy in LDS
 template <bool COUNT>
-__device__ __forceinline__ int traverse_compact(const rtw_launch& L, const uint4* base, const Ray& r, float& t_out,
+RTW_DHD int traverse_compact(const rtw_launch& L, const uint4* base, const Ray& r, float& t_out,
                                                 Counters& cnt) {
     const uint32_t oct = order_of(L, r);
     const uint4* __restrict__ cn = base + (size_t)oct * L.n_nodes;
@@ -705,8 +721,8 @@ __device__ __forceinline__ int traverse_compact(const rtw_launch& L, const uint4
         const uint4 c = cn[i];
         if (c.w & RTW_LEAF_BIT) {
             if constexpr (COUNT) cnt.leaves++;
-            sphere_leaf(L, r, rt, mk(__uint_as_float(c.x), __uint_as_float(c.y), __uint_as_float(c.z)),
-                        __uint_as_float(c.w & ~RTW_LEAF_BIT), i, closest, hit);
+            sphere_leaf(L, r, rt, mk(ubits(c.x), ubits(c.y), ubits(c.z)),
+                        ubits(c.w & ~RTW_LEAF_BIT), i, closest, hit);
             i++;
         } else {
             if constexpr (COUNT) cnt.nodes++;
@@ -729,7 +745,7 @@ __device__ __forceinline__ int traverse_compact(const rtw_launch& L, const uint4
 // `nodes` is the base of the node arrays (the octant copy is picked here).
 // COMPACT = false: walk `nodes` (e.g. their LDS stage) even where compact nodes exist.
 template <uint32_t FEAT, bool COMPACT = true>
-__device__ __forceinline__ int traverse(const float4* __restrict__ nodes, const rtw_launch& L, const Ray& r,
+RTW_DHD int traverse(const float4* __restrict__ nodes, const rtw_launch& L, const Ray& r,
                                         float& t_out, Counters& cnt, uint64_t mkey = 0) {
     if constexpr (COMPACT && (FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING)) == 0) {
         if (L.cnodes && L.fast_box) {  // per-step counters only in counted passes
@@ -749,7 +765,7 @@ __device__ __forceinline__ int traverse(const float4* __restrict__ nodes, const 
     return hit_with_order(hit, oct);
 }
 
-__device__ __forceinline__ f3 background(const rtw_launch& L, const Ray& r) {
+RTW_DHD f3 background(const rtw_launch& L, const Ray& r) {
     if (L.bg_mode == RTW_BG_GRADIENT) {  // camera.zig:204-206
         f3 ud = unit_vector(r.d);
         float a = 0.5f * (ud.y + 1.0f);
@@ -767,7 +783,7 @@ struct HitPrep {
 };
 
 // hit record of a quad, in the frame of ray r (Quad.hit objects.zig:237-254)
-__device__ __forceinline__ void quad_prep(const rtw_dev_quad& q, const Ray& r, float t, HitPrep& h) {
+RTW_DHD void quad_prep(const rtw_dev_quad& q, const Ray& r, float t, HitPrep& h) {
     h.p = r.o + splat(t) * r.d;
     const f3 planar = h.p - ld3(q.q);
     const f3 w = ld3(q.w);
@@ -781,7 +797,7 @@ __device__ __forceinline__ void quad_prep(const rtw_dev_quad& q, const Ray& r, f
 }
 
 template <uint32_t FEAT>
-__device__ __forceinline__ HitPrep object_prep(const rtw_launch& L, const Ray& r, uint32_t kind, uint32_t idx,
+RTW_DHD HitPrep object_prep(const rtw_launch& L, const Ray& r, uint32_t kind, uint32_t idx,
                                             uint32_t sub, float t) {
     HitPrep h;
     if (kind == RTW_OBJ_QUAD) {
@@ -829,7 +845,7 @@ __device__ __forceinline__ HitPrep object_prep(const rtw_launch& L, const Ray& r
 }
 
 template <uint32_t FEAT>
-__device__ __forceinline__ HitPrep hit_prep(const float4* __restrict__ nodes, const rtw_launch& L, const Ray& r,
+RTW_DHD HitPrep hit_prep(const float4* __restrict__ nodes, const rtw_launch& L, const Ray& r,
                                             int hit, float t) {
     if (L.n_orders > 1) {  // sphere scenes only: the octant copy the walk used
         nodes = order_base(nodes, L, (uint32_t)hit >> RTW_HIT_NODE_BITS);
@@ -864,7 +880,7 @@ __device__ __forceinline__ HitPrep hit_prep(const float4* __restrict__ nodes, co
 // Does Material.scatter start by drawing vec3.randomUnitVector?
 // (Lambertian material.zig:44, Metal :67, Isotropic :140)
 template <uint32_t FEAT>
-__device__ __forceinline__ bool needs_unit_vector(uint32_t kind) {
+RTW_DHD bool needs_unit_vector(uint32_t kind) {
     if (kind == RTW_MAT_LAMBERTIAN || kind == RTW_MAT_METAL) return true;
     if constexpr ((FEAT & RTW_F_LIGHT) != 0) return kind == RTW_MAT_ISOTROPIC;
     return false;
@@ -874,7 +890,7 @@ __device__ __forceinline__ bool needs_unit_vector(uint32_t kind) {
 // materials that draw one, the random unit vector `ruv` (already drawn from rng).
 // Adds thr*emission to acc; returns true with (att, sc) when the ray scatters.
 template <uint32_t FEAT>
-__device__ __forceinline__ bool scatter_finish(const rtw_launch& L, const Ray& r, const HitPrep& h, f3 ruv,
+RTW_DHD bool scatter_finish(const rtw_launch& L, const Ray& r, const HitPrep& h, f3 ruv,
                                                rtw_rng& rng, f3 thr, f3& acc, f3& att, Ray& sc) {
     const rtw_dev_material& m = h.m;
     sc.o = h.p;
@@ -925,7 +941,7 @@ __device__ __forceinline__ bool scatter_finish(const rtw_launch& L, const Ray& r
 
 // Sequential form (one lane at a time): used by v0 and the debug kernel.
 template <uint32_t FEAT>
-__device__ __forceinline__ bool shade(const float4* __restrict__ nodes, const rtw_launch& L, const Ray& r, int hit,
+RTW_DHD bool shade(const float4* __restrict__ nodes, const rtw_launch& L, const Ray& r, int hit,
                                       float t, rtw_rng& rng, f3 thr, f3& acc, f3& att, Ray& sc) {
     const HitPrep h = hit_prep<FEAT>(nodes, L, r, hit, t);
     f3 ruv = mk(0, 0, 0);
@@ -941,7 +957,7 @@ __device__ __forceinline__ bool shade(const float4* __restrict__ nodes, const rt
 // but measured -3 % on C2: removed)
 // ---------------------------------------------------------------------------
 template <int D>
-__device__ __forceinline__ void seq_reject(rtw_rng& rng, float (&out)[D]) {
+RTW_DHD void seq_reject(rtw_rng& rng, float (&out)[D]) {
     for (;;) {
         float w[D];
         float ls;
@@ -960,7 +976,7 @@ __device__ __forceinline__ void seq_reject(rtw_rng& rng, float (&out)[D]) {
 // Camera.getRay for every lane of the wave (`active` lanes get a ray): the same
 // draws in the same order as get_ray, the disk's rejection loop outside the
 // per-lane branch (one loop for the wave).
-__device__ __forceinline__ Ray get_ray_wave(const rtw_launch& L, bool active, uint32_t i, uint32_t j, rtw_rng& rng) {
+RTW_DHD Ray get_ray_wave(const rtw_launch& L, bool active, uint32_t i, uint32_t j, rtw_rng& rng) {
     const f3 du = ld3(L.du), dv = ld3(L.dv);
     f3 pixel_sample = mk(0, 0, 0);
     if (active) {
@@ -984,7 +1000,7 @@ __device__ __forceinline__ Ray get_ray_wave(const rtw_launch& L, bool active, ui
 
 // One sample's radiance: getRay + iterative rayColor (camera.zig:169-208).
 template <uint32_t FEAT>
-__device__ f3 sample_radiance(const float4* __restrict__ nodes, const rtw_launch& L, uint32_t pixel, uint32_t x,
+__host__ __device__ f3 sample_radiance(const float4* __restrict__ nodes, const rtw_launch& L, uint32_t pixel, uint32_t x,
                               uint32_t y, uint32_t s, Counters& cnt) {
     rtw_rng rng;
     rng.s = rtw_mix64(L.key0 ^ (((uint64_t)pixel << 32) | (uint64_t)s));
@@ -1008,7 +1024,7 @@ __device__ f3 sample_radiance(const float4* __restrict__ nodes, const rtw_launch
     return acc;
 }
 
-__device__ __forceinline__ bool map_row(const rtw_launch& L, uint32_t r, uint32_t& y) {
+RTW_DHD bool map_row(const rtw_launch& L, uint32_t r, uint32_t& y) {
     if (L.n_shards) {
         y = rtw_tile_row_image(L.rpb, L.n_shards, L.shard, r);
     } else {
@@ -1017,7 +1033,7 @@ __device__ __forceinline__ bool map_row(const rtw_launch& L, uint32_t r, uint32_
     return y < L.H;
 }
 
-__device__ __forceinline__ void flush_counters(const rtw_launch& L, const Counters& c, uint32_t samples) {
+RTW_DHD void flush_counters(const rtw_launch& L, const Counters& c, uint32_t samples) {
     if (!L.counters) return;
     atomicAdd(&L.counters[RTW_STAT_RAYS], (unsigned long long)c.rays);
     atomicAdd(&L.counters[RTW_STAT_NODES], (unsigned long long)c.nodes);
@@ -1027,6 +1043,6 @@ __device__ __forceinline__ void flush_counters(const rtw_launch& L, const Counte
     if (c.tail_rays) atomicAdd(&L.counters[RTW_STAT_TAIL_RAYS], (unsigned long long)c.tail_rays);
 }
 
-__device__ __forceinline__ bool is_nan3(f3 c) { return !(c.x == c.x) || !(c.y == c.y) || !(c.z == c.z); }
+RTW_DHD bool is_nan3(f3 c) { return !(c.x == c.x) || !(c.y == c.y) || !(c.z == c.z); }
 
 }  // namespace

@@ -152,6 +152,7 @@ void rtw_tuning_defaults(rtw_tuning* t) {
     t->mega_shade_min = 48;  // tuned on C2: 8..64 -> 48 best
     t->mega_waves = 1;
     t->mega_tile_order = 1;
+    t->cpu_threads = 0;
     t->wf_paths = 0;
 }
 
@@ -193,9 +194,12 @@ int rtw_scene_create_ex(const rtw_scene_desc* d, int device, const rtw_tuning* t
         if (im.width && im.height && (!im.data || im.bytes_per_row < 4 * im.width))
             return fail(RTW_E_INVALID, "bad image");
     }
-    int ndev = 0;
-    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(RTW_E_NODEVICE, "no HIP device visible");
-    if (device < 0 || device >= ndev) return fail(RTW_E_INVALID, "device index out of range");
+    const bool host = device == RTW_DEVICE_CPU;  // a host context: no GPU involved (rtw_cpu.hip)
+    if (!host) {
+        int ndev = 0;
+        if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(RTW_E_NODEVICE, "no HIP device visible");
+        if (device < 0 || device >= ndev) return fail(RTW_E_INVALID, "device index out of range");
+    }
 
     rtw_ctx* ctx = new rtw_ctx();
     ctx->device = device;
@@ -221,7 +225,7 @@ int rtw_scene_create_ex(const rtw_scene_desc* d, int device, const rtw_tuning* t
     // compact 16-B walk for static sphere SAH trees (rtw_compact_nodes)
     std::vector<rtw_cnode> cnodes;
     {
-        bool want = d->bvh_mode == RTW_BVH_SAH && !objects && ctx->box_pad > 0 && tu.compact_nodes;
+        bool want = d->bvh_mode == RTW_BVH_SAH && !objects && ctx->box_pad > 0 && tu.compact_nodes && !host;
         for (uint32_t i = 0; want && i < d->n_spheres; i++) want = !d->spheres[i].is_moving;
         if (want && !rtw_compact_nodes(ctx->nodes_host, orders, cnodes)) cnodes.clear();
     }
@@ -305,18 +309,20 @@ int rtw_scene_create_ex(const rtw_scene_desc* d, int device, const rtw_tuning* t
         if (nb) std::memcpy(blob.data() + o_imgs + img_info[i].offset, d->images[i].data, nb);
     }
 
-    hipError_t e = hipSetDevice(device);
-    // blocking stream: orders with the legacy NULL stream (torch's default), so a caller passing
-    // device buffers and stream == NULL sees its prior NULL-stream work (e.g. zero fills) complete first
-    if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->stream, hipStreamDefault);
-    if (e == hipSuccess) e = hipMalloc(&ctx->d_blob, off);
-    if (e == hipSuccess) e = hipMemcpy(ctx->d_blob, blob.data(), off, hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMalloc(&ctx->d_dbg, 64 * sizeof(float));
-    if (e == hipSuccess) e = hipMalloc(&ctx->d_work, 256);
-    if (e != hipSuccess) {
-        int code = hip_fail(e, "rtw_scene_create upload");
-        rtw_scene_destroy(ctx);
-        return code;
+    if (!host) {
+        hipError_t e = hipSetDevice(device);
+        // blocking stream: orders with the legacy NULL stream (torch's default), so a caller passing
+        // device buffers and stream == NULL sees its prior NULL-stream work (e.g. zero fills) complete first
+        if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->stream, hipStreamDefault);
+        if (e == hipSuccess) e = hipMalloc(&ctx->d_blob, off);
+        if (e == hipSuccess) e = hipMemcpy(ctx->d_blob, blob.data(), off, hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = hipMalloc(&ctx->d_dbg, 64 * sizeof(float));
+        if (e == hipSuccess) e = hipMalloc(&ctx->d_work, 256);
+        if (e != hipSuccess) {
+            int code = hip_fail(e, "rtw_scene_create upload");
+            rtw_scene_destroy(ctx);
+            return code;
+        }
     }
     ctx->blob_bytes = off;
     {   // FNV-1a 64 of the scene image (rtw_scene_hash)
@@ -324,7 +330,8 @@ int rtw_scene_create_ex(const rtw_scene_desc* d, int device, const rtw_tuning* t
         for (size_t i = 0; i < off; i++) h = (h ^ blob[i]) * 0x100000001B3ull;
         ctx->scene_hash = h;
     }
-    uint8_t* dev = static_cast<uint8_t*>(ctx->d_blob);
+    if (host) ctx->host_blob = blob;  // the launch pointers address the host copy
+    uint8_t* dev = host ? ctx->host_blob.data() : static_cast<uint8_t*>(ctx->d_blob);
     rtw_launch& L = ctx->base;
     L.nodes = reinterpret_cast<const float4*>(dev + o_nodes);
     L.cnodes = cnodes.empty() ? nullptr : reinterpret_cast<const uint4*>(dev + o_cnod);
@@ -353,14 +360,15 @@ int rtw_scene_create_ex(const rtw_scene_desc* d, int device, const rtw_tuning* t
         // allocation halves the batch on failure (run_wavefront)
         size_t free_b = 0, total_b = 0;
         uint64_t cap = 1ull << 29;
-        if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b)
+        if (!host && hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b)
             cap = std::min<uint64_t>(cap, (uint64_t)(0.35 * (double)free_b) / RTW_WF_PATH_BYTES);
         ctx->wf_max_paths = tu.wf_paths ? tu.wf_paths : std::max<uint64_t>(cap, 1u << 20);
     }
     ctx->wf_iters = tu.wf_iters;
     {
         int n_cu = 0;
-        if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || n_cu < 1)
+        if (host || hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
+            n_cu < 1)
             n_cu = 256;
         ctx->n_cu = n_cu;
     }
@@ -392,7 +400,12 @@ int rtw_scene_create_ex(const rtw_scene_desc* d, int device, const rtw_tuning* t
     // SAH trees: FMA slab test on the padded boxes (only enlarges the set of visited nodes;
     // reference trees keep the exact aabb.zig walk)
     L.fast_box = ctx->box_pad > 0 && tu.fast_box ? 1u : 0u;
-    ctx->grid = rtw_persistent_grid(ctx->feat, (uint32_t)n_nodes, (int)L.waves, L.use_lds != 0);
+    if (host) {  // the exact aabb.zig slab test and IEEE sphere test (the hardware estimates are device-only)
+        L.fast_box = 0;
+        L.fast_reject = 0;
+    }
+    ctx->cpu_threads = tu.cpu_threads;
+    ctx->grid = host ? 0 : rtw_persistent_grid(ctx->feat, (uint32_t)n_nodes, (int)L.waves, L.use_lds != 0);
 
     ctx->stats.n_nodes = (uint32_t)n_nodes;
     ctx->stats.n_leaves = d->objects ? d->n_objects : d->n_spheres;
@@ -406,6 +419,10 @@ int rtw_scene_create_ex(const rtw_scene_desc* d, int device, const rtw_tuning* t
 
 void rtw_scene_destroy(rtw_ctx* ctx) {
     if (!ctx) return;
+    if (ctx->device == RTW_DEVICE_CPU) {
+        delete ctx;
+        return;
+    }
     (void)hipSetDevice(ctx->device);
     if (ctx->last_done) (void)hipEventSynchronize(ctx->last_done);  // a render left on a caller's stream
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
@@ -658,6 +675,17 @@ int rtw_render(rtw_ctx* ctx, const rtw_camera* cam, uint32_t pix_begin, uint32_t
     if (spp_begin > spp_end) return fail(RTW_E_INVALID, "bad sample range");
     if (pix_begin == pix_end || spp_begin == spp_end) return RTW_OK;
     std::lock_guard<std::mutex> lock(ctx->mu);
+    if (ctx->device == RTW_DEVICE_CPU) {  // host context: Camera.render on host threads (rtw_cpu.hip)
+        rtw_launch L = make_launch(ctx, cam, seed);
+        L.s0 = spp_begin;
+        L.s1 = spp_end;
+        const int rc = rtw_cpu_render(L, pix_begin, pix_end, accum, ctx->cpu_threads, cancel);
+        if (rc == RTW_E_CANCELLED) return fail(rc, "cancelled");
+        if (progress && progress((uint64_t)(pix_end - pix_begin) * (spp_end - spp_begin),
+                                 (uint64_t)(pix_end - pix_begin) * (spp_end - spp_begin), user))
+            return fail(RTW_E_CANCELLED, "cancelled by progress callback");
+        return rc;
+    }
     HIP_TRY(hipSetDevice(ctx->device));
     if (int rc = stream_enter(ctx, ctx->stream)) return rc;
     const size_t bytes = (size_t)cam->size * 16;
@@ -696,6 +724,7 @@ int rtw_render(rtw_ctx* ctx, const rtw_camera* cam, uint32_t pix_begin, uint32_t
 int rtw_render_device(rtw_ctx* ctx, const rtw_camera* cam, uint32_t pix_begin, uint32_t pix_end, uint32_t spp_begin,
                       uint32_t spp_end, uint64_t seed, float* d_accum, void* stream, const rtw_render_opts* opts) {
     if (!ctx || !d_accum) return fail(RTW_E_INVALID, "null ctx/accum");
+    if (ctx->device == RTW_DEVICE_CPU) return fail(RTW_E_INVALID, "host context: use rtw_render");
     if (int rc = validate_cam(cam)) return rc;
     if (pix_end > cam->size || pix_begin > pix_end) return fail(RTW_E_INVALID, "pixel range out of image");
     if (spp_begin > spp_end) return fail(RTW_E_INVALID, "bad sample range");
@@ -747,6 +776,7 @@ int rtw_render_rows_device(rtw_ctx* ctx, const rtw_camera* cam, uint32_t rpb, ui
                            uint32_t spp_begin, uint32_t spp_end, uint64_t seed, float* d_tile, void* stream,
                            const rtw_render_opts* opts) {
     if (!ctx || !d_tile) return fail(RTW_E_INVALID, "null ctx/tile");
+    if (ctx->device == RTW_DEVICE_CPU) return fail(RTW_E_INVALID, "host context: use rtw_render");
     if (int rc = validate_cam(cam)) return rc;
     if (!rpb || !n_shards || shard >= n_shards) return fail(RTW_E_INVALID, "bad shard spec");
     if (spp_begin > spp_end) return fail(RTW_E_INVALID, "bad sample range");
@@ -804,6 +834,7 @@ int rtw_texture_from_accum(const float* accum, uint32_t n, uint8_t* out) {
 
 int rtw_debug_rng(rtw_ctx* ctx, uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t n, float* out) {
     if (!ctx || !out || n > 64) return fail(RTW_E_INVALID, "bad debug_rng args (n <= 64)");
+    if (ctx->device == RTW_DEVICE_CPU) return fail(RTW_E_INVALID, "host context");
     std::lock_guard<std::mutex> lock(ctx->mu);
     HIP_TRY(hipSetDevice(ctx->device));
     if (int rc = stream_enter(ctx, ctx->stream)) return rc;
@@ -818,6 +849,7 @@ int rtw_debug_rng(rtw_ctx* ctx, uint64_t seed, uint32_t pixel, uint32_t sample, 
 int rtw_debug_sample(rtw_ctx* ctx, const rtw_camera* cam, uint64_t seed, uint32_t pixel, uint32_t sample,
                      float out[3]) {
     if (!ctx || !out) return fail(RTW_E_INVALID, "null args");
+    if (ctx->device == RTW_DEVICE_CPU) return fail(RTW_E_INVALID, "host context");
     if (int rc = validate_cam(cam)) return rc;
     if (pixel >= cam->size) return fail(RTW_E_INVALID, "pixel out of range");
     std::lock_guard<std::mutex> lock(ctx->mu);

@@ -100,6 +100,9 @@ int rtw_persistent_grid(uint32_t feat, uint32_t n_nodes, int waves, bool use_lds
 
 void rtw_launch_render(const rtw_launch& L, void* stream, int variant, int grid);
 void rtw_set_error(const char* msg);  // the thread's rtw_last_error() message (rtw_host.hip)
+// host backend (rtw_cpu.hip): samples [L.s0, L.s1) of pixels [pix_begin, pix_end) onto host float4 accum
+int rtw_cpu_render(const rtw_launch& L, uint32_t pix_begin, uint32_t pix_end, float* accum, uint32_t threads,
+                   const volatile int32_t* cancel);
 void rtw_launch_debug_rng(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t n, float* d_out, void* stream);
 void rtw_launch_debug_sample(const rtw_launch& L, uint32_t pixel, uint32_t sample, float* d_out, void* stream);
 
@@ -167,7 +170,8 @@ int rtw_build_bvh(const rtw_scene_desc& desc, std::vector<rtw_node>& nodes, rtw_
 
 // One scene on one device (the opaque rtw_ctx of include/rtw_gpu.h).
 struct rtw_ctx {
-    int device = 0;
+    int device = 0;                // RTW_DEVICE_CPU: a host context (rtw_cpu.hip)
+    std::vector<uint8_t> host_blob;  // host context: the scene image the launch pointers address
     hipStream_t stream = nullptr;
     void* d_blob = nullptr;        // single allocation holding every scene array
     size_t blob_bytes = 0;
@@ -185,6 +189,7 @@ struct rtw_ctx {
     uint64_t wf_cap = 0;
     uint64_t wf_max_paths = 1u << 26;  // paths per wavefront batch (x RTW_WF_PATH_BYTES); set at scene creation
     uint32_t wf_iters = 9;         // wavefront bounces before the tail kernel (rtw_tuning.wf_iters)
+    uint32_t cpu_threads = 0;      // host context: worker threads (rtw_tuning.cpu_threads; 0 = all)
     int n_cu = 256;                // compute units of the device (wavefront grids)
     std::vector<hipEvent_t> ev_pool;  // recycled timing events
     uint64_t scene_hash = 0;       // FNV-1a 64 of the uploaded scene image

@@ -185,9 +185,9 @@ int rtw_multi_create(rtw_ctx* const* ctxs, uint32_t n, rtw_multi** out) {
     if (!ctxs || n == 0) return mfail(RTW_E_INVALID, "no contexts");
     rtw_multi* m = new rtw_multi();
     for (uint32_t k = 0; k < n; k++) {
-        if (!ctxs[k]) {
+        if (!ctxs[k] || ctxs[k]->device == RTW_DEVICE_CPU) {
             delete m;
-            return mfail(RTW_E_INVALID, "null context");
+            return mfail(RTW_E_INVALID, "null or host context");
         }
         for (uint32_t j = 0; j < k; j++)
             if (ctxs[j]->device == ctxs[k]->device) {
