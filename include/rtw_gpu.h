@@ -310,7 +310,7 @@ typedef struct rtw_tuning {
     uint32_t mega_waves;       /* persistent kernel: launch-bound variant (default 1; 1, 6 or 8) */
     uint32_t mega_tile_order;  /* persistent kernel: 1 = last tile row first (default) */
     uint32_t cpu_threads;      /* host context (RTW_DEVICE_CPU): render threads, 0 = every available core */
-    uint32_t _pad0;
+    uint32_t wide_walk;        /* 1 = two-wide stack walk for static sphere SAH trees read through L1/L2 (default) */
     uint64_t wf_paths;         /* wavefront batch capacity in paths; 0 = auto (2^29 within 35 % of free memory) */
 } rtw_tuning;
 

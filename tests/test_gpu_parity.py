@@ -314,13 +314,16 @@ def test_v1_knobs_invariant(rtw, book1, knob):
 
 @pytest.mark.parametrize("knob", [{"wf_iters": 1}, {"wf_iters": 50}, {"wf_paths": 4096}, {"fast_box": 0},
                                   {"lds": 127 & ~1}, {"sah_max_leaf": 4}, {"compact_nodes": 0}, {"lds": 127 & ~2},
-                                  {"fuse": 0}, {"fuse": 1}, {"lds": 127 & ~4}, {"bvh_orders": 1}])
+                                  {"fuse": 0}, {"fuse": 1}, {"lds": 127 & ~4}, {"bvh_orders": 1},
+                                  {"lds": 127 & ~2, "wide_walk": 0}, {"fuse": 5}, {"lds": 127 & ~2, "fuse": 5},
+                                  {"lds": 127 & ~2, "fuse": 5, "wide_walk": 0}])
 def test_wavefront_knobs_invariant(rtw, book1, knob):
     """Wavefront tuning (rtw_tuning: bounces before the tail kernel, batch size ->
     many batches, FMA vs reference slab test, LDS-staged nodes, SAH leaf runs of up
     to 4 spheres, 16-B fp16-box nodes vs 32-B nodes, compact nodes in LDS, fused
     gen+trace+shade kernel vs separate kernels, LDS vs L1/L2 tail, materials in LDS,
-    one node ordering instead of 8) never changes a pixel."""
+    one node ordering instead of 8, the two-wide stack walk through L1/L2 vs the
+    octant-ordered compact walk, the fused step through L1/L2) never changes a pixel."""
     arr, world = book1
     cam = rtw.book1_camera(image_width=300, aspect_ratio=1.5, spp=5).init()
     ref = render_rows(rtw, world, cam, 0, 200, 0, 5, 4)
@@ -333,18 +336,20 @@ def test_wavefront_knobs_invariant(rtw, book1, knob):
 @pytest.mark.parametrize("n,seed", [(20000, 3), (100000, 0)])
 def test_compact_nodes_are_exact(rtw, n, seed):
     """The 16-B node walk (fp16 inner boxes rounded outward, leaves with radius^2)
-    visits a superset of the 32-B walk's boxes: identical images on dense stress
+    and the two-wide stack walk (fp16 child boxes, leaf boxes padded like inner ones)
+    visit a superset of the 32-B walk's boxes: identical images on dense stress
     worlds (small spheres far from the origin: the coarsest fp16 boxes), at the
     BASELINE config-4 camera."""
     arr = rtw.flatten(rtw.worlds.stress_world(n, seed), bvh_mode=rtw._abi.RTW_BVH_SAH)
     cam = rtw.book1_camera(image_width=480, aspect_ratio=16 / 9, spp=4).init()
     outs = []
-    for c in (0, 1):
-        w = rtw.World(arr, tuning={"compact_nodes": c})
+    for tu in ({"compact_nodes": 0}, {"compact_nodes": 1, "wide_walk": 0}, {"compact_nodes": 1, "wide_walk": 1}):
+        w = rtw.World(arr, tuning=tu)
         outs.append(render_rows(rtw, w, cam, 0, cam.derived.image_height, 0, 4, 6))
         w.close()
     assert np.isfinite(outs[1]).all()
     assert np.array_equal(outs[0], outs[1])
+    assert np.array_equal(outs[0], outs[2])  # the two-wide stack walk (rtw_wide2_nodes): same hits
 
 
 @pytest.mark.parametrize("scene", ["book1", "stress"])

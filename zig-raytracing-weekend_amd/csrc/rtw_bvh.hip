@@ -700,3 +700,69 @@ bool rtw_compact_nodes(const std::vector<rtw_node>& nodes, uint32_t orders, std:
     }
     return true;
 }
+
+// ---------------------------------------------------------------------------
+// Two-wide nodes for the stack walk of large static sphere SAH trees (trees the
+// kernels read through L1/L2, e.g. the 100 k-sphere stress scene).  One 32-B
+// record per inner node of ordering 0 holds BOTH children, so a walk step tests
+// two children after one dependent load, and the near inner child is chosen per
+// ray at run time instead of by 8 octant-ordered copies: 1/8 of the footprint in
+// L1/L2 and about half the dependent loads per ray.
+//   slot k (v[4k .. 4k+3]) of an inner child: box per axis min | max << 16 (fp16
+//           rounded outward, a superset of the padded box), then the child's record
+//           index (pre-order over the inner nodes, root 0)
+//   slot k of a leaf child: the sphere in place -- center.xyz (fp32), bits(r * r) |
+//           RTW_LEAF_BIT (as the compact nodes), tested with no box (bvh.zig:123-125)
+// leaf_id[2 * record + k] = the leaf's index in ordering 0: the hit id the shading
+// reads (looked up once per ray, after the walk).
+// *max_stack = the most entries the walk can push (the max inner depth).
+bool rtw_wide2_nodes(const std::vector<rtw_node>& nodes, uint32_t n_per, std::vector<rtw_cnode>& out,
+                     std::vector<uint32_t>& leaf_id, uint32_t* max_stack) {
+    auto word = [&](uint32_t i) {
+        uint32_t w;
+        std::memcpy(&w, &nodes[i].a[3], 4);
+        return w;
+    };
+    if (n_per < 3 || nodes.size() < n_per || (word(0) & RTW_LEAF_BIT)) return false;
+    std::vector<uint32_t> widx(n_per, 0), depth(n_per, 0);
+    uint32_t n_inner = 0;
+    for (uint32_t i = 0; i < n_per; i++)
+        if (!(word(i) & RTW_LEAF_BIT)) widx[i] = n_inner++;
+    out.assign(2 * (size_t)n_inner, rtw_cnode{});
+    leaf_id.assign(2 * (size_t)n_inner, 0u);
+    depth[0] = 1;
+    uint32_t dmax = 1;
+    auto next = [&](uint32_t j) { return (word(j) & RTW_LEAF_BIT) ? j + 1 : (word(j) & RTW_SKIP_MASK); };
+    for (uint32_t i = 0; i < n_per; i++) {
+        if (word(i) & RTW_LEAF_BIT) continue;
+        const uint32_t c[2] = {i + 1, next(i + 1)};
+        if (c[1] >= n_per || next(c[1]) != (word(i) & RTW_SKIP_MASK)) return false;  // not a binary tree
+        for (int k = 0; k < 2; k++) {
+            const uint32_t j = c[k];
+            const rtw_node& n = nodes[j];
+            const size_t slot = 2 * (size_t)widx[i] + k;
+            rtw_cnode& o = out[slot];
+            if (word(j) & RTW_LEAF_BIT) {
+                uint32_t mv;
+                std::memcpy(&mv, &n.b[3], 4);
+                const float rr = n.b[0] * n.b[0];
+                uint32_t rb;
+                std::memcpy(&rb, &rr, 4);
+                if (mv || !(rr >= 0) || !std::isfinite(rr) || (rb & RTW_LEAF_BIT)) return false;
+                std::memcpy(&o.v[0], &n.a[0], 12);
+                o.v[3] = rb | RTW_LEAF_BIT;
+                leaf_id[slot] = j;
+                continue;
+            }
+            for (int a = 0; a < 3; a++) {  // padded by rtw_build_bvh
+                if (!(std::fabs(n.a[a]) <= 60000.0f) || !(std::fabs(n.b[a]) <= 60000.0f)) return false;
+                o.v[a] = (uint32_t)h_down(n.a[a]) | ((uint32_t)h_up(n.b[a]) << 16);
+            }
+            o.v[3] = widx[j];
+            depth[j] = depth[i] + 1;
+            dmax = std::max(dmax, depth[j]);
+        }
+    }
+    if (max_stack) *max_stack = dmax;
+    return true;
+}

@@ -153,6 +153,7 @@ void rtw_tuning_defaults(rtw_tuning* t) {
     t->mega_waves = 1;
     t->mega_tile_order = 1;
     t->cpu_threads = 0;
+    t->wide_walk = 1;
     t->wf_paths = 0;
 }
 
@@ -229,6 +230,14 @@ int rtw_scene_create_ex(const rtw_scene_desc* d, int device, const rtw_tuning* t
         for (uint32_t i = 0; want && i < d->n_spheres; i++) want = !d->spheres[i].is_moving;
         if (want && !rtw_compact_nodes(ctx->nodes_host, orders, cnodes)) cnodes.clear();
     }
+    // two-wide records for the stack walk of trees read through L1/L2 (rtw_wide2_nodes)
+    std::vector<rtw_cnode> w2;
+    std::vector<uint32_t> w2leaf;
+    uint32_t w2_stack = 0;
+    if (!cnodes.empty() && tu.wide_walk && tu.sah_max_leaf <= 1 &&
+        !rtw_wide2_nodes(ctx->nodes_host, (uint32_t)(ctx->nodes_host.size() / orders), w2, w2leaf, &w2_stack))
+        w2.clear();
+    if (w2_stack > RTW_W2_STACK_MAX) w2.clear();
 
     // Blob layout (each section 256-B aligned): nodes | cvec | spheres | quads | members | instances | media |
     // materials | textures | images-info | perlin | image bytes
@@ -258,6 +267,9 @@ int rtw_scene_create_ex(const rtw_scene_desc* d, int device, const rtw_tuning* t
         img_bytes += align((size_t)d->images[i].bytes_per_row * d->images[i].height);
     }
     off = align(off + img_bytes + 16);
+    const size_t hashed = off;  // the scene image; the walk's derived records below are a tuning choice
+    const size_t o_w2 = off; off = align(off + w2.size() * sizeof(rtw_cnode));
+    const size_t o_w2l = off; off = align(off + w2leaf.size() * sizeof(uint32_t));
 
     std::vector<uint8_t> blob(off, 0);
     std::memcpy(blob.data() + o_nodes, ctx->nodes_host.data(), ctx->nodes_host.size() * sizeof(rtw_node));
@@ -265,6 +277,8 @@ int rtw_scene_create_ex(const rtw_scene_desc* d, int device, const rtw_tuning* t
         if (nb) std::memcpy(blob.data() + o, src, nb);
     };
     put(o_cnod, cnodes.data(), cnodes.size() * sizeof(rtw_cnode));
+    put(o_w2, w2.data(), w2.size() * sizeof(rtw_cnode));
+    put(o_w2l, w2leaf.data(), w2leaf.size() * sizeof(uint32_t));
     put(o_cvec, cvec.data(), cvec.size() * sizeof(float));
     put(o_sph, geom.spheres.data(), geom.spheres.size() * sizeof(rtw_dev_sphere));
     put(o_quad, geom.quads.data(), geom.quads.size() * sizeof(rtw_dev_quad));
@@ -327,7 +341,7 @@ int rtw_scene_create_ex(const rtw_scene_desc* d, int device, const rtw_tuning* t
     ctx->blob_bytes = off;
     {   // FNV-1a 64 of the scene image (rtw_scene_hash)
         uint64_t h = 0xCBF29CE484222325ull;
-        for (size_t i = 0; i < off; i++) h = (h ^ blob[i]) * 0x100000001B3ull;
+        for (size_t i = 0; i < hashed; i++) h = (h ^ blob[i]) * 0x100000001B3ull;
         ctx->scene_hash = h;
     }
     if (host) ctx->host_blob = blob;  // the launch pointers address the host copy
@@ -335,6 +349,9 @@ int rtw_scene_create_ex(const rtw_scene_desc* d, int device, const rtw_tuning* t
     rtw_launch& L = ctx->base;
     L.nodes = reinterpret_cast<const float4*>(dev + o_nodes);
     L.cnodes = cnodes.empty() ? nullptr : reinterpret_cast<const uint4*>(dev + o_cnod);
+    L.w2nodes = w2.empty() ? nullptr : reinterpret_cast<const uint4*>(dev + o_w2);
+    L.w2leaf = w2.empty() ? nullptr : reinterpret_cast<const uint32_t*>(dev + o_w2l);
+    L.w2_stack = w2.empty() ? 0u : w2_stack;
     L.cvec = reinterpret_cast<const float4*>(dev + o_cvec);
     L.sph = reinterpret_cast<const rtw_dev_sphere*>(dev + o_sph);
     L.quads = reinterpret_cast<const rtw_dev_quad*>(dev + o_quad);

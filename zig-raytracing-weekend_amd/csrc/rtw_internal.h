@@ -18,6 +18,8 @@ struct rtw_launch {
     // scene (device pointers)
     const float4* nodes;
     const uint4* cnodes;         // compact 16-B copy of `nodes` (static sphere SAH trees) or null
+    const uint4* w2nodes;        // two-wide records of ordering 0 (rtw_wide2_nodes) or null
+    const uint32_t* w2leaf;      // their leaf slots' hit ids (ordering-0 leaf index)
     const float4* cvec;          // per-sphere center_vec (moving spheres)
     const rtw_dev_sphere* sph;   // every sphere (instance members)
     const rtw_dev_quad* quads;
@@ -31,6 +33,7 @@ struct rtw_launch {
     const float4* perlin;        // RTW_PERLIN_BYTES per table
     uint32_t n_nodes;
     uint32_t n_perlin;
+    uint32_t w2_stack;           // entries of the two-wide walk's per-lane LDS stack (its max depth)
 
     // camera (Camera.init outputs, src/camera.zig:118-154)
     float center[3], pixel00[3], du[3], dv[3], disk_u[3], disk_v[3], background[3];
@@ -163,6 +166,11 @@ struct rtw_cnode {
 };
 // false: the tree cannot be encoded (coordinates beyond fp16 range, non-finite radius)
 bool rtw_compact_nodes(const std::vector<rtw_node>& nodes, uint32_t orders, std::vector<rtw_cnode>& out);
+
+// two-wide 32-B records (2 x rtw_cnode per inner node) of ordering 0 for the stack walk of large static
+// sphere SAH trees (rtw_bvh.hip rtw_wide2_nodes); false: not encodable (leaf runs, fp16 range)
+bool rtw_wide2_nodes(const std::vector<rtw_node>& nodes, uint32_t n_per, std::vector<rtw_cnode>& out,
+                     std::vector<uint32_t>& leaf_id, uint32_t* max_stack);
 
 int rtw_build_bvh(const rtw_scene_desc& desc, std::vector<rtw_node>& nodes, rtw_geometry& geom,
                   uint32_t* depth, uint32_t* axis_draws, float* box_pad = nullptr, float* extent = nullptr,

@@ -8,6 +8,7 @@
 #define RTW_WF_MAX_ITERS 100
 #define RTW_WF_STRIPES 256    // output queues (one atomic counter each)
 #define RTW_WF_LEN_STRIDE 16  // counters 64 B apart
+#define RTW_W2_STACK_MAX 32   // deepest per-lane LDS stack of the two-wide walk (256 threads x 32 x 4 B = 32 KiB)
 
 // One batch: n_pix logical pixels (8x8 tiles over the launch rows) x n_s samples.
 // Path p = s_local * n_pix + q.

@@ -178,6 +178,90 @@ __device__ __forceinline__ rtw_launch stage_geom(const rtw_launch& L, float4* ld
     return G;
 }
 
+// The two-wide stack walk (rtw_bvh.hip rtw_wide2_nodes: large static sphere SAH trees
+// read through L1/L2).  Each step loads one 32-B record: a leaf child's sphere is
+// tested at once (Sphere.hit on (0.001, closest), objects.zig:116-136, no box:
+// bvh.zig:123-125), an inner child's box with the FMA slab test of the compact walk
+// (fp16 bounds, supersets of the padded boxes); of two entered inner children the
+// nearer is walked first and the other pushed.  Any visiting order of a superset
+// of the boxes the reference walk enters finds the same closest hit (bvh.zig:122-136
+// keeps the nearest root; Interval.surrounds is strict).  The hit id is the leaf's
+// index in ordering 0 (octant bits 0).  Per-lane stack in the kernel's dynamic LDS,
+// entry k at [k * 256 + threadIdx.x] (256-thread blocks, L.w2_stack entries each:
+// the tree's inner depth, so it never overflows).
+__device__ __forceinline__ void w2_box(uint4 c, const RayTrav& rt, uint32_t sx, uint32_t sy, uint32_t sz,
+                                       float closest, float& lo, float& hi) {
+    // per axis the (near | far << 16) pair of this ray: swapped where the direction is negative
+    const uint32_t x = __builtin_amdgcn_perm(c.x, c.x, sx), y = __builtin_amdgcn_perm(c.y, c.y, sy),
+                   z = __builtin_amdgcn_perm(c.z, c.z, sz);
+    const float tnx = __builtin_fmaf(h_lo(x), rt.inv.x, rt.oinv.x), tfx = __builtin_fmaf(h_hi(x), rt.inv.x, rt.oinv.x);
+    const float tny = __builtin_fmaf(h_lo(y), rt.inv.y, rt.oinv.y), tfy = __builtin_fmaf(h_hi(y), rt.inv.y, rt.oinv.y);
+    const float tnz = __builtin_fmaf(h_lo(z), rt.inv.z, rt.oinv.z), tfz = __builtin_fmaf(h_hi(z), rt.inv.z, rt.oinv.z);
+    lo = __builtin_fmaxf(__builtin_fmaxf(kTmin, tnx), __builtin_fmaxf(tny, tnz));
+    hi = __builtin_fminf(__builtin_fminf(closest, tfx), __builtin_fminf(tfy, tfz));
+}
+
+template <bool COUNT>
+__device__ __forceinline__ int traverse_wide2(const rtw_launch& L, const Ray& r, float& t_out, Counters& cnt) {
+    extern __shared__ uint32_t wf_w2_stack[];
+    uint32_t* __restrict__ stk = wf_w2_stack + threadIdx.x;
+    const RayTrav rt = ray_trav(r, true);
+    constexpr uint32_t KEEP = 0x03020100u, SWAP = 0x01000302u;  // v_perm_b32 byte selectors
+    const uint32_t sx = rt.inv.x < 0.0f ? SWAP : KEEP, sy = rt.inv.y < 0.0f ? SWAP : KEEP,
+                   sz = rt.inv.z < 0.0f ? SWAP : KEEP;
+    const uint4* __restrict__ wn = L.w2nodes;
+    float closest = kInf;
+    int hit = -1;  // the record slot 2 * node + k of the closest sphere
+    uint32_t node = 0, sp = 0;
+    for (;;) {
+        const uint4 a = wn[2u * node], b = wn[2u * node + 1u];
+        const bool f0 = (a.w & RTW_LEAF_BIT) != 0, f1 = (b.w & RTW_LEAF_BIT) != 0;
+        if (f0) {
+            if constexpr (COUNT) cnt.leaves++;
+            sphere_leaf(L, r, rt, mk(ubits(a.x), ubits(a.y), ubits(a.z)), ubits(a.w & ~RTW_LEAF_BIT), 2u * node,
+                        closest, hit);
+        }
+        if (f1) {
+            if constexpr (COUNT) cnt.leaves++;
+            sphere_leaf(L, r, rt, mk(ubits(b.x), ubits(b.y), ubits(b.z)), ubits(b.w & ~RTW_LEAF_BIT),
+                        2u * node + 1u, closest, hit);
+        }
+        if constexpr (COUNT) cnt.nodes += (f0 ? 0u : 1u) + (f1 ? 0u : 1u);
+        float lo0, hi0, lo1, hi1;
+        w2_box(a, rt, sx, sy, sz, closest, lo0, hi0);
+        w2_box(b, rt, sx, sy, sz, closest, lo1, hi1);
+        // next node without nested control flow (an if / else-if chain with the exit in one arm
+        // compiles to nested loops: lanes that pop wait for the lanes that descend).  (Stack
+        // entries carrying their entry distance, so that stale ones are dropped unloaded, measured
+        // slower: C4 trace +4 %.)
+        const bool i0 = !f0 && !(hi0 <= lo0), i1 = !f1 && !(hi1 <= lo1);
+        const bool second = lo1 < lo0;
+        uint32_t nxt = (i0 && !(i1 && second)) ? a.w : b.w;
+        if (i0 && i1) stk[sp * 256u] = second ? a.w : b.w;
+        sp += (i0 && i1) ? 1u : 0u;
+        const bool pop = !(i0 || i1), done = pop && sp == 0;
+        if (pop && !done) {
+            sp--;
+            nxt = stk[sp * 256u];
+        }
+        if (done) break;
+        node = nxt;
+    }
+    t_out = closest;
+    return hit < 0 ? hit : (int)L.w2leaf[hit];
+}
+
+// the walk of a static sphere scene through L1/L2: two-wide when the records exist
+template <uint32_t FEAT>
+__device__ __forceinline__ int wf_traverse_global(const rtw_launch& L, const Ray& r, float& t, Counters& cnt,
+                                                  uint64_t mkey) {
+    if constexpr ((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING)) == 0) {
+        if (L.w2nodes)
+            return L.counters ? traverse_wide2<true>(L, r, t, cnt) : traverse_wide2<false>(L, r, t, cnt);
+    }
+    return traverse<FEAT>(L.nodes, L, r, t, cnt, mkey);
+}
+
 // trace: closest hit per ray of the input set (no shading state in registers)
 template <uint32_t FEAT, bool LDS>
 __global__ __launch_bounds__(256) void wf_trace(rtw_launch L, rtw_wf W, uint32_t it) {
@@ -227,7 +311,7 @@ __global__ __launch_bounds__(256) void wf_trace(rtw_launch L, rtw_wf W, uint32_t
             const Ray r = wf_load_ray(S, slot, depth);
             if (depth) {
                 float t;
-                const int h = traverse<FEAT>(L.nodes, L, r, t, cnt, wf_mkey<FEAT>(S, slot));
+                const int h = wf_traverse_global<FEAT>(L, r, t, cnt, wf_mkey<FEAT>(S, slot));
                 W.hit[slot] = make_float2(t, __int_as_float(h));
                 cnt.rays++;
             }
@@ -373,7 +457,7 @@ __device__ __forceinline__ void wf_tail_body(const rtw_launch& L, const rtw_wf& 
                 hit = L.counters ? traverse_compact<true>(L, lds, r, t, cnt) : traverse_compact<false>(L, lds, r, t, cnt);
             else
                 hit = nodes ? traverse<FEAT, false>(nodes, L, r, t, cnt, rng.s)  // the LDS stage
-                            : traverse<FEAT>(L.nodes, L, r, t, cnt, rng.s);
+                            : wf_traverse_global<FEAT>(L, r, t, cnt, rng.s);
             bool done = true;
             if (hit < 0) {
                 acc = acc + thr * background(L, r);
@@ -476,7 +560,7 @@ __device__ __forceinline__ int wf_walk(const rtw_launch& L, const void* lds, con
     } else if constexpr (WALK == WALK_LDS) {
         return traverse<FEAT, false>(static_cast<const float4*>(lds), L, r, t, cnt, mkey);  // the LDS stage
     } else {
-        return traverse<FEAT>(L.nodes, L, r, t, cnt, mkey);
+        return wf_traverse_global<FEAT>(L, r, t, cnt, mkey);
     }
 }
 
@@ -702,6 +786,25 @@ uint32_t wf_grid(K kernel, int n_cu, size_t lds = 0, uint32_t threads = 256) {
     return g ? g : per;
 }
 
+// the same, cached per host thread for one dynamic LDS size (c = {grid, lds + 1})
+template <typename K>
+uint32_t wf_grid_cached(K kernel, int n_cu, size_t lds, uint32_t (&c)[2]) {
+    if (c[1] != lds + 1) {
+        c[0] = wf_grid(kernel, n_cu, lds);
+        c[1] = (uint32_t)(lds + 1);
+    }
+    return c[0];
+}
+
+// dynamic LDS of the kernels that walk through L1/L2: the two-wide walk's per-lane stacks
+template <uint32_t FEAT>
+size_t wf_w2_lds(const rtw_launch& L) {
+    if constexpr ((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING)) == 0) {
+        if (L.w2nodes) return (size_t)256u * 4u * L.w2_stack;
+    }
+    return 0;
+}
+
 template <uint32_t FEAT>
 struct WfGrids {
     uint32_t trace, shade, tail;
@@ -744,8 +847,8 @@ void wf_run_fused(const rtw_launch& L, const rtw_wf& W, hipStream_t st, int n_cu
                  ldyn = lds + (L.perlin_lds ? (size_t)L.n_perlin * RTW_PERLIN_BYTES : 0) +
                         ((FEAT & RTW_F_GEOM) ? L.geom_lds : 0u) + L.shade_lds,
                  tdyn = lds + ((FEAT & RTW_F_GEOM) ? L.geom_lds : 0u) + L.shade_lds,
-                 gdyn = 0;
-    thread_local uint32_t cgrid[2] = {0, 0}, tgrid[2] = {0, 0}, lgrid[2] = {0, 0}, ggrid = 0;
+                 gdyn = wf_w2_lds<FEAT>(L);
+    thread_local uint32_t cgrid[2] = {0, 0}, tgrid[2] = {0, 0}, lgrid[2] = {0, 0}, ggrid[2] = {0, 0}, wtail[2] = {0, 0};
     uint32_t grid = 0;
     if constexpr ((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING)) == 0) {
         if (clds && cgrid[1] != cdyn) {
@@ -763,8 +866,7 @@ void wf_run_fused(const rtw_launch& L, const rtw_wf& W, hipStream_t st, int n_cu
         }
         grid = lgrid[0];
     } else {
-        if (!ggrid) ggrid = wf_grid(wf_step<FEAT, false>, n_cu, gdyn);
-        grid = ggrid;
+        grid = wf_grid_cached(wf_step<FEAT, false>, n_cu, gdyn, ggrid);
     }
     // iteration 0 appends to len[1]; every later iteration's output counters are
     // zeroed by the kernel two iterations before (wf_step_zero_next)
@@ -808,7 +910,9 @@ void wf_run_fused(const rtw_launch& L, const rtw_wf& W, hipStream_t st, int n_cu
             hipLaunchKernelGGL(wf_tail_lds<FEAT>, dim3(tl[0]), dim3(256), tdyn, st, L, W, iters);
             done = true;
         }
-        if (!done) hipLaunchKernelGGL(wf_tail<FEAT>, dim3(wf_grids<FEAT>(n_cu).tail), dim3(256), 0, st, L, W, iters);
+        if (!done)
+            hipLaunchKernelGGL(wf_tail<FEAT>, dim3(wf_grid_cached(wf_tail<FEAT>, n_cu, gdyn, wtail)), dim3(256), gdyn, st,
+                               L, W, iters);
         RTW_TIME_END(T)
     }
     RTW_TIME_BEGIN(T, RTW_K_REDUCE)
@@ -841,6 +945,8 @@ void wf_run(const rtw_launch& L, const rtw_wf& W, hipStream_t st, int n_cu, rtw_
     hipLaunchKernelGGL(wf_gen<FEAT>, dim3((W.n_paths + 255u) / 256u), dim3(256), 0, st, L, W);
     RTW_TIME_END(T)
     const uint32_t iters = L.max_depth < W.iters ? L.max_depth : W.iters;
+    const size_t w2l = wf_w2_lds<FEAT>(L);  // the two-wide walk's stacks (trace / tail through L1/L2)
+    thread_local uint32_t wtrace[2] = {0, 0}, wtail[2] = {0, 0};
     const size_t lds_need = (size_t)L.n_nodes * L.n_orders * 32u;
     const size_t lds = (L.wf_lds && lds_need <= RTW_WF_LDS_MAX)
                            ? (lds_need + 511u) / 512u * 512u : 0;
@@ -873,7 +979,8 @@ void wf_run(const rtw_launch& L, const rtw_wf& W, hipStream_t st, int n_cu, rtw_
         if (lds)
             hipLaunchKernelGGL((wf_trace<FEAT, true>), dim3(lds_grid), dim3(256), tlds, st, L, W, it);
         else
-            hipLaunchKernelGGL((wf_trace<FEAT, false>), dim3(g.trace), dim3(256), 0, st, L, W, it);
+            hipLaunchKernelGGL((wf_trace<FEAT, false>), dim3(wf_grid_cached(wf_trace<FEAT, false>, n_cu, w2l, wtrace)),
+                               dim3(256), w2l, st, L, W, it);
         RTW_TIME_END(T)
     shade_step:
         RTW_TIME_BEGIN(T, RTW_K_SHADE)
@@ -892,7 +999,8 @@ void wf_run(const rtw_launch& L, const rtw_wf& W, hipStream_t st, int n_cu, rtw_
             }
             hipLaunchKernelGGL(wf_tail_lds<FEAT>, dim3(tl[0]), dim3(256), tdyn, st, L, W, iters);
         } else {
-            hipLaunchKernelGGL(wf_tail<FEAT>, dim3(g.tail), dim3(256), 0, st, L, W, iters);
+            hipLaunchKernelGGL(wf_tail<FEAT>, dim3(wf_grid_cached(wf_tail<FEAT>, n_cu, w2l, wtail)), dim3(256), w2l, st, L,
+                               W, iters);
         }
         RTW_TIME_END(T)
     }
