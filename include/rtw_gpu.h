@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define RTW_ABI_VERSION 3
+#define RTW_ABI_VERSION 4
 
 enum rtw_status {
     RTW_OK = 0,
@@ -312,6 +312,8 @@ typedef struct rtw_tuning {
     uint32_t cpu_threads;      /* host context (RTW_DEVICE_CPU): render threads, 0 = every available core */
     uint32_t wide_walk;        /* 1 = two-wide stack walk for static sphere SAH trees read through L1/L2 (default) */
     uint64_t wf_paths;         /* wavefront batch capacity in paths; 0 = auto (2^29 within 35 % of free memory) */
+    uint32_t tile_lists;       /* 1 = camera rays of small static sphere trees test per-8x8-tile candidate lists (default) (ABI 4) */
+    uint32_t _pad1;
 } rtw_tuning;
 
 void rtw_tuning_defaults(rtw_tuning* out);

@@ -314,7 +314,7 @@ def test_v1_knobs_invariant(rtw, book1, knob):
 
 @pytest.mark.parametrize("knob", [{"wf_iters": 1}, {"wf_iters": 50}, {"wf_paths": 4096}, {"fast_box": 0},
                                   {"lds": 127 & ~1}, {"sah_max_leaf": 4}, {"compact_nodes": 0}, {"lds": 127 & ~2},
-                                  {"fuse": 0}, {"fuse": 1}, {"lds": 127 & ~4}, {"bvh_orders": 1},
+                                  {"fuse": 0}, {"fuse": 1}, {"lds": 127 & ~4}, {"bvh_orders": 1}, {"tile_lists": 0},
                                   {"lds": 127 & ~2, "wide_walk": 0}, {"fuse": 5}, {"lds": 127 & ~2, "fuse": 5},
                                   {"lds": 127 & ~2, "fuse": 5, "wide_walk": 0}])
 def test_wavefront_knobs_invariant(rtw, book1, knob):
@@ -322,7 +322,8 @@ def test_wavefront_knobs_invariant(rtw, book1, knob):
     many batches, FMA vs reference slab test, LDS-staged nodes, SAH leaf runs of up
     to 4 spheres, 16-B fp16-box nodes vs 32-B nodes, compact nodes in LDS, fused
     gen+trace+shade kernel vs separate kernels, LDS vs L1/L2 tail, materials in LDS,
-    one node ordering instead of 8, the two-wide stack walk through L1/L2 vs the
+    one node ordering instead of 8, camera rays against per-tile candidate lists vs
+    the walk, the two-wide stack walk through L1/L2 vs the
     octant-ordered compact walk, the fused step through L1/L2) never changes a pixel."""
     arr, world = book1
     cam = rtw.book1_camera(image_width=300, aspect_ratio=1.5, spp=5).init()

@@ -110,7 +110,8 @@ class RtwTuning(C.Structure):
                 ("compact_nodes", C.c_uint32), ("fast_box", C.c_uint32), ("fast_reject", C.c_uint32),
                 ("lds", C.c_uint32), ("fuse", C.c_uint32), ("wf_iters", C.c_uint32), ("mega_shade_min", C.c_uint32),
                 ("mega_waves", C.c_uint32), ("mega_tile_order", C.c_uint32), ("cpu_threads", C.c_uint32),
-                ("wide_walk", C.c_uint32), ("wf_paths", C.c_uint64)]
+                ("wide_walk", C.c_uint32), ("wf_paths", C.c_uint64),
+                ("tile_lists", C.c_uint32), ("_pad1", C.c_uint32)]
 
 
 def tuning(**fields) -> RtwTuning:

@@ -154,6 +154,7 @@ void rtw_tuning_defaults(rtw_tuning* t) {
     t->mega_tile_order = 1;
     t->cpu_threads = 0;
     t->wide_walk = 1;
+    t->tile_lists = 1;
     t->wf_paths = 0;
 }
 
@@ -352,6 +353,7 @@ int rtw_scene_create_ex(const rtw_scene_desc* d, int device, const rtw_tuning* t
     L.w2nodes = w2.empty() ? nullptr : reinterpret_cast<const uint4*>(dev + o_w2);
     L.w2leaf = w2.empty() ? nullptr : reinterpret_cast<const uint32_t*>(dev + o_w2l);
     L.w2_stack = w2.empty() ? 0u : w2_stack;
+    L.tile_lists = tu.tile_lists ? 1u : 0u;
     L.cvec = reinterpret_cast<const float4*>(dev + o_cvec);
     L.sph = reinterpret_cast<const rtw_dev_sphere*>(dev + o_sph);
     L.quads = reinterpret_cast<const rtw_dev_quad*>(dev + o_quad);
@@ -449,6 +451,7 @@ void rtw_scene_destroy(rtw_ctx* ctx) {
     if (ctx->d_dbg) (void)hipFree(ctx->d_dbg);
     if (ctx->d_work) (void)hipFree(ctx->d_work);
     if (ctx->d_wf) (void)hipFree(ctx->d_wf);
+    if (ctx->d_tl) (void)hipFree(ctx->d_tl);
     for (hipEvent_t e : ctx->ev_pool) (void)hipEventDestroy(e);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
@@ -604,6 +607,24 @@ int run_wavefront(rtw_ctx* ctx, rtw_launch L, hipStream_t stream, rtw_timer* T) 
     for (int k = 0; k < 3; k++) W.len[k] = reinterpret_cast<uint32_t*>(take(RTW_WF_STRIPES * RTW_WF_LEN_STRIDE * 4));
     W.n_pix = (uint32_t)n_pix;
     W.iters = ctx->wf_iters;
+    // camera-ray candidate lists (the compact-LDS fused step of static sphere scenes, rtw_tuning.tile_lists)
+    if (L.tile_lists && L.cnodes && L.n_orders == 8) {
+        const uint64_t tiles = n_pix / 64;
+        if (ctx->tl_cap < tiles) {
+            if (ctx->d_tl) {
+                HIP_TRY(hipStreamSynchronize(stream));
+                (void)hipFree(ctx->d_tl);
+            }
+            ctx->d_tl = nullptr;
+            ctx->tl_cap = 0;
+            if (hipMalloc(&ctx->d_tl, tiles * RTW_TL_BYTES + 256) == hipSuccess) ctx->tl_cap = tiles;
+            else (void)hipGetLastError();  // no lists: the walk
+        }
+        if (ctx->tl_cap >= tiles) {
+            W.tl = static_cast<uint4*>(ctx->d_tl);
+            W.tl_count = reinterpret_cast<uint32_t*>(static_cast<char*>(ctx->d_tl) + tiles * RTW_TL_MAX * 32);
+        }
+    }
     const uint32_t s_end = L.s1;
     for (uint32_t s = L.s0; s < s_end; s += (uint32_t)n_s) {
         L.s0 = s;

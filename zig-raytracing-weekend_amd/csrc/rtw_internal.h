@@ -34,6 +34,7 @@ struct rtw_launch {
     uint32_t n_nodes;
     uint32_t n_perlin;
     uint32_t w2_stack;           // entries of the two-wide walk's per-lane LDS stack (its max depth)
+    uint32_t tile_lists;         // camera rays of the compact-LDS fused step test per-tile candidate lists
 
     // camera (Camera.init outputs, src/camera.zig:118-154)
     float center[3], pixel00[3], du[3], dv[3], disk_u[3], disk_v[3], background[3];
@@ -193,6 +194,8 @@ struct rtw_ctx {
     uint32_t feat = 0;             // RTW_F_* scene features
     int grid = 0;                  // resident blocks of the persistent kernel
     int variant = 2;               // 2 = wavefront v2 (default), 1 = persistent v1, 0 = simple v0 (rtw_tuning.kernel)
+    void* d_tl = nullptr;          // camera-ray tile candidate lists (rtw_wavefront.h), tl_cap tiles
+    uint64_t tl_cap = 0;
     void* d_wf = nullptr;          // wavefront path state (rtw_wavefront.h), wf_cap paths
     uint64_t wf_cap = 0;
     uint64_t wf_max_paths = 1u << 26;  // paths per wavefront batch (x RTW_WF_PATH_BYTES); set at scene creation

@@ -8,6 +8,9 @@
 #define RTW_WF_MAX_ITERS 100
 #define RTW_WF_STRIPES 256    // output queues (one atomic counter each)
 #define RTW_WF_LEN_STRIDE 16  // counters 64 B apart
+#define RTW_TL_MAX 32          // camera-ray candidate list entries per 8x8 tile (more: the tile walks the tree)
+#define RTW_TL_WALK 0xFFFFFFFFu
+#define RTW_TL_BYTES (RTW_TL_MAX * 32 + 4)  // per tile
 #define RTW_W2_STACK_MAX 32   // deepest per-lane LDS stack of the two-wide walk (256 threads x 32 x 4 B = 32 KiB)
 
 // One batch: n_pix logical pixels (8x8 tiles over the launch rows) x n_s samples.
@@ -43,6 +46,8 @@ struct rtw_wf {
     uint32_t* len[3];   // stripe lengths of iteration it's input: len[it % 3][s * RTW_WF_LEN_STRIDE]
                         // (three sets: a fused step kernel zeroes the counters of
                         // iteration it+2 while it appends to those of it+1)
+    uint4* tl;          // camera-ray candidate lists: tile t's entry k at tl[2 * (t * RTW_TL_MAX + k)] (2 x 16 B)
+    uint32_t* tl_count; // candidates of tile t, or RTW_TL_WALK (too many: walk the tree); null = off
     uint32_t n_pix, n_s, n_paths, n_tx;
     uint32_t stripe_cap;
     uint32_t iters;     // wavefront iterations before the tail kernel

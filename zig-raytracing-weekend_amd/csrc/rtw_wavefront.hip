@@ -262,6 +262,140 @@ __device__ __forceinline__ int wf_traverse_global(const rtw_launch& L, const Ray
     return traverse<FEAT>(L.nodes, L, r, t, cnt, mkey);
 }
 
+// ---------------------------------------------------------------------------
+// Camera-ray candidate lists (iteration 0 of the compact-LDS fused step).
+// A wave's camera rays are one 8x8 tile of one sample (wf_pixel), and every ray of
+// the tile starts on the defocus disk and passes through the tile's pixel rectangle
+// widened by the +-0.5 jitter (Camera.getRay, camera.zig:169-180).  wf_tile_lists
+// keeps, per tile, every sphere such a ray can reach (a conservative superset,
+// margins far above fp32 rounding) sorted by a lower bound of its ray parameter;
+// the step then runs the exact Sphere.hit (objects.zig:116-136, the walk's
+// sphere_leaf) on the list in order -- the same code on every lane of the wave, no
+// divergent walk -- and stops once every lane's closest hit is nearer than the next
+// candidate's bound.  The closest of a superset of the spheres the walk would test
+// is the same hit (bvh.zig:122-136 keeps the nearest root), so the image is the
+// same; the hit id is the ordering-0 leaf index, as the two-wide walk's.  A tile
+// with more than RTW_TL_MAX candidates walks the tree.
+//
+// Geometry: with f the unit normal of the pixel plane (du x dv) and h its distance
+// from the camera centre (the focus distance), every ray's depth grows by h per unit
+// of t, so all rays reach depth z = (C - centre).f at t = z / h, where they lie in
+// the tile's rectangle scaled by t plus a disk of radius |1 - t| * r_disk.  A ray
+// passes within rho of C only if that cross-section comes within rho * sec(phi) of
+// C (phi: the largest angle of a ray to f); a hit has depth >= z - rho, i.e.
+// t >= (z - rho) / h.  Spheres reaching the camera plane (z <= rho) are always kept.
+__global__ __launch_bounds__(64) void wf_tile_lists(rtw_launch L, rtw_wf W) {
+    __shared__ float s_t[RTW_TL_MAX];
+    __shared__ uint32_t s_id[RTW_TL_MAX];
+    const uint32_t tile = blockIdx.x, lane = threadIdx.x;
+    uint32_t pixel, out_idx, x = 0, y = 0;
+    const bool ok = wf_pixel(L, W, tile * 64u + lane, pixel, out_idx, x, y);
+    float x0 = ok ? (float)x : 1e30f, x1 = ok ? (float)x : -1e30f, y0 = ok ? (float)y : 1e30f, y1 = ok ? (float)y : -1e30f;
+    for (int o = 32; o > 0; o >>= 1) {
+        x0 = fminf(x0, __shfl_xor(x0, o));
+        x1 = fmaxf(x1, __shfl_xor(x1, o));
+        y0 = fminf(y0, __shfl_xor(y0, o));
+        y1 = fmaxf(y1, __shfl_xor(y1, o));
+    }
+    if (!(x0 <= x1)) {  // no pixel of the tile is rendered
+        if (lane == 0) W.tl_count[tile] = 0;
+        return;
+    }
+    const f3 du = ld3(L.du), dv = ld3(L.dv), ctr = ld3(L.center);
+    const f3 fw = cross(du, dv);
+    const float fl = __builtin_sqrtf(length_squared(fw)), ul = __builtin_sqrtf(length_squared(du)),
+                vl = __builtin_sqrtf(length_squared(dv));
+    const f3 fz = divs(fw, fl), uh = divs(du, ul), vh = divs(dv, vl);
+    const f3 p0 = ld3(L.pixel00) - ctr;
+    const float h = dot(p0, fz), pu = dot(p0, uh), pv = dot(p0, vh);
+    // the pixel plane must face the rays and du, dv be orthogonal (Camera.init); else walk
+    const bool frame = h > 0.0f && fl > 0.0f && __builtin_fabsf(dot(du, dv)) <= 1e-4f * ul * vl;
+    const float off = (float)L.pixel_offset;
+    const float ru0 = pu + (x0 + off - 0.5f) * ul, ru1 = pu + (x1 + off + 0.5f) * ul;
+    const float rv0 = pv + (y0 + off - 0.5f) * vl, rv1 = pv + (y1 + off + 0.5f) * vl;
+    const float rd = L.defocus_angle > 0 ? fmaxf(__builtin_sqrtf(length_squared(ld3(L.disk_u))),
+                                                 __builtin_sqrtf(length_squared(ld3(L.disk_v)))) : 0.0f;
+    const float mu = fmaxf(__builtin_fabsf(ru0), __builtin_fabsf(ru1)), mv = fmaxf(__builtin_fabsf(rv0), __builtin_fabsf(rv1));
+    const float tphi = (__builtin_sqrtf(mu * mu + mv * mv) + rd) / h;
+    const float sec = __builtin_sqrtf(1.0f + tphi * tphi) * 1.001f;
+    uint32_t count = 0;
+    bool over = !frame;
+    for (uint32_t base = 0; base < L.n_nodes && !over; base += 64u) {
+        const uint32_t k = base + lane;
+        bool cand = false;
+        float tlow = 0.0f;
+        if (k < L.n_nodes) {
+            const uint4 c = L.cnodes[k];  // ordering 0
+            if (c.w & RTW_LEAF_BIT) {
+                const f3 cc = mk(ubits(c.x), ubits(c.y), ubits(c.z)) - ctr;
+                const float rho = __builtin_sqrtf(ubits(c.w & ~RTW_LEAF_BIT));
+                const float z = dot(cc, fz), cu = dot(cc, uh), cv = dot(cc, vh);
+                const float slack = 1e-3f * (__builtin_fabsf(z) + __builtin_fabsf(cu) + __builtin_fabsf(cv) + rho) + 1e-5f;
+                if (!(z > rho + slack)) {
+                    cand = true;  // reaches the camera plane (or NaN): always tested
+                } else {
+                    const float t = z / h;
+                    const float dx = fmaxf(0.0f, fmaxf(t * ru0 - cu, cu - t * ru1));
+                    const float dy = fmaxf(0.0f, fmaxf(t * rv0 - cv, cv - t * rv1));
+                    const float gap = __builtin_sqrtf(dx * dx + dy * dy) - __builtin_fabsf(1.0f - t) * rd;
+                    cand = !(gap > rho * sec + slack);
+                    tlow = fmaxf(0.0f, (z - rho - slack) / h * 0.9999f);
+                }
+            }
+        }
+        const uint64_t m = __ballot(cand);
+        const uint32_t n = (uint32_t)__popcll(m);
+        if (count + n > RTW_TL_MAX) {
+            over = true;
+            break;
+        }
+        if (cand) {
+            const uint32_t at = count + (uint32_t)__popcll(m & ((lane == 0) ? 0ull : (~0ull >> (64 - lane))));
+            s_t[at] = tlow;
+            s_id[at] = k;
+        }
+        count += n;
+    }
+    if (over) {
+        if (lane == 0) W.tl_count[tile] = RTW_TL_WALK;
+        return;
+    }
+    __syncthreads();
+    if (lane < count) {  // rank by (bound, index): sorted front to back
+        const float me = s_t[lane];
+        uint32_t rank = 0;
+        for (uint32_t j = 0; j < count; j++) rank += (s_t[j] < me || (s_t[j] == me && j < lane)) ? 1u : 0u;
+        const uint32_t id = s_id[lane];
+        const uint4 c = L.cnodes[id];
+        uint4* e = W.tl + 2u * ((size_t)tile * RTW_TL_MAX + rank);
+        e[0] = make_uint4(c.x, c.y, c.z, c.w & ~RTW_LEAF_BIT);
+        e[1] = make_uint4(id, fbits(me), 0u, 0u);
+    }
+    if (lane == 0) W.tl_count[tile] = count;
+}
+
+// The closest hit of a camera ray from its tile's list (wave-uniform: every lane of
+// the wave is a ray of `tile`); RTW_TL_WALK -> false (walk the tree)
+template <bool COUNT>
+__device__ __forceinline__ bool wf_tile_hit(const rtw_launch& L, const rtw_wf& W, uint32_t tile, const Ray& r, int& hit,
+                                            float& t_out, Counters& cnt) {
+    tile = __builtin_amdgcn_readfirstlane(tile);
+    const uint32_t n = W.tl_count[tile];
+    if (n == RTW_TL_WALK) return false;
+    const RayTrav rt = ray_trav(r, true);
+    const uint4* __restrict__ e = W.tl + 2u * (size_t)tile * RTW_TL_MAX;
+    float closest = kInf;
+    hit = -1;
+    for (uint32_t k = 0; k < n; k++) {
+        const uint4 a = e[2u * k], b = e[2u * k + 1u];
+        if (!__ballot(!(closest < ubits(b.y)))) break;  // every lane's hit is nearer than the rest can be
+        if constexpr (COUNT) cnt.leaves++;
+        sphere_leaf(L, r, rt, mk(ubits(a.x), ubits(a.y), ubits(a.z)), ubits(a.w), b.x, closest, hit);
+    }
+    t_out = closest;
+    return true;
+}
+
 // trace: closest hit per ray of the input set (no shading state in registers)
 template <uint32_t FEAT, bool LDS>
 __global__ __launch_bounds__(256) void wf_trace(rtw_launch L, rtw_wf W, uint32_t it) {
@@ -622,7 +756,16 @@ __device__ __forceinline__ void wf_step_body(const rtw_launch& L, const rtw_wf& 
             bool hitp = false, need_uv = false;
             if (live) {
                 float t;
-                const int hit = wf_walk<FEAT, WALK>(L, lds, r, t, cnt, rng.s);
+                int hit = -1;
+                bool listed = false;
+                if constexpr (WALK == WALK_CLDS) {  // camera rays: the tile's candidate list
+                    if (it == 0 && W.tl_count) {
+                        const uint32_t tile = (slot - (slot / W.n_pix) * W.n_pix) >> 6;
+                        listed = L.counters ? wf_tile_hit<true>(L, W, tile, r, hit, t, cnt)
+                                            : wf_tile_hit<false>(L, W, tile, r, hit, t, cnt);
+                    }
+                }
+                if (!listed) hit = wf_walk<FEAT, WALK>(L, lds, r, t, cnt, rng.s);
                 cnt.rays++;
                 if (hit < 0) {
                     acc = acc + thr * background(L, r);
@@ -872,6 +1015,9 @@ void wf_run_fused(const rtw_launch& L, const rtw_wf& W, hipStream_t st, int n_cu
     // zeroed by the kernel two iterations before (wf_step_zero_next)
     (void)hipMemsetAsync(W.len[1], 0, RTW_WF_STRIPES * RTW_WF_LEN_STRIDE * 4, st);
     const uint32_t iters = L.max_depth < W.iters ? L.max_depth : W.iters;
+    rtw_wf Wt = W;  // the camera-ray lists only serve the compact-LDS step
+    if (!clds || !W.tl_count || iters == 0) Wt.tl_count = nullptr;
+    if (Wt.tl_count) hipLaunchKernelGGL(wf_tile_lists, dim3(W.n_pix / 64u), dim3(64), 0, st, L, Wt);
     // rayColor(depth <= 0) = 0 (camera.zig:183-185): no iteration writes W.ls, which holds the
     // previous render's radiance, so the reduce must add zeros
     if (iters == 0) (void)hipMemsetAsync(W.ls, 0, (size_t)W.n_paths * sizeof(float4), st);
@@ -881,7 +1027,7 @@ void wf_run_fused(const rtw_launch& L, const rtw_wf& W, hipStream_t st, int n_cu
             if (clds) {
                 rtw_launch Lc = L;  // the materials are staged only when they fit
                 if (cdyn == cdyn0) Lc.mat_lds = 0;
-                hipLaunchKernelGGL(wf_step_clds<FEAT>, dim3(grid), dim3(1024), cdyn, st, Lc, W, it);
+                hipLaunchKernelGGL(wf_step_clds<FEAT>, dim3(grid), dim3(1024), cdyn, st, Lc, Wt, it);
                 RTW_TIME_END(T)
                 continue;
             }
