@@ -34,7 +34,8 @@ struct rtw_launch {
     uint32_t n_nodes;
     uint32_t n_perlin;
     uint32_t w2_stack;           // entries of the two-wide walk's per-lane LDS stack (its max depth)
-    uint32_t tile_lists;         // camera rays of the compact-LDS fused step test per-tile candidate lists
+    uint32_t tile_lists;         // camera rays of the fused step of static sphere scenes test per-tile candidate
+                                 // lists of at most this many spheres (0 = off; more candidates: the walk)
 
     // camera (Camera.init outputs, src/camera.zig:118-154)
     float center[3], pixel00[3], du[3], dv[3], disk_u[3], disk_v[3], background[3];

@@ -8,7 +8,7 @@
 #define RTW_WF_MAX_ITERS 100
 #define RTW_WF_STRIPES 256    // output queues (one atomic counter each)
 #define RTW_WF_LEN_STRIDE 16  // counters 64 B apart
-#define RTW_TL_MAX 32          // camera-ray candidate list entries per 8x8 tile (more: the tile walks the tree)
+#define RTW_TL_MAX 64          // camera-ray candidate list capacity per 8x8 tile (rtw_tuning.tile_lists caps it)
 #define RTW_TL_WALK 0xFFFFFFFFu
 #define RTW_TL_BYTES (RTW_TL_MAX * 32 + 4)  // per tile
 #define RTW_W2_STACK_MAX 32   // deepest per-lane LDS stack of the two-wide walk (256 threads x 32 x 4 B = 32 KiB)

@@ -275,7 +275,7 @@ __device__ __forceinline__ int wf_traverse_global(const rtw_launch& L, const Ray
 // candidate's bound.  The closest of a superset of the spheres the walk would test
 // is the same hit (bvh.zig:122-136 keeps the nearest root), so the image is the
 // same; the hit id is the ordering-0 leaf index, as the two-wide walk's.  A tile
-// with more than RTW_TL_MAX candidates walks the tree.
+// with more than L.tile_lists candidates walks the tree.
 //
 // Geometry: with f the unit normal of the pixel plane (du x dv) and h its distance
 // from the camera centre (the focus distance), every ray's depth grows by h per unit
@@ -345,7 +345,7 @@ __global__ __launch_bounds__(64) void wf_tile_lists(rtw_launch L, rtw_wf W) {
         }
         const uint64_t m = __ballot(cand);
         const uint32_t n = (uint32_t)__popcll(m);
-        if (count + n > RTW_TL_MAX) {
+        if (count + n > L.tile_lists) {
             over = true;
             break;
         }
@@ -758,7 +758,8 @@ __device__ __forceinline__ void wf_step_body(const rtw_launch& L, const rtw_wf& 
                 float t;
                 int hit = -1;
                 bool listed = false;
-                if constexpr (WALK == WALK_CLDS) {  // camera rays: the tile's candidate list
+                if constexpr (WALK != WALK_GLOBAL && (FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING)) == 0) {
+                    // camera rays: the tile's candidate list
                     if (it == 0 && W.tl_count) {
                         const uint32_t tile = (slot - (slot / W.n_pix) * W.n_pix) >> 6;
                         listed = L.counters ? wf_tile_hit<true>(L, W, tile, r, hit, t, cnt)
@@ -1015,8 +1016,9 @@ void wf_run_fused(const rtw_launch& L, const rtw_wf& W, hipStream_t st, int n_cu
     // zeroed by the kernel two iterations before (wf_step_zero_next)
     (void)hipMemsetAsync(W.len[1], 0, RTW_WF_STRIPES * RTW_WF_LEN_STRIDE * 4, st);
     const uint32_t iters = L.max_depth < W.iters ? L.max_depth : W.iters;
-    rtw_wf Wt = W;  // the camera-ray lists only serve the compact-LDS step
-    if (!clds || !W.tl_count || iters == 0) Wt.tl_count = nullptr;
+    rtw_wf Wt = W;  // the camera-ray lists serve the LDS-staged steps of static sphere scenes
+    if ((!clds && !lds) || !W.tl_count || iters == 0 || (FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING)))
+        Wt.tl_count = nullptr;
     if (Wt.tl_count) hipLaunchKernelGGL(wf_tile_lists, dim3(W.n_pix / 64u), dim3(64), 0, st, L, Wt);
     // rayColor(depth <= 0) = 0 (camera.zig:183-185): no iteration writes W.ls, which holds the
     // previous render's radiance, so the reduce must add zeros
@@ -1033,7 +1035,7 @@ void wf_run_fused(const rtw_launch& L, const rtw_wf& W, hipStream_t st, int n_cu
             }
         }
         if (lds)
-            hipLaunchKernelGGL((wf_step<FEAT, true>), dim3(grid), dim3(256), ldyn, st, L, W, it);
+            hipLaunchKernelGGL((wf_step<FEAT, true>), dim3(grid), dim3(256), ldyn, st, L, Wt, it);
         else
             hipLaunchKernelGGL((wf_step<FEAT, false>), dim3(grid), dim3(256), gdyn, st, L, W, it);
         RTW_TIME_END(T)
