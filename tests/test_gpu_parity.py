@@ -458,3 +458,28 @@ def test_c3_geometry_multi_batch_and_shards(rtw, oracle, book1, oracle_book1):
     img.index_copy_(0, torch.tensor(dst, device="cuda"),
                     tiles.view(-1, W, 4).index_select(0, torch.tensor(src, device="cuda")))
     assert torch.equal(img.view(-1, 4), full)
+
+
+@pytest.mark.parametrize("cam_seed", range(6))
+def test_tile_lists_random_cameras(rtw, book1, cam_seed):
+    """The camera-ray candidate lists (wf_tile_lists: a conservative superset of the
+    spheres a tile's jittered, defocused rays can reach) never change a pixel, for
+    random cameras: inside and around the sphere field, wide and narrow fields of
+    view, strong defocus, near focus planes, the +1 pixel quirk -- bit-identical to
+    the walk."""
+    arr, _ = book1
+    g = np.random.default_rng(100 + cam_seed)
+    lookfrom = tuple(float(v) for v in g.uniform([-14, 0.3, -14], [14, 6, 14]))
+    lookat = tuple(float(v) for v in g.uniform([-4, 0, -4], [4, 1.5, 4]))
+    cam = rtw.Camera(aspect_ratio=float(g.uniform(0.6, 2.0)), image_width=int(g.integers(96, 200)),
+                     samples_per_pixel=3, max_depth=8, background_mode=rtw._abi.RTW_BG_GRADIENT,
+                     vfov=float(g.uniform(8, 100)), lookfrom=lookfrom, lookat=lookat,
+                     defocus_angle=float(g.choice([0.0, 0.6, 4.0, 12.0])),
+                     focus_dist=float(g.uniform(0.5, 20))).init()
+    outs = []
+    for tl in (0, 1):
+        w = rtw.World(arr, tuning={"tile_lists": tl})
+        outs.append(render_rows(rtw, w, cam, 0, cam.derived.image_height, 0, 3, cam_seed))
+        w.close()
+    assert np.isfinite(outs[1]).all()
+    assert np.array_equal(outs[0], outs[1])
