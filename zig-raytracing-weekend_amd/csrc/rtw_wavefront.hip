@@ -513,7 +513,9 @@ __device__ __forceinline__ void wf_shade_body(const rtw_launch& L, const rtw_wf&
         f3 thr = mk(0, 0, 0), acc = mk(0, 0, 0);
         rtw_rng rng;
         rng.s = 0;
-        Ray sc;
+        Ray sc, rin;
+        HitPrep hp;
+        bool hitp = false, need_uv = false;
         if (e.get(W, slot)) {
             const Ray r = wf_load_ray(S, slot, depth);
             if (depth) {
@@ -525,15 +527,36 @@ __device__ __forceinline__ void wf_shade_body(const rtw_launch& L, const rtw_wf&
                     acc = acc + thr * background(L, r);
                 } else {
                     rng.s = S.rng[slot];
-                    f3 att;
-                    if (shade<FEAT>(L.nodes, L, r, hit, h.x, rng, thr, acc, att, sc) && depth > 1) {
-                        thr = thr * att;
-                        push = true;
+                    if constexpr ((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM)) == 0) {
+                        // sphere scenes: the split form of the fused step (hit record, then one
+                        // randomUnitVector rejection loop for the wave, then the material)
+                        hp = hit_prep<FEAT>(L.nodes, L, r, hit, h.x);
+                        hitp = true;
+                        need_uv = needs_unit_vector<FEAT>(hp.m.kind);
+                        rin = r;
+                    } else {
+                        f3 att;
+                        if (shade<FEAT>(L.nodes, L, r, hit, h.x, rng, thr, acc, att, sc) && depth > 1) {
+                            thr = thr * att;
+                            push = true;
+                        }
                     }
                 }
-                if (!push) W.ls[pid] = make_float4(acc.x, acc.y, acc.z, 0);
             }
         }
+        if constexpr ((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM)) == 0) {
+            float uv3[3] = {0.0f, 0.0f, 0.0f};
+            if (need_uv) seq_reject<3>(rng, uv3);
+            if (hitp) {
+                const f3 ruv = need_uv ? unit_vector(mk(uv3[0], uv3[1], uv3[2])) : mk(0, 0, 0);
+                f3 att;
+                if (scatter_finish<FEAT>(L, rin, hp, ruv, rng, thr, acc, att, sc) && depth > 1) {
+                    thr = thr * att;
+                    push = true;
+                }
+            }
+        }
+        if (depth && !push) W.ls[pid] = make_float4(acc.x, acc.y, acc.z, 0);
         const uint32_t out = wf_push(W, it, push);
         if (push) {
             wf_store_ray(O, out, sc, depth - 1);
@@ -582,6 +605,8 @@ __device__ __forceinline__ void wf_tail_body(const rtw_launch& L, const rtw_wf& 
             if (exhausted) break;
             continue;
         }
+        bool done = true, hitp = false, need_uv = false;
+        HitPrep hp;
         if (active) {  // one more iteration of rayColor
             cnt.rays++;
             cnt.tail_rays++;
@@ -592,9 +617,15 @@ __device__ __forceinline__ void wf_tail_body(const rtw_launch& L, const rtw_wf& 
             else
                 hit = nodes ? traverse<FEAT, false>(nodes, L, r, t, cnt, rng.s)  // the LDS stage
                             : wf_traverse_global<FEAT>(L, r, t, cnt, rng.s);
-            bool done = true;
             if (hit < 0) {
                 acc = acc + thr * background(L, r);
+            } else if constexpr ((FEAT & ~RTW_F_CHECKER) == 0) {
+                // untextured static sphere scenes: the fused step's split form (hit record, one
+                // randomUnitVector rejection loop for the wave, then the material; C2 tail -10 %,
+                // C4 -5 %; the textured C5 tail +5 %: nested form there)
+                hp = hit_prep<FEAT>(L.nodes, L, r, hit, t);
+                hitp = true;
+                need_uv = needs_unit_vector<FEAT>(hp.m.kind);
             } else {
                 f3 att;
                 Ray sc;
@@ -605,10 +636,25 @@ __device__ __forceinline__ void wf_tail_body(const rtw_launch& L, const rtw_wf& 
                     done = false;
                 }
             }
-            if (done) {
-                W.ls[pid] = make_float4(acc.x, acc.y, acc.z, 0);
-                active = false;
+        }
+        if constexpr ((FEAT & ~RTW_F_CHECKER) == 0) {
+            float uv3[3] = {0.0f, 0.0f, 0.0f};
+            if (need_uv) seq_reject<3>(rng, uv3);
+            if (hitp) {
+                const f3 ruv = need_uv ? unit_vector(mk(uv3[0], uv3[1], uv3[2])) : mk(0, 0, 0);
+                f3 att;
+                Ray sc;
+                if (scatter_finish<FEAT>(L, r, hp, ruv, rng, thr, acc, att, sc) && depth > 1) {
+                    thr = thr * att;
+                    r = sc;
+                    depth--;
+                    done = false;
+                }
             }
+        }
+        if (active && done) {
+            W.ls[pid] = make_float4(acc.x, acc.y, acc.z, 0);
+            active = false;
         }
     }
     flush_counters(L, cnt, 0);
@@ -616,6 +662,12 @@ __device__ __forceinline__ void wf_tail_body(const rtw_launch& L, const rtw_wf& 
 
 template <uint32_t FEAT>
 __global__ __launch_bounds__(256) void wf_tail(rtw_launch L, rtw_wf W, uint32_t it) {
+    wf_tail_body<FEAT, false>(L, W, it, nullptr);
+}
+// untextured static sphere scenes: capped at 96 VGPRs for 5 waves/SIMD (no spills there; the
+// split shading form took it to 98 = 4 waves: C4 tail +3 %); other scene classes would spill
+template <uint32_t FEAT>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void wf_tail_w5(rtw_launch L, rtw_wf W, uint32_t it) {
     wf_tail_body<FEAT, false>(L, W, it, nullptr);
 }
 
@@ -940,6 +992,18 @@ uint32_t wf_grid_cached(K kernel, int n_cu, size_t lds, uint32_t (&c)[2]) {
     return c[0];
 }
 
+// the global tail launch of either form
+template <uint32_t FEAT>
+void wf_launch_tail(const rtw_launch& L, const rtw_wf& W, hipStream_t st, int n_cu, size_t lds, uint32_t (&cache)[2],
+                    uint32_t it) {
+    if constexpr ((FEAT & ~RTW_F_CHECKER) == 0)
+        hipLaunchKernelGGL(wf_tail_w5<FEAT>, dim3(wf_grid_cached(wf_tail_w5<FEAT>, n_cu, lds, cache)), dim3(256), lds, st,
+                           L, W, it);
+    else
+        hipLaunchKernelGGL(wf_tail<FEAT>, dim3(wf_grid_cached(wf_tail<FEAT>, n_cu, lds, cache)), dim3(256), lds, st, L,
+                           W, it);
+}
+
 // dynamic LDS of the kernels that walk through L1/L2: the two-wide walk's per-lane stacks
 template <uint32_t FEAT>
 size_t wf_w2_lds(const rtw_launch& L) {
@@ -1058,9 +1122,7 @@ void wf_run_fused(const rtw_launch& L, const rtw_wf& W, hipStream_t st, int n_cu
             hipLaunchKernelGGL(wf_tail_lds<FEAT>, dim3(tl[0]), dim3(256), tdyn, st, L, W, iters);
             done = true;
         }
-        if (!done)
-            hipLaunchKernelGGL(wf_tail<FEAT>, dim3(wf_grid_cached(wf_tail<FEAT>, n_cu, gdyn, wtail)), dim3(256), gdyn, st,
-                               L, W, iters);
+        if (!done) wf_launch_tail<FEAT>(L, W, st, n_cu, gdyn, wtail, iters);
         RTW_TIME_END(T)
     }
     RTW_TIME_BEGIN(T, RTW_K_REDUCE)
@@ -1147,8 +1209,7 @@ void wf_run(const rtw_launch& L, const rtw_wf& W, hipStream_t st, int n_cu, rtw_
             }
             hipLaunchKernelGGL(wf_tail_lds<FEAT>, dim3(tl[0]), dim3(256), tdyn, st, L, W, iters);
         } else {
-            hipLaunchKernelGGL(wf_tail<FEAT>, dim3(wf_grid_cached(wf_tail<FEAT>, n_cu, w2l, wtail)), dim3(256), w2l, st, L,
-                               W, iters);
+            wf_launch_tail<FEAT>(L, W, st, n_cu, w2l, wtail, iters);
         }
         RTW_TIME_END(T)
     }
