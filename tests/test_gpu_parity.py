@@ -344,13 +344,15 @@ def test_compact_nodes_are_exact(rtw, n, seed):
     arr = rtw.flatten(rtw.worlds.stress_world(n, seed), bvh_mode=rtw._abi.RTW_BVH_SAH)
     cam = rtw.book1_camera(image_width=480, aspect_ratio=16 / 9, spp=4).init()
     outs = []
-    for tu in ({"compact_nodes": 0}, {"compact_nodes": 1, "wide_walk": 0}, {"compact_nodes": 1, "wide_walk": 1}):
+    for tu in ({"compact_nodes": 0, "tile_lists": 0}, {"compact_nodes": 1, "wide_walk": 0},
+               {"compact_nodes": 1, "wide_walk": 1}):
         w = rtw.World(arr, tuning=tu)
         outs.append(render_rows(rtw, w, cam, 0, cam.derived.image_height, 0, 4, 6))
         w.close()
     assert np.isfinite(outs[1]).all()
     assert np.array_equal(outs[0], outs[1])
     assert np.array_equal(outs[0], outs[2])  # the two-wide stack walk (rtw_wide2_nodes): same hits
+    # (the defaults also give camera rays the frustum-walked tile lists of large trees: same hits)
 
 
 @pytest.mark.parametrize("scene", ["book1", "stress"])

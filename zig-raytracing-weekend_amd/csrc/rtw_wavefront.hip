@@ -283,65 +283,122 @@ __device__ __forceinline__ int wf_traverse_global(const rtw_launch& L, const Ray
 // the tile's rectangle scaled by t plus a disk of radius |1 - t| * r_disk.  A ray
 // passes within rho of C only if that cross-section comes within rho * sec(phi) of
 // C (phi: the largest angle of a ray to f); a hit has depth >= z - rho, i.e.
-// t >= (z - rho) / h.  Spheres reaching the camera plane (z <= rho) are always kept.
-__global__ __launch_bounds__(64) void wf_tile_lists(rtw_launch L, rtw_wf W) {
-    __shared__ float s_t[RTW_TL_MAX];
-    __shared__ uint32_t s_id[RTW_TL_MAX];
-    const uint32_t tile = blockIdx.x, lane = threadIdx.x;
+// t >= (z - rho) / h.  Spheres wholly behind the camera plane (z < -rho) are never kept (a ray's
+// depth is t * h > 0); those straddling it are kept when near the axis (tile_reach).
+// The tile's ray set (see above): pixel rectangle at depth h in the (uh, vh) frame around the
+// camera centre, defocus radius rd, sec of the widest ray angle
+struct TileFrustum {
+    f3 ctr, fz, uh, vh;
+    float h, ru0, ru1, rv0, rv1, rd, sec;
+    bool ok;  // false: no usable frame (the tile walks the tree)
+};
+
+__device__ __forceinline__ TileFrustum tile_frustum(const rtw_launch& L, float x0, float x1, float y0, float y1) {
+    TileFrustum F;
+    const f3 du = ld3(L.du), dv = ld3(L.dv);
+    F.ctr = ld3(L.center);
+    const f3 fw = cross(du, dv);
+    const float fl = __builtin_sqrtf(length_squared(fw)), ul = __builtin_sqrtf(length_squared(du)),
+                vl = __builtin_sqrtf(length_squared(dv));
+    F.fz = divs(fw, fl);
+    F.uh = divs(du, ul);
+    F.vh = divs(dv, vl);
+    const f3 p0 = ld3(L.pixel00) - F.ctr;
+    F.h = dot(p0, F.fz);
+    const float pu = dot(p0, F.uh), pv = dot(p0, F.vh);
+    // the pixel plane must face the rays and du, dv be orthogonal (Camera.init)
+    F.ok = F.h > 0.0f && fl > 0.0f && __builtin_fabsf(dot(du, dv)) <= 1e-4f * ul * vl;
+    const float off = (float)L.pixel_offset;
+    F.ru0 = pu + (x0 + off - 0.5f) * ul;
+    F.ru1 = pu + (x1 + off + 0.5f) * ul;
+    F.rv0 = pv + (y0 + off - 0.5f) * vl;
+    F.rv1 = pv + (y1 + off + 0.5f) * vl;
+    F.rd = L.defocus_angle > 0 ? fmaxf(__builtin_sqrtf(length_squared(ld3(L.disk_u))),
+                                       __builtin_sqrtf(length_squared(ld3(L.disk_v)))) : 0.0f;
+    const float mu = fmaxf(__builtin_fabsf(F.ru0), __builtin_fabsf(F.ru1)),
+                mv = fmaxf(__builtin_fabsf(F.rv0), __builtin_fabsf(F.rv1));
+    const float tphi = (__builtin_sqrtf(mu * mu + mv * mv) + F.rd) / F.h;
+    F.sec = __builtin_sqrtf(1.0f + tphi * tphi) * 1.001f;
+    return F;
+}
+
+// Can a ray of the tile pass within rho of c?  (conservative; tlow: a lower bound of the ray
+// parameter of any such hit, 0 when the sphere reaches the camera plane)
+__device__ __forceinline__ bool tile_reach(const TileFrustum& F, f3 c, float rho, float& tlow) {
+    const f3 cc = c - F.ctr;
+    const float z = dot(cc, F.fz), cu = dot(cc, F.uh), cv = dot(cc, F.vh);
+    const float slack = 1e-3f * (__builtin_fabsf(z) + __builtin_fabsf(cu) + __builtin_fabsf(cv) + rho) + 1e-5f;
+    tlow = 0.0f;
+    if (z < -(rho + slack)) return false;  // wholly behind the camera plane: rays only go forward (t > 0)
+    if (!(z > rho + slack)) {
+        // straddles the camera plane: a hit has depth in (0, z + rho], so t <= t1 and the hit point is
+        // within |1 - t| rd + t |T| <= max(1, t1) rd + t1 |T|max of the axis (T: the pixel-plane target)
+        const float t1 = fmaxf(0.0f, (z + rho + slack) / F.h);
+        const float tmax = __builtin_sqrtf(fmaxf(F.ru0 * F.ru0, F.ru1 * F.ru1) + fmaxf(F.rv0 * F.rv0, F.rv1 * F.rv1));
+        const float lat = __builtin_sqrtf(cu * cu + cv * cv);
+        return !(lat > rho + fmaxf(1.0f, t1) * F.rd + t1 * tmax + slack);  // NaN: tested
+    }
+    const float t = z / F.h;
+    const float dx = fmaxf(0.0f, fmaxf(t * F.ru0 - cu, cu - t * F.ru1));
+    const float dy = fmaxf(0.0f, fmaxf(t * F.rv0 - cv, cv - t * F.rv1));
+    const float gap = __builtin_sqrtf(dx * dx + dy * dy) - __builtin_fabsf(1.0f - t) * F.rd;
+    tlow = fmaxf(0.0f, (z - rho - slack) / F.h * 0.9999f);
+    return !(gap > rho * F.sec + slack);
+}
+
+// the tile's pixel bounds over its lanes' pixels (wave-wide min / max); false: no pixel rendered
+__device__ __forceinline__ bool tile_bounds(const rtw_launch& L, const rtw_wf& W, uint32_t q, float& x0, float& x1,
+                                            float& y0, float& y1) {
     uint32_t pixel, out_idx, x = 0, y = 0;
-    const bool ok = wf_pixel(L, W, tile * 64u + lane, pixel, out_idx, x, y);
-    float x0 = ok ? (float)x : 1e30f, x1 = ok ? (float)x : -1e30f, y0 = ok ? (float)y : 1e30f, y1 = ok ? (float)y : -1e30f;
+    const bool ok = wf_pixel(L, W, q, pixel, out_idx, x, y);
+    x0 = ok ? (float)x : 1e30f; x1 = ok ? (float)x : -1e30f;
+    y0 = ok ? (float)y : 1e30f; y1 = ok ? (float)y : -1e30f;
     for (int o = 32; o > 0; o >>= 1) {
         x0 = fminf(x0, __shfl_xor(x0, o));
         x1 = fmaxf(x1, __shfl_xor(x1, o));
         y0 = fminf(y0, __shfl_xor(y0, o));
         y1 = fmaxf(y1, __shfl_xor(y1, o));
     }
-    if (!(x0 <= x1)) {  // no pixel of the tile is rendered
+    return x0 <= x1;
+}
+
+// write tile's list from (tlow, ordering-0 leaf index) pairs in LDS, ranked by (tlow, index)
+__device__ __forceinline__ void tile_emit(const rtw_launch& L, const rtw_wf& W, uint32_t tile, const float* s_t,
+                                          const uint32_t* s_id, uint32_t count, uint32_t k) {
+    if (k >= count) return;
+    const float me = s_t[k];
+    uint32_t rank = 0;
+    for (uint32_t j = 0; j < count; j++) rank += (s_t[j] < me || (s_t[j] == me && j < k)) ? 1u : 0u;
+    const uint32_t id = s_id[k];
+    const float4 A = L.nodes[2u * id], B = L.nodes[2u * id + 1u];  // ordering 0 leaf: center, radius
+    const float rr = B.x * B.x;  // objects.zig:126, as the compact nodes
+    uint4* e = W.tl + 2u * ((size_t)tile * RTW_TL_MAX + rank);
+    e[0] = make_uint4(fbits(A.x), fbits(A.y), fbits(A.z), fbits(rr));
+    e[1] = make_uint4(id, fbits(me), 0u, 0u);
+}
+
+// small trees: one 64-lane block per tile scans every leaf of ordering 0
+__global__ __launch_bounds__(64) void wf_tile_lists(rtw_launch L, rtw_wf W) {
+    __shared__ float s_t[RTW_TL_MAX];
+    __shared__ uint32_t s_id[RTW_TL_MAX];
+    const uint32_t tile = blockIdx.x, lane = threadIdx.x;
+    float x0, x1, y0, y1;
+    if (!tile_bounds(L, W, tile * 64u + lane, x0, x1, y0, y1)) {  // no pixel of the tile is rendered
         if (lane == 0) W.tl_count[tile] = 0;
         return;
     }
-    const f3 du = ld3(L.du), dv = ld3(L.dv), ctr = ld3(L.center);
-    const f3 fw = cross(du, dv);
-    const float fl = __builtin_sqrtf(length_squared(fw)), ul = __builtin_sqrtf(length_squared(du)),
-                vl = __builtin_sqrtf(length_squared(dv));
-    const f3 fz = divs(fw, fl), uh = divs(du, ul), vh = divs(dv, vl);
-    const f3 p0 = ld3(L.pixel00) - ctr;
-    const float h = dot(p0, fz), pu = dot(p0, uh), pv = dot(p0, vh);
-    // the pixel plane must face the rays and du, dv be orthogonal (Camera.init); else walk
-    const bool frame = h > 0.0f && fl > 0.0f && __builtin_fabsf(dot(du, dv)) <= 1e-4f * ul * vl;
-    const float off = (float)L.pixel_offset;
-    const float ru0 = pu + (x0 + off - 0.5f) * ul, ru1 = pu + (x1 + off + 0.5f) * ul;
-    const float rv0 = pv + (y0 + off - 0.5f) * vl, rv1 = pv + (y1 + off + 0.5f) * vl;
-    const float rd = L.defocus_angle > 0 ? fmaxf(__builtin_sqrtf(length_squared(ld3(L.disk_u))),
-                                                 __builtin_sqrtf(length_squared(ld3(L.disk_v)))) : 0.0f;
-    const float mu = fmaxf(__builtin_fabsf(ru0), __builtin_fabsf(ru1)), mv = fmaxf(__builtin_fabsf(rv0), __builtin_fabsf(rv1));
-    const float tphi = (__builtin_sqrtf(mu * mu + mv * mv) + rd) / h;
-    const float sec = __builtin_sqrtf(1.0f + tphi * tphi) * 1.001f;
+    const TileFrustum F = tile_frustum(L, x0, x1, y0, y1);
     uint32_t count = 0;
-    bool over = !frame;
+    bool over = !F.ok;
     for (uint32_t base = 0; base < L.n_nodes && !over; base += 64u) {
         const uint32_t k = base + lane;
         bool cand = false;
         float tlow = 0.0f;
         if (k < L.n_nodes) {
             const uint4 c = L.cnodes[k];  // ordering 0
-            if (c.w & RTW_LEAF_BIT) {
-                const f3 cc = mk(ubits(c.x), ubits(c.y), ubits(c.z)) - ctr;
-                const float rho = __builtin_sqrtf(ubits(c.w & ~RTW_LEAF_BIT));
-                const float z = dot(cc, fz), cu = dot(cc, uh), cv = dot(cc, vh);
-                const float slack = 1e-3f * (__builtin_fabsf(z) + __builtin_fabsf(cu) + __builtin_fabsf(cv) + rho) + 1e-5f;
-                if (!(z > rho + slack)) {
-                    cand = true;  // reaches the camera plane (or NaN): always tested
-                } else {
-                    const float t = z / h;
-                    const float dx = fmaxf(0.0f, fmaxf(t * ru0 - cu, cu - t * ru1));
-                    const float dy = fmaxf(0.0f, fmaxf(t * rv0 - cv, cv - t * rv1));
-                    const float gap = __builtin_sqrtf(dx * dx + dy * dy) - __builtin_fabsf(1.0f - t) * rd;
-                    cand = !(gap > rho * sec + slack);
-                    tlow = fmaxf(0.0f, (z - rho - slack) / h * 0.9999f);
-                }
-            }
+            if (c.w & RTW_LEAF_BIT)
+                cand = tile_reach(F, mk(ubits(c.x), ubits(c.y), ubits(c.z)), __builtin_sqrtf(ubits(c.w & ~RTW_LEAF_BIT)),
+                                  tlow);
         }
         const uint64_t m = __ballot(cand);
         const uint32_t n = (uint32_t)__popcll(m);
@@ -361,17 +418,66 @@ __global__ __launch_bounds__(64) void wf_tile_lists(rtw_launch L, rtw_wf W) {
         return;
     }
     __syncthreads();
-    if (lane < count) {  // rank by (bound, index): sorted front to back
-        const float me = s_t[lane];
-        uint32_t rank = 0;
-        for (uint32_t j = 0; j < count; j++) rank += (s_t[j] < me || (s_t[j] == me && j < lane)) ? 1u : 0u;
-        const uint32_t id = s_id[lane];
-        const uint4 c = L.cnodes[id];
-        uint4* e = W.tl + 2u * ((size_t)tile * RTW_TL_MAX + rank);
-        e[0] = make_uint4(c.x, c.y, c.z, c.w & ~RTW_LEAF_BIT);
-        e[1] = make_uint4(id, fbits(me), 0u, 0u);
-    }
+    tile_emit(L, W, tile, s_t, s_id, count, lane);
     if (lane == 0) W.tl_count[tile] = count;
+}
+
+// large trees: a 64-lane block builds 64 tiles' lists, lane j walking tile j's frustum down the
+// ordering-0 tree (32-B nodes; an inner box is kept when its bounding sphere is reachable)
+__global__ __launch_bounds__(64) void wf_tile_lists_walk(rtw_launch L, rtw_wf W) {
+    __shared__ float s_t[64][RTW_TL_MAX + 1];
+    __shared__ uint32_t s_id[64][RTW_TL_MAX + 1];
+    const uint32_t lane = threadIdx.x, t0 = blockIdx.x * 64u, n_tiles = W.n_pix >> 6;
+    uint32_t count = 0;
+    bool over = false, empty = false;
+    TileFrustum F;
+    for (uint32_t j = 0; j < 64; j++) {  // the bounds of tile t0 + j, wave-wide; lane j keeps them
+        float x0 = 0, x1 = 0, y0 = 0, y1 = 0;
+        bool any = false;
+        if (t0 + j < n_tiles) any = tile_bounds(L, W, (t0 + j) * 64u + lane, x0, x1, y0, y1);
+        if (lane == j) {
+            empty = !any;
+            F = tile_frustum(L, x0, x1, y0, y1);
+        }
+    }
+    const uint32_t tile = t0 + lane;
+    if (tile < n_tiles && !empty) {
+        over = !F.ok;
+        uint32_t i = 0;
+        while (i < L.n_nodes && !over) {
+            const float4 A = L.nodes[2u * i], B = L.nodes[2u * i + 1u];
+            const uint32_t w = fbits(A.w);
+            float tlow;
+            if (w & RTW_LEAF_BIT) {
+                if (tile_reach(F, mk(A.x, A.y, A.z), __builtin_fabsf(B.x), tlow)) {
+                    if (count == L.tile_lists) over = true;
+                    else {
+                        s_t[lane][count] = tlow;
+                        s_id[lane][count] = i;
+                        count++;
+                    }
+                }
+                i = w & RTW_SKIP_MASK;
+            } else {
+                const f3 lo = mk(A.x, A.y, A.z), hi = mk(B.x, B.y, B.z);
+                const f3 m = (lo + hi) * splat(0.5f);
+                const float rad = __builtin_sqrtf(length_squared(hi - lo)) * 0.5001f + 1e-5f;
+                i = tile_reach(F, m, rad, tlow) ? i + 1u : (w & RTW_SKIP_MASK);
+            }
+        }
+    }
+    __syncthreads();
+    if (tile >= n_tiles) return;
+    if (empty) {
+        W.tl_count[tile] = 0;
+        return;
+    }
+    if (over) {
+        W.tl_count[tile] = RTW_TL_WALK;
+        return;
+    }
+    for (uint32_t k = 0; k < count; k++) tile_emit(L, W, tile, s_t[lane], s_id[lane], count, k);
+    W.tl_count[tile] = count;
 }
 
 // The closest hit of a camera ray from its tile's list (wave-uniform: every lane of
@@ -444,8 +550,17 @@ __global__ __launch_bounds__(256) void wf_trace(rtw_launch L, rtw_wf W, uint32_t
             uint32_t depth;
             const Ray r = wf_load_ray(S, slot, depth);
             if (depth) {
-                float t;
-                const int h = wf_traverse_global<FEAT>(L, r, t, cnt, wf_mkey<FEAT>(S, slot));
+                float t = kInf;
+                int h = -1;
+                bool listed = false;
+                if constexpr ((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING)) == 0) {
+                    if (it == 0 && W.tl_count) {  // camera rays (slot = path id): the tile's candidate list
+                        const uint32_t tile = (slot - (slot / W.n_pix) * W.n_pix) >> 6;
+                        listed = L.counters ? wf_tile_hit<true>(L, W, tile, r, h, t, cnt)
+                                            : wf_tile_hit<false>(L, W, tile, r, h, t, cnt);
+                    }
+                }
+                if (!listed) h = wf_traverse_global<FEAT>(L, r, t, cnt, wf_mkey<FEAT>(S, slot));
                 W.hit[slot] = make_float2(t, __int_as_float(h));
                 cnt.rays++;
             }
@@ -1013,6 +1128,23 @@ size_t wf_w2_lds(const rtw_launch& L) {
     return 0;
 }
 
+// The camera-ray candidate lists of a batch (static sphere scenes with the compact nodes): the
+// flat scan for small trees, the frustum walk for large ones.  Returns W with tl_count null when off.
+template <uint32_t FEAT>
+rtw_wf wf_lists(const rtw_launch& L, const rtw_wf& W, hipStream_t st) {
+    rtw_wf Wt = W;
+    if (!W.tl_count || !L.cnodes || (FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING)) || L.max_depth == 0) {
+        Wt.tl_count = nullptr;
+        return Wt;
+    }
+    const uint32_t tiles = W.n_pix / 64u;
+    if (L.n_nodes <= 4096u)
+        hipLaunchKernelGGL(wf_tile_lists, dim3(tiles), dim3(64), 0, st, L, Wt);
+    else
+        hipLaunchKernelGGL(wf_tile_lists_walk, dim3((tiles + 63u) / 64u), dim3(64), 0, st, L, Wt);
+    return Wt;
+}
+
 template <uint32_t FEAT>
 struct WfGrids {
     uint32_t trace, shade, tail;
@@ -1081,9 +1213,8 @@ void wf_run_fused(const rtw_launch& L, const rtw_wf& W, hipStream_t st, int n_cu
     (void)hipMemsetAsync(W.len[1], 0, RTW_WF_STRIPES * RTW_WF_LEN_STRIDE * 4, st);
     const uint32_t iters = L.max_depth < W.iters ? L.max_depth : W.iters;
     rtw_wf Wt = W;  // the camera-ray lists serve the LDS-staged steps of static sphere scenes
-    if ((!clds && !lds) || !W.tl_count || iters == 0 || (FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING)))
-        Wt.tl_count = nullptr;
-    if (Wt.tl_count) hipLaunchKernelGGL(wf_tile_lists, dim3(W.n_pix / 64u), dim3(64), 0, st, L, Wt);
+    if ((clds || lds) && iters) Wt = wf_lists<FEAT>(L, W, st);
+    else Wt.tl_count = nullptr;
     // rayColor(depth <= 0) = 0 (camera.zig:183-185): no iteration writes W.ls, which holds the
     // previous render's radiance, so the reduce must add zeros
     if (iters == 0) (void)hipMemsetAsync(W.ls, 0, (size_t)W.n_paths * sizeof(float4), st);
@@ -1155,6 +1286,7 @@ void wf_run(const rtw_launch& L, const rtw_wf& W, hipStream_t st, int n_cu, rtw_
     hipLaunchKernelGGL(wf_gen<FEAT>, dim3((W.n_paths + 255u) / 256u), dim3(256), 0, st, L, W);
     RTW_TIME_END(T)
     const uint32_t iters = L.max_depth < W.iters ? L.max_depth : W.iters;
+    const rtw_wf Wt = iters ? wf_lists<FEAT>(L, W, st) : W;  // camera rays: iteration 0 of wf_trace (L1/L2)
     const size_t w2l = wf_w2_lds<FEAT>(L);  // the two-wide walk's stacks (trace / tail through L1/L2)
     thread_local uint32_t wtrace[2] = {0, 0}, wtail[2] = {0, 0};
     const size_t lds_need = (size_t)L.n_nodes * L.n_orders * 32u;
@@ -1190,7 +1322,7 @@ void wf_run(const rtw_launch& L, const rtw_wf& W, hipStream_t st, int n_cu, rtw_
             hipLaunchKernelGGL((wf_trace<FEAT, true>), dim3(lds_grid), dim3(256), tlds, st, L, W, it);
         else
             hipLaunchKernelGGL((wf_trace<FEAT, false>), dim3(wf_grid_cached(wf_trace<FEAT, false>, n_cu, w2l, wtrace)),
-                               dim3(256), w2l, st, L, W, it);
+                               dim3(256), w2l, st, L, it == 0 ? Wt : W, it);
         RTW_TIME_END(T)
     shade_step:
         RTW_TIME_BEGIN(T, RTW_K_SHADE)
