@@ -2,7 +2,7 @@
 set -u
 mkdir -p gpurun_out/ab
 for rep in 1 2; do
-for lib in default build/rtw_ilp.so; do
+for lib in ${LIBS:-default build/rtw_ilp.so}; do
   for c in c2 c4 cornell; do
     if [ $lib = default ]; then L=""; else L=$lib; fi
     RTW_LIB=$L timeout -k 10 240 python bench.py --config $c --no-cpu-baseline --steps 3 > gpurun_out/ab/${c}_$(basename $lib)_$rep.json 2>/dev/null || exit $?
