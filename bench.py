@@ -40,7 +40,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--single-process", action="store_true",
                     help="drive the N GPUs from this one process through the C ABI (rtw_multi: shard renders + one "
-                         "grouped RCCL send/recv); the default without torchrun when --gpus > 1")
+                         "grouped RCCL send/recv); without it, --gpus N > 1 needs torchrun (one process per GPU)")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="c2",
@@ -63,9 +63,12 @@ def main():
     world_size = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    single = args.single_process or (world_size == 1 and args.gpus > 1)
+    single = args.single_process
     if world_size > 1 and (single or world_size != args.gpus):
         raise SystemExit("torchrun: --gpus must equal the number of ranks and excludes --single-process")
+    if world_size == 1 and args.gpus > 1 and not single:
+        raise SystemExit("--gpus N > 1: launch one process per GPU with torchrun (the driver's scaling run), or "
+                         "pass --single-process for the one-process rtw_multi path")
     n_shards = args.gpus if single else world_size
     torch.cuda.set_device(local_rank)
     distributed = world_size > 1
@@ -84,6 +87,14 @@ def main():
     # single-process multi-GPU: one context per device + the RCCL communicators of rtw_multi
     worlds = [world] + [pkg.World(arr, device=k, tuning=tun) for k in range(1, n_shards)] if single else [world]
     multi = pkg.distributed.MultiDeviceRender(worlds, ROWS_PER_BLOCK) if single else None
+    # the exchange's participants as the collective layer reports them: rtw_multi's RCCL communicator
+    # (ncclCommCount), or torch.distributed's process group (backend "nccl" = RCCL on ROCm)
+    if single:
+        rccl = {"mode": "rtw_multi", "rccl_ranks": multi.info()[1], "backend": "rccl (ncclCommInitAll)"}
+    elif distributed:
+        rccl = {"mode": "torchrun", "rccl_ranks": dist.get_world_size(), "backend": str(dist.get_backend())}
+    else:
+        rccl = {"mode": "single_gpu", "rccl_ranks": None, "backend": None}
     build_s = time.time() - t0
     # the reference topology (bvh.zig) defines the algorithmic bytes
     world_ref = pkg.World(pkg.flatten(objs, bvh_mode=pkg._abi.RTW_BVH_REFERENCE), device=local_rank)
@@ -204,7 +215,7 @@ def main():
     # the launch time is this run's HIP events.  HBM traffic (PMC) and the SURVEY §8d algorithmic
     # bytes are reported beside it; the latter is a diagnostic, not a fraction of any peak.
     dom_kind = {"trace": "wf_step" if fused else "wf_trace", "tail": "wf_tail", "mega": "render_"}.get(dom, dom)
-    valu, valu_src = pmc_valu(args, dom_kind)
+    valu, valu_src = pmc_valu(args, dom_kind, single)
     lane_ops = valu.get("lane_ops") if valu else None
     achieved_valu = lane_ops / dom_launch_s / 1e12 if (lane_ops and dom_launch_s > 0) else None
     issue = (valu["active_inst_valu"] * 4 / (N_SIMD * dom_launch_s * CLOCK_HZ)) if (valu and dom_launch_s > 0) else None
@@ -273,7 +284,9 @@ def main():
                        "bvh_depth": stats["depth"], "parallelism": f"row-interleaved tiles x{n_shards}"
                        + (" + RCCL gather" if distributed else "")
                        + (" (one process, rtw_multi: grouped RCCL send/recv)" if single else ""),
-                       "rows_per_block": ROWS_PER_BLOCK},
+                       "rows_per_block": ROWS_PER_BLOCK, "exchange": rccl,
+                       "timed_scope": "device API (rtw_render_rows_device / rtw_render_multi_device) into an "
+                                      "HBM-resident float4 accumulator; no host copy inside the timed region"},
             "roofline": roofline,
             "cpu_baseline": cpu,
             "nan_samples": nan_count,
@@ -290,7 +303,7 @@ def pmc_traffic(args, kernel_prefix):
     (tools/pmc_traffic.sh -> profiles/pmc_traffic_<config>_<bvh>.json; FETCH_SIZE x2 + WRITE_SIZE,
     MI355X_MICROARCH.md § HBM).  PMC counters cannot be read inside the timed run."""
     f = os.path.join(REPO, "profiles", f"pmc_traffic_{args.config}_{args.bvh}.json")
-    if args.spp or not os.path.exists(f):
+    if args.spp or args.tuning or os.environ.get("RTW_LIB") or not os.path.exists(f):
         return None, None
     data = json.load(open(f))
     for name, e in data.items():
@@ -299,11 +312,13 @@ def pmc_traffic(args, kernel_prefix):
     return None, None
 
 
-def pmc_valu(args, kind):
+def pmc_valu(args, kind, single=False):
     """VALU counters per launch of the dominant kernel kind from the committed SQ pass
-    (tools/pmc_valu.sh -> profiles/pmc_valu_<config>_<bvh>.json).  Returns (entry, path)."""
+    (tools/pmc_valu.sh -> profiles/pmc_valu_<config>_<bvh>.json).  Returns (entry, path).
+    The pass was taken with the product defaults on one device: an A/B build (--tuning, RTW_LIB) or the
+    single-process multi path runs other kernels, so no roofline is derived from it there."""
     f = os.path.join(REPO, "profiles", f"pmc_valu_{args.config}_{args.bvh}.json")
-    if args.spp or not os.path.exists(f):
+    if args.spp or args.tuning or single or os.environ.get("RTW_LIB") or not os.path.exists(f):
         return None, None
     for name, e in json.load(open(f)).items():
         if name.startswith(kind) and e.get("lane_ops"):

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define RTW_ABI_VERSION 4
+#define RTW_ABI_VERSION 5
 
 enum rtw_status {
     RTW_OK = 0,
@@ -248,6 +248,15 @@ typedef struct rtw_render_opts {
     uint32_t flags;            /* RTW_RENDER_* */
     uint64_t* counters;        /* optional device-side stats out (RTW_STAT_COUNT u64) or NULL */
     rtw_kernel_timing* timing; /* optional host out: per-kernel device time (the call then synchronises) */
+    /* ABI 5: stop and progress, polled before every spp batch and after each one (a call given any of
+     * them synchronises after every batch).  Samples of the batches that finished stay in the buffer
+     * and its .w is the last finished batch's end (camera.zig:56), so a stopped render can resume. */
+    const volatile uint8_t* running; /* RenderThread.running (src/main.zig:50, a Zig `bool`; stop() clears
+                                        it, main.zig:58-60; Camera.render polls it, camera.zig:107):
+                                        0 = stop, non-zero = go on; NULL = not polled */
+    const volatile int32_t* cancel;  /* non-zero = stop (rtw_render's flag); NULL = not polled */
+    rtw_progress_fn progress;        /* samples finished so far in this call; non-zero return = stop */
+    void* user;                      /* passed to progress */
 } rtw_render_opts;
 
 enum { RTW_RENDER_NO_SYNC = 1u };  /* rtw_render_device: do not synchronise the stream */
@@ -334,6 +343,11 @@ void rtw_scene_destroy(rtw_ctx* ctx);
 int rtw_render(rtw_ctx* ctx, const rtw_camera* cam, uint32_t pix_begin, uint32_t pix_end,
                uint32_t spp_begin, uint32_t spp_end, uint64_t seed, float* accum,
                const volatile int32_t* cancel, rtw_progress_fn progress, void* user);
+/* ABI 5: the same with rtw_render_opts (spp_batch and the stop/progress fields; flags, counters and
+ * timing must be 0/NULL).  A host context polls running/cancel per pixel as well (camera.zig:107).
+ * A stopped call returns RTW_E_CANCELLED with the finished batches in accum. */
+int rtw_render_ex(rtw_ctx* ctx, const rtw_camera* cam, uint32_t pix_begin, uint32_t pix_end,
+                  uint32_t spp_begin, uint32_t spp_end, uint64_t seed, float* accum, const rtw_render_opts* opts);
 
 /* Same, on a DEVICE buffer float4[W*H] already resident on ctx's device, on
  * `stream` (a hipStream_t, or NULL for the ctx's own stream).  With
@@ -348,6 +362,11 @@ int rtw_render_device(rtw_ctx* ctx, const rtw_camera* cam, uint32_t pix_begin, u
 int rtw_render_rows_device(rtw_ctx* ctx, const rtw_camera* cam, uint32_t rows_per_block, uint32_t n_shards,
                            uint32_t shard, uint32_t spp_begin, uint32_t spp_end, uint64_t seed,
                            float* d_tile, void* stream, const rtw_render_opts* opts);
+/* ABI 5: the same shard into a caller-owned HOST tile float4[rows_in_shard * W] (blocking), on a GPU
+ * context or a host context (RTW_DEVICE_CPU: the shard rendered on host threads, e.g. one process per
+ * rank without a GPU).  opts as rtw_render_ex (may be NULL). */
+int rtw_render_rows(rtw_ctx* ctx, const rtw_camera* cam, uint32_t rows_per_block, uint32_t n_shards, uint32_t shard,
+                    uint32_t spp_begin, uint32_t spp_end, uint64_t seed, float* tile, const rtw_render_opts* opts);
 uint32_t rtw_shard_rows(uint32_t height, uint32_t rows_per_block, uint32_t n_shards, uint32_t shard);
 /* Image row of row `tile_row` of a shard's compact tile (>= height: padding; 0xFFFFFFFF: bad spec).
  * The same function places rows in the render kernels and the multi-GPU gather. */
@@ -373,15 +392,23 @@ int rtw_multi_create(rtw_ctx* const* ctxs, uint32_t n, rtw_multi** out);
 void rtw_multi_destroy(rtw_multi* m);
 enum { RTW_RENDER_FRESH = 2u };  /* rtw_render_multi_device: start the range from zero, do not read d_accum */
 /* d_accum: float4[W*H] on ctxs[0]'s device; stream: a hipStream_t of that device or NULL.
- * opts: spp_batch and flags (RTW_RENDER_NO_SYNC, RTW_RENDER_FRESH) are honoured; counters
- * and timing must be NULL. */
+ * opts: spp_batch, flags (RTW_RENDER_NO_SYNC, RTW_RENDER_FRESH) and the ABI-5 stop/progress fields
+ * are honoured (every device renders batch b, all of them finish, then progress and the flags are
+ * polled; the tiles meet on device 0 once, after the last finished batch -- also on a stop, which
+ * returns RTW_E_CANCELLED with the frame holding every finished batch); counters and timing must
+ * be NULL. */
 int rtw_render_multi_device(rtw_multi* m, const rtw_camera* cam, uint32_t rows_per_block, uint32_t spp_begin,
                             uint32_t spp_end, uint64_t seed, float* d_accum, void* stream,
                             const rtw_render_opts* opts);
 /* Same on a caller-owned HOST float4[W*H] (ColorAndSamples), blocking; cancel is polled
- * before the render starts. */
+ * between spp batches (rtw_render_multi_ex: the full rtw_render_opts, e.g. the Zig `running` flag
+ * and a progress callback). */
 int rtw_render_multi(rtw_multi* m, const rtw_camera* cam, uint32_t rows_per_block, uint32_t spp_begin,
                      uint32_t spp_end, uint64_t seed, float* accum, const volatile int32_t* cancel);
+int rtw_render_multi_ex(rtw_multi* m, const rtw_camera* cam, uint32_t rows_per_block, uint32_t spp_begin,
+                        uint32_t spp_end, uint64_t seed, float* accum, const rtw_render_opts* opts);
+/* ABI 5: devices of the rtw_multi and ranks of its RCCL communicator (ncclCommCount of device 0's). */
+int rtw_multi_info(rtw_multi* m, uint32_t* n_devices, int* rccl_ranks);
 
 /* SharedStateImageWriter texel update: u8(256*clamp(sqrt(rgb/w),0,0.999)), alpha 255
  * (src/camera.zig:58-65, src/color.zig:43-62). Host, n pixels. */

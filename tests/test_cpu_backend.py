@@ -132,3 +132,53 @@ def test_host_context_cancel_and_refusals(rtw):
     ctxs = (C.c_void_p * 1)(world.handle.value)
     assert L.rtw_multi_create(ctxs, 1, C.byref(h)) == rtw._abi.RTW_E_INVALID
     world.close()
+
+
+def test_host_render_rows_shards_reassemble(rtw):
+    """rtw_render_rows on a host context (ABI 5): every shard of a row-interleaved split, rendered into its
+    own host tile, reassembles to the single-call host render bit for bit (rows past H never written)."""
+    arr = rtw.flatten(rtw.worlds.generate_world(0, "book1"))
+    world = rtw.World(arr, device=CPU)
+    cam = rtw.book1_camera(image_width=72, aspect_ratio=1.5, spp=3).init()
+    W, H = cam.derived.image_width, cam.derived.image_height
+    full = host_render(rtw, arr, cam, 3, 4)
+    for n, rpb in ((3, 8), (2, 5), (4, 1)):
+        image = np.zeros((H, W, 4), np.float32)
+        for k in range(n):
+            rows = rtw.distributed.shard_rows(H, rpb, n, k)
+            tile = np.full((len(rows) * W + W, 4), -7.0, np.float32)   # one guard row past the shard
+            tile[:len(rows) * W] = 0
+            rtw.distributed.render_rows_host(world, cam, rpb, n, k, 0, 3, tile, seed=4)
+            assert (tile[len(rows) * W:] == -7.0).all()
+            image[rows] = tile[:len(rows) * W].reshape(len(rows), W, 4)
+        assert np.array_equal(image.reshape(-1, 4), full), (n, rpb)
+    world.close()
+
+
+def test_host_render_ex_stop_and_progress(rtw):
+    """ABI-5 stop/progress on a host context: a cleared `running` byte (RenderThread.running) stops before
+    anything is rendered; progress after every spp batch, and a stop from it keeps the finished batches
+    (w = their end); resuming the range completes the image bit-identically."""
+    arr = rtw.flatten(rtw.worlds.generate_world(0, "book1"))
+    world = rtw.World(arr, device=CPU)
+    cam = rtw.book1_camera(image_width=48, aspect_ratio=1.5, spp=6).init()
+    L = rtw.lib()
+    buf = np.zeros((cam.size, 4), np.float32)
+    running = C.c_uint8(0)
+    o = rtw._abi.render_opts(running=running)
+    assert L.rtw_render_ex(world.handle, C.byref(cam.derived), 0, cam.size, 0, 6, 2, buf.ctypes.data,
+                           C.byref(o)) == rtw._abi.RTW_E_CANCELLED
+    assert not buf.any()
+    running.value = 1
+    seen = []
+    o = rtw._abi.render_opts(spp_batch=2, running=running,
+                             progress=lambda d, t: seen.append((d, t)) or len(seen) == 1)
+    assert L.rtw_render_ex(world.handle, C.byref(cam.derived), 0, cam.size, 0, 6, 2, buf.ctypes.data,
+                           C.byref(o)) == rtw._abi.RTW_E_CANCELLED
+    assert seen == [(cam.size * 2, cam.size * 6)]
+    assert (buf[:, 3] == 2).all()
+    o = rtw._abi.render_opts(running=running)
+    rtw._abi.check(L.rtw_render_ex(world.handle, C.byref(cam.derived), 0, cam.size, 2, 6, 2, buf.ctypes.data,
+                                   C.byref(o)), "rtw_render_ex")
+    assert np.array_equal(buf, host_render(rtw, arr, cam, 6, 2))
+    world.close()

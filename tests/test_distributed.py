@@ -1,6 +1,9 @@
 """Multi-GPU path on CPU: row sharding covers the image exactly once, and the
-gather + reassembly of bench.py/distributed.py rebuilds the image over a real
-world_size-2 gloo process group (synthetic tiles stand in for the GPU render)."""
+gather + reassembly of bench.py/distributed.py rebuilds the image over real
+world_size-2/3 gloo process groups -- from synthetic (y, x) tiles, and from
+shards each rank RENDERS on a host context (rtw_render_rows, the GPU path's
+per-sample code on host threads), bit-identical to a one-process render."""
+import ctypes as C
 import os
 import socket
 
@@ -105,3 +108,56 @@ def test_gather_reassembles_image_gloo(world_size, H, rpb):
     assert np.array_equal(img[:, :, 0], np.repeat(np.arange(H, dtype=np.float32)[:, None], W, 1))
     assert np.array_equal(img[:, :, 1], np.repeat(np.arange(W, dtype=np.float32)[None, :], H, 0))
     assert (img[:, :, 3] == 7).all()
+
+
+def _render_worker(rank, world_size, port, W, spp, rpb, q):
+    """One rank: its shard of Book-1 rendered on a host context (rtw_render_rows), gathered to rank 0."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world_size)
+    pkg = load_pkg()
+    d = pkg.distributed
+    arr = pkg.flatten(pkg.worlds.generate_world(0, "book1"))
+    world = pkg.World(arr, device=pkg._abi.RTW_DEVICE_CPU, tuning={"cpu_threads": 2})
+    cam = pkg.book1_camera(image_width=W, aspect_ratio=1.5, spp=spp).init()
+    H = cam.derived.image_height
+    cap = d.tile_rows_capacity(H, rpb, world_size)
+    tile = np.zeros((cap * W, 4), np.float32)
+    d.render_rows_host(world, cam, rpb, world_size, rank, 0, spp, tile, seed=13)
+    src, dst = d.reassembly_index(H, rpb, world_size)
+    image = torch.zeros((H, W, 4)) if rank == 0 else None
+    glist = [torch.empty((cap * W, 4)) for _ in range(world_size)] if rank == 0 else None
+    d.gather_tiles(torch.from_numpy(tile), image, glist, torch.tensor(src), torch.tensor(dst), W, world_size, rank)
+    if rank == 0:
+        q.put(image.numpy().reshape(-1, 4))
+    dist.barrier()
+    world.close()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world_size,rpb", [(2, 8), (3, 4)])
+def test_gather_of_rendered_shards_gloo(rtw, world_size, rpb):
+    """Each rank renders its row-interleaved shard (main.zig:314-326's split, made shardable) and rank 0
+    gathers and reassembles: the image equals a single-process host render of the whole frame bit for bit
+    (the counter-based RNG keys every sample by (seed, pixel, sample))."""
+    W, spp = 60, 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_render_worker, args=(r, world_size, port, W, spp, rpb, q))
+             for r in range(world_size)]
+    for p in procs:
+        p.start()
+    img = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    arr = rtw.flatten(rtw.worlds.generate_world(0, "book1"))
+    world = rtw.World(arr, device=rtw._abi.RTW_DEVICE_CPU)
+    cam = rtw.book1_camera(image_width=W, aspect_ratio=1.5, spp=spp).init()
+    ref = np.zeros((cam.size, 4), np.float32)
+    o = rtw._abi.render_opts()
+    rtw._abi.check(rtw.lib().rtw_render_ex(world.handle, C.byref(cam.derived), 0, cam.size, 0, spp, 13,
+                                           ref.ctypes.data, C.byref(o)), "rtw_render_ex")
+    world.close()
+    assert (ref[:, 3] == spp).all()
+    assert np.array_equal(img, ref)

@@ -100,9 +100,31 @@ class RtwKernelTiming(C.Structure):
     _fields_ = [("ms", C.c_float * 8), ("launches", C.c_uint32 * 8)]
 
 
+PROGRESS_FN = C.CFUNCTYPE(C.c_int, C.c_uint64, C.c_uint64, C.c_void_p)
+
+
 class RtwRenderOpts(C.Structure):
+    # ABI 5: running (a Zig bool, RenderThread.running: 0 = stop), cancel (non-zero = stop), progress
     _fields_ = [("spp_batch", C.c_uint32), ("flags", C.c_uint32), ("counters", C.c_void_p),
-                ("timing", C.POINTER(RtwKernelTiming))]
+                ("timing", C.POINTER(RtwKernelTiming)), ("running", C.c_void_p), ("cancel", C.c_void_p),
+                ("progress", PROGRESS_FN), ("user", C.c_void_p)]
+
+
+def render_opts(spp_batch: int = 0, flags: int = 0, counters=None, timing=None, running=None, cancel=None,
+                progress=None) -> RtwRenderOpts:
+    """rtw_render_opts.  running: a ctypes.c_uint8 (or c_bool) flag, 0 = stop (the reference's
+    RenderThread.running); cancel: a ctypes.c_int32, non-zero = stop; progress(done, total) -> True stops.
+    The returned struct keeps the callback alive (attribute _keep)."""
+    o = RtwRenderOpts(spp_batch, flags, counters, C.pointer(timing) if timing is not None else None)
+    if running is not None:
+        o.running = C.addressof(running)
+    if cancel is not None:
+        o.cancel = C.addressof(cancel)
+    if progress is not None:
+        cb = PROGRESS_FN(lambda done, total, user: 1 if progress(done, total) else 0)
+        o.progress = cb
+        o._keep = cb
+    return o
 
 
 class RtwTuning(C.Structure):
@@ -130,8 +152,6 @@ class RtwSceneStats(C.Structure):
                 ("device_bytes", C.c_uint64), ("axis_draws", C.c_uint32), ("_pad", C.c_uint32)]
 
 
-PROGRESS_FN = C.CFUNCTYPE(C.c_int, C.c_uint64, C.c_uint64, C.c_void_p)
-
 # every symbol include/rtw_gpu.h declares: name -> (restype, argtypes)
 SIGNATURES = {
     "rtw_version": (C.c_int, []),
@@ -144,6 +164,13 @@ SIGNATURES = {
     "rtw_scene_create_ex": (C.c_int, [C.POINTER(RtwSceneDesc), C.c_int, C.POINTER(RtwTuning), C.POINTER(C.c_void_p)]),
     "rtw_render": (C.c_int, [C.c_void_p, C.POINTER(RtwCamera), C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
                              C.c_uint64, C.c_void_p, C.c_void_p, PROGRESS_FN, C.c_void_p]),
+    "rtw_render_ex": (C.c_int, [C.c_void_p, C.POINTER(RtwCamera), C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
+                                C.c_uint64, C.c_void_p, C.POINTER(RtwRenderOpts)]),
+    "rtw_render_rows": (C.c_int, [C.c_void_p, C.POINTER(RtwCamera), C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
+                                  C.c_uint32, C.c_uint64, C.c_void_p, C.POINTER(RtwRenderOpts)]),
+    "rtw_render_multi_ex": (C.c_int, [C.c_void_p, C.POINTER(RtwCamera), C.c_uint32, C.c_uint32, C.c_uint32,
+                                      C.c_uint64, C.c_void_p, C.POINTER(RtwRenderOpts)]),
+    "rtw_multi_info": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint32), C.POINTER(C.c_int)]),
     "rtw_render_device": (C.c_int, [C.c_void_p, C.POINTER(RtwCamera), C.c_uint32, C.c_uint32, C.c_uint32,
                                     C.c_uint32, C.c_uint64, C.c_void_p, C.c_void_p, C.POINTER(RtwRenderOpts)]),
     "rtw_render_rows_device": (C.c_int, [C.c_void_p, C.POINTER(RtwCamera), C.c_uint32, C.c_uint32, C.c_uint32,

@@ -128,17 +128,19 @@ class Camera:
         self.render_range(state, start, end, 0, self.samples_per_pixel)
 
     def render_range(self, state: "RayTraceState", pix_begin: int, pix_end: int, spp_begin: int, spp_end: int,
-                     progress: Optional[Callable[[int, int], bool]] = None) -> None:
+                     progress: Optional[Callable[[int, int], bool]] = None, spp_batch: int = 0) -> None:
+        """Samples [spp_begin, spp_end) of pixels [pix_begin, pix_end) through rtw_render_ex, polling the
+        state's RenderThread.running flag (camera.zig:107) between sample batches (spp_batch, 0 = auto);
+        progress(done, total) -> True stops.  A stop raises RtwError(RTW_E_CANCELLED) with the finished
+        batches in the buffer (and the texture updated from them)."""
         w = state.writer
         buf = w.buffer
         assert buf.flags["C_CONTIGUOUS"] and buf.dtype == np.float32 and buf.shape == (self.size, 4)
-        cb = _abi.PROGRESS_FN(0)
-        if progress is not None:
-            cb = _abi.PROGRESS_FN(lambda done, total, user: 1 if progress(done, total) else 0)
-        rc = _abi.lib().rtw_render(state.world.handle, C.byref(self.derived), pix_begin, pix_end, spp_begin,
-                                   spp_end, state.seed, buf.ctypes.data, C.addressof(state.cancel), cb, None)
-        _abi.check(rc, "rtw_render")
+        opts = _abi.render_opts(spp_batch=spp_batch, running=state.running, progress=progress)
+        rc = _abi.lib().rtw_render_ex(state.world.handle, C.byref(self.derived), pix_begin, pix_end, spp_begin,
+                                      spp_end, state.seed, buf.ctypes.data, C.byref(opts))
         w.update_texture(pix_begin, pix_end)
+        _abi.check(rc, "rtw_render_ex")
 
 
 @dataclass
@@ -148,11 +150,13 @@ class RayTraceState:
     writer: SharedStateImageWriter
     world: World
     seed: int = 0
-    cancel: C.c_int32 = field(default_factory=lambda: C.c_int32(0))
+    # RenderThread.running (src/main.zig:50, a Zig bool; true from RenderThread.start, main.zig:55): the
+    # render polls it between sample batches (camera.zig:107), through rtw_render_opts.running
+    running: C.c_uint8 = field(default_factory=lambda: C.c_uint8(1))
 
     def stop(self):
-        """RenderThread.stop (src/main.zig:58-60): polled between sample batches."""
-        self.cancel.value = 1
+        """RenderThread.stop (src/main.zig:58-60): running = false."""
+        self.running.value = 0
 
     def count_samples(self) -> float:
         """countSamples (src/main.zig:470-477): f32 sum of buffer[i][3] (progress / POWER)."""
@@ -203,7 +207,7 @@ def progressive_render(state: RayTraceState, spp_begin: int = 0, batch: int = 1,
         cam.init()
     s = spp_begin
     spp = cam.samples_per_pixel
-    while s < spp and not state.cancel.value:
+    while s < spp and state.running.value:
         e = min(spp, s + batch)
         cam.render_range(state, 0, cam.size, s, e)
         s = e

@@ -19,27 +19,31 @@
 
 #include "rtw_device.h"
 
-int rtw_cpu_render(const rtw_launch& L, uint32_t pix_begin, uint32_t pix_end, float* accum, uint32_t threads,
-                   const volatile int32_t* cancel) {
-    const uint32_t n = pix_end - pix_begin;
+int rtw_cpu_render(const rtw_launch& L, uint32_t begin, uint32_t end, float* out, uint32_t threads,
+                   const rtw_render_opts* stop) {
+    const uint32_t n = end - begin;
     if (threads == 0) threads = std::max(1u, std::thread::hardware_concurrency());
     threads = std::min<uint32_t>(threads, std::max(1u, n));
     std::atomic<bool> stopped{false};
     // contiguous chunks, as startRender's Tasks (main.zig:318-324); samples in order per pixel
     auto work = [&](uint32_t t) {
-        const uint32_t a = pix_begin + (uint32_t)((uint64_t)n * t / threads);
-        const uint32_t b = pix_begin + (uint32_t)((uint64_t)n * (t + 1) / threads);
+        const uint32_t a = begin + (uint32_t)((uint64_t)n * t / threads);
+        const uint32_t b = begin + (uint32_t)((uint64_t)n * (t + 1) / threads);
         Counters cnt;
         for (uint32_t i = a; i < b; i++) {
-            if (cancel && *cancel) {  // polled per pixel, as Camera.render polls `running` (camera.zig:107)
+            if (rtw_stop_requested(stop)) {  // polled per pixel, as Camera.render polls `running` (camera.zig:107)
                 stopped = true;
                 return;
             }
-            const uint32_t x = i % L.W, y = i / L.W;
-            float* px = accum + 4 * (size_t)i;
+            const uint32_t x = i % L.W;
+            uint32_t y = i / L.W;
+            if (L.n_shards && !map_row(L, y, y)) continue;  // a shard's logical row -> image row (rows past H: none)
+            if (y >= L.H) continue;
+            const uint32_t pixel = y * L.W + x;
+            float* px = out + 4 * (size_t)i;
             float r = px[0], g = px[1], bl = px[2];
             for (uint32_t s = L.s0; s < L.s1; s++) {
-                const f3 c = sample_radiance<RTW_F_ALL>(L.nodes, L, i, x + L.pixel_offset, y + L.pixel_offset, s,
+                const f3 c = sample_radiance<RTW_F_ALL>(L.nodes, L, pixel, x + L.pixel_offset, y + L.pixel_offset, s,
                                                         cnt);
                 r += c.x;
                 g += c.y;

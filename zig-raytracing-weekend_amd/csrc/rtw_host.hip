@@ -241,12 +241,11 @@ int rtw_scene_create_ex(const rtw_scene_desc* d, int device, const rtw_tuning* t
     if (w2_stack > RTW_W2_STACK_MAX) w2.clear();
 
     // Blob layout (each section 256-B aligned): nodes | cvec | spheres | quads | members | instances | media |
-    // materials | textures | images-info | perlin | image bytes
+    // materials | textures | images-info | perlin | image bytes || compact nodes | two-wide records (not hashed)
     auto align = [](size_t x) { return (x + 255) & ~size_t(255); };
     const size_t n_nodes = ctx->nodes_host.size() / orders;  // per ordering
     size_t off = 0;
     const size_t o_nodes = off; off = align(off + ctx->nodes_host.size() * sizeof(rtw_node));
-    const size_t o_cnod = off; off = align(off + cnodes.size() * sizeof(rtw_cnode));
     const size_t o_cvec = off; off = align(off + cvec.size() * sizeof(float) + 16);
     const size_t o_sph = off; off = align(off + geom.spheres.size() * sizeof(rtw_dev_sphere) + 16);
     const size_t o_quad = off; off = align(off + geom.quads.size() * sizeof(rtw_dev_quad) + 16);
@@ -268,7 +267,10 @@ int rtw_scene_create_ex(const rtw_scene_desc* d, int device, const rtw_tuning* t
         img_bytes += align((size_t)d->images[i].bytes_per_row * d->images[i].height);
     }
     off = align(off + img_bytes + 16);
-    const size_t hashed = off;  // the scene image; the walk's derived records below are a tuning choice
+    // the scene image: the walks' derived records below (compact nodes, two-wide records) depend on the
+    // backend and the tuning, so a checkpoint's hash matches on every context of the same scene
+    const size_t hashed = off;
+    const size_t o_cnod = off; off = align(off + cnodes.size() * sizeof(rtw_cnode));
     const size_t o_w2 = off; off = align(off + w2.size() * sizeof(rtw_cnode));
     const size_t o_w2l = off; off = align(off + w2leaf.size() * sizeof(uint32_t));
 
@@ -641,12 +643,15 @@ int run_wavefront(rtw_ctx* ctx, rtw_launch L, hipStream_t stream, rtw_timer* T) 
     return RTW_OK;
 }
 
+// Enqueue [s0, s1) in batches of `batch` samples on `stream`.  When the caller polls (ctl's stop
+// flags or progress, ABI 5) the stop flags are read before every batch and, after each one, the stream
+// is synchronised and progress called: a stop keeps the finished batches (their .w = the last batch's end).
 int run_batches(rtw_ctx* ctx, rtw_launch L, uint32_t s0, uint32_t s1, uint32_t batch, hipStream_t stream,
-                bool sync_each, const volatile int32_t* cancel, rtw_progress_fn progress, void* user,
-                uint64_t pixels, rtw_timer* T = nullptr) {
+                const rtw_render_opts* ctl, uint64_t pixels, rtw_timer* T = nullptr) {
     const uint64_t total = pixels * (uint64_t)(s1 - s0);
+    const bool polled = rtw_polled(ctl);
     for (uint32_t s = s0; s < s1; s += batch) {
-        if (cancel && *cancel) return fail(RTW_E_CANCELLED, "cancelled");
+        if (rtw_stop_requested(ctl)) return fail(RTW_E_CANCELLED, "cancelled");
         L.s0 = s;
         L.s1 = (s1 - s < batch) ? s1 : s + batch;
         if (ctx->variant == 2) {
@@ -659,11 +664,36 @@ int run_batches(rtw_ctx* ctx, rtw_launch L, uint32_t s0, uint32_t s1, uint32_t b
             hipError_t e = hipGetLastError();
             if (e != hipSuccess) return hip_fail(e, "render launch");
         }
-        if (sync_each) {
+        if (polled) {
             HIP_TRY(hipStreamSynchronize(stream));
-            if (progress && progress(pixels * (uint64_t)(L.s1 - s0), total, user)) return fail(RTW_E_CANCELLED, "cancelled by progress callback");
+            if (ctl->progress && ctl->progress(pixels * (uint64_t)(L.s1 - s0), total, ctl->user))
+                return fail(RTW_E_CANCELLED, "cancelled by progress callback");
         }
     }
+    return RTW_OK;
+}
+
+// Host context: samples [s0, s1) in batches on host threads (rtw_cpu.hip), stop flags polled per pixel,
+// progress after each batch.  begin/end/out as rtw_cpu_render.
+int run_host(const rtw_ctx* ctx, rtw_launch L, uint32_t begin, uint32_t end, uint32_t s0, uint32_t s1,
+             uint32_t batch, float* out, const rtw_render_opts* ctl, uint64_t pixels) {
+    if (!batch) batch = s1 - s0;
+    const uint64_t total = pixels * (uint64_t)(s1 - s0);
+    for (uint32_t s = s0; s < s1; s += batch) {
+        L.s0 = s;
+        L.s1 = (s1 - s < batch) ? s1 : s + batch;
+        if (rtw_cpu_render(L, begin, end, out, ctx->cpu_threads, ctl) == RTW_E_CANCELLED)
+            return fail(RTW_E_CANCELLED, "cancelled");
+        if (ctl && ctl->progress && ctl->progress(pixels * (uint64_t)(L.s1 - s0), total, ctl->user))
+            return fail(RTW_E_CANCELLED, "cancelled by progress callback");
+    }
+    return RTW_OK;
+}
+
+// the ABI-5 options of the host-buffer entry points: stop/progress and spp_batch only
+int check_host_opts(const rtw_render_opts* o) {
+    if (o && (o->flags || o->counters || o->timing))
+        return fail(RTW_E_INVALID, "host-buffer render: flags, counters and timing must be 0/NULL");
     return RTW_OK;
 }
 
@@ -690,6 +720,20 @@ void set_tiles(rtw_launch& L) {
     L.n_tiles = L.n_tiles_x * ((L.n_rows + RTW_TILE_H - 1) / RTW_TILE_H);
 }
 
+// the context's device staging buffer of the host-buffer entry points, >= bytes
+int ensure_scratch(rtw_ctx* ctx, size_t bytes) {
+    if (ctx->scratch_bytes >= bytes) return RTW_OK;
+    if (ctx->d_scratch) {
+        HIP_TRY(hipStreamSynchronize(ctx->stream));
+        (void)hipFree(ctx->d_scratch);
+    }
+    ctx->d_scratch = nullptr;
+    ctx->scratch_bytes = 0;
+    HIP_TRY(hipMalloc(&ctx->d_scratch, bytes));
+    ctx->scratch_bytes = bytes;
+    return RTW_OK;
+}
+
 // Order this call's stream after the previous call's work on this context (another stream).
 int stream_enter(rtw_ctx* ctx, hipStream_t s) {
     if (ctx->last_stream && ctx->last_stream != s) HIP_TRY(hipStreamWaitEvent(s, ctx->last_done, 0));
@@ -702,6 +746,39 @@ int stream_leave(rtw_ctx* ctx, hipStream_t s) {
     return RTW_OK;
 }
 
+// A GPU context's shard render into the device tile on stream s (the caller holds ctx->mu and has set
+// the device and entered the stream): row blocks b with b % n_shards == shard, tile rows in order.
+int render_rows_locked(rtw_ctx* ctx, const rtw_camera* cam, uint32_t rpb, uint32_t n_shards, uint32_t shard,
+                       uint32_t spp_begin, uint32_t spp_end, uint64_t seed, float* d_tile, hipStream_t s,
+                       const rtw_render_opts* opts, uint32_t rows) {
+    rtw_launch L = make_launch(ctx, cam, seed);
+    L.accum = reinterpret_cast<float4*>(d_tile);
+    L.row0 = 0;
+    // logical rows 0 .. (#blocks owned * rpb); rows past H are masked in-kernel
+    const uint32_t nblk = (cam->image_height + rpb - 1) / rpb;
+    const uint32_t owned = nblk > shard ? (nblk - shard + n_shards - 1) / n_shards : 0;
+    L.n_rows = owned * rpb;
+    L.rpb = rpb;
+    L.n_shards = n_shards;
+    L.shard = shard;
+    L.pix_begin = 0;
+    L.pix_end = cam->size;
+    L.counters = opts ? reinterpret_cast<unsigned long long*>(opts->counters) : nullptr;
+    set_tiles(L);
+    uint32_t batch = opts && opts->spp_batch ? opts->spp_batch : auto_batch(ctx, (uint64_t)rows * cam->image_width, spp_end - spp_begin);
+    rtw_timer T;
+    T.stream = s;
+    T.pool.swap(ctx->ev_pool);
+    rtw_timer* tp = (opts && opts->timing) ? &T : nullptr;
+    int rc = run_batches(ctx, L, spp_begin, spp_end, batch, s, opts, (uint64_t)rows * cam->image_width, tp);
+    ctx->ev_pool.swap(T.pool);
+    if (int rl = stream_leave(ctx, s)) return rl;
+    if (tp && rc == RTW_OK) rc = harvest_timing(ctx, T, opts->timing);
+    if (rc) return rc;
+    if (!(opts && (opts->flags & RTW_RENDER_NO_SYNC))) HIP_TRY(hipStreamSynchronize(s));
+    return RTW_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -709,36 +786,32 @@ extern "C" {
 int rtw_render(rtw_ctx* ctx, const rtw_camera* cam, uint32_t pix_begin, uint32_t pix_end, uint32_t spp_begin,
                uint32_t spp_end, uint64_t seed, float* accum, const volatile int32_t* cancel,
                rtw_progress_fn progress, void* user) {
+    rtw_render_opts o{};
+    o.cancel = cancel;
+    o.progress = progress;
+    o.user = user;
+    return rtw_render_ex(ctx, cam, pix_begin, pix_end, spp_begin, spp_end, seed, accum, &o);
+}
+
+int rtw_render_ex(rtw_ctx* ctx, const rtw_camera* cam, uint32_t pix_begin, uint32_t pix_end, uint32_t spp_begin,
+                  uint32_t spp_end, uint64_t seed, float* accum, const rtw_render_opts* opts) {
     if (!ctx || !accum) return fail(RTW_E_INVALID, "null ctx/accum");
     if (int rc = validate_cam(cam)) return rc;
+    if (int rc = check_host_opts(opts)) return rc;
     if (pix_end > cam->size || pix_begin > pix_end) return fail(RTW_E_INVALID, "pixel range out of image");
     if (spp_begin > spp_end) return fail(RTW_E_INVALID, "bad sample range");
     if (pix_begin == pix_end || spp_begin == spp_end) return RTW_OK;
+    const uint32_t ubatch = opts ? opts->spp_batch : 0u;
     std::lock_guard<std::mutex> lock(ctx->mu);
     if (ctx->device == RTW_DEVICE_CPU) {  // host context: Camera.render on host threads (rtw_cpu.hip)
         rtw_launch L = make_launch(ctx, cam, seed);
-        L.s0 = spp_begin;
-        L.s1 = spp_end;
-        const int rc = rtw_cpu_render(L, pix_begin, pix_end, accum, ctx->cpu_threads, cancel);
-        if (rc == RTW_E_CANCELLED) return fail(rc, "cancelled");
-        if (progress && progress((uint64_t)(pix_end - pix_begin) * (spp_end - spp_begin),
-                                 (uint64_t)(pix_end - pix_begin) * (spp_end - spp_begin), user))
-            return fail(RTW_E_CANCELLED, "cancelled by progress callback");
-        return rc;
+        L.n_shards = 0;
+        return run_host(ctx, L, pix_begin, pix_end, spp_begin, spp_end, ubatch, accum, opts, pix_end - pix_begin);
     }
     HIP_TRY(hipSetDevice(ctx->device));
     if (int rc = stream_enter(ctx, ctx->stream)) return rc;
     const size_t bytes = (size_t)cam->size * 16;
-    if (ctx->scratch_bytes < bytes) {
-        if (ctx->d_scratch) {
-            HIP_TRY(hipStreamSynchronize(ctx->stream));
-            (void)hipFree(ctx->d_scratch);
-        }
-        ctx->d_scratch = nullptr;
-        ctx->scratch_bytes = 0;
-        HIP_TRY(hipMalloc(&ctx->d_scratch, bytes));
-        ctx->scratch_bytes = bytes;
-    }
+    if (int rc = ensure_scratch(ctx, bytes)) return rc;
     const size_t o = (size_t)pix_begin * 16, nb = (size_t)(pix_end - pix_begin) * 16;
     HIP_TRY(hipMemcpyAsync((char*)ctx->d_scratch + o, (char*)accum + o, nb, hipMemcpyHostToDevice, ctx->stream));
     rtw_launch L = make_launch(ctx, cam, seed);
@@ -750,9 +823,10 @@ int rtw_render(rtw_ctx* ctx, const rtw_camera* cam, uint32_t pix_begin, uint32_t
     L.n_shards = 0;
     L.counters = nullptr;
     set_tiles(L);
-    const uint32_t batch = auto_batch(ctx, pix_end - pix_begin, spp_end - spp_begin);
-    int rc = run_batches(ctx, L, spp_begin, spp_end, batch, ctx->stream, true, cancel, progress, user,
-                         pix_end - pix_begin);
+    const uint32_t batch = ubatch ? ubatch : auto_batch(ctx, pix_end - pix_begin, spp_end - spp_begin);
+    rtw_render_opts ctl{};  // the host API always reports progress per batch when asked, like rtw_render did
+    if (opts) ctl = *opts;
+    int rc = run_batches(ctx, L, spp_begin, spp_end, batch, ctx->stream, &ctl, pix_end - pix_begin);
     // copy back whatever was rendered (also on cancel: completed batches are valid)
     hipError_t e = hipMemcpyAsync((char*)accum + o, (char*)ctx->d_scratch + o, nb, hipMemcpyDeviceToHost, ctx->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
@@ -787,7 +861,7 @@ int rtw_render_device(rtw_ctx* ctx, const rtw_camera* cam, uint32_t pix_begin, u
     T.stream = s;
     T.pool.swap(ctx->ev_pool);
     rtw_timer* tp = (opts && opts->timing) ? &T : nullptr;
-    int rc = run_batches(ctx, L, spp_begin, spp_end, batch, s, false, nullptr, nullptr, nullptr, pix_end - pix_begin, tp);
+    int rc = run_batches(ctx, L, spp_begin, spp_end, batch, s, opts, pix_end - pix_begin, tp);
     ctx->ev_pool.swap(T.pool);
     if (int rl = stream_leave(ctx, s)) return rl;
     if (tp && rc == RTW_OK) rc = harvest_timing(ctx, T, opts->timing);
@@ -816,7 +890,7 @@ int rtw_render_rows_device(rtw_ctx* ctx, const rtw_camera* cam, uint32_t rpb, ui
                            uint32_t spp_begin, uint32_t spp_end, uint64_t seed, float* d_tile, void* stream,
                            const rtw_render_opts* opts) {
     if (!ctx || !d_tile) return fail(RTW_E_INVALID, "null ctx/tile");
-    if (ctx->device == RTW_DEVICE_CPU) return fail(RTW_E_INVALID, "host context: use rtw_render");
+    if (ctx->device == RTW_DEVICE_CPU) return fail(RTW_E_INVALID, "host context: use rtw_render_rows");
     if (int rc = validate_cam(cam)) return rc;
     if (!rpb || !n_shards || shard >= n_shards) return fail(RTW_E_INVALID, "bad shard spec");
     if (spp_begin > spp_end) return fail(RTW_E_INVALID, "bad sample range");
@@ -826,33 +900,42 @@ int rtw_render_rows_device(rtw_ctx* ctx, const rtw_camera* cam, uint32_t rpb, ui
     HIP_TRY(hipSetDevice(ctx->device));
     hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
     if (int rc = stream_enter(ctx, s)) return rc;
-    rtw_launch L = make_launch(ctx, cam, seed);
-    L.accum = reinterpret_cast<float4*>(d_tile);
-    L.row0 = 0;
-    // logical rows 0 .. (#blocks owned * rpb); rows past H are masked in-kernel
-    const uint32_t nblk = (cam->image_height + rpb - 1) / rpb;
-    const uint32_t owned = nblk > shard ? (nblk - shard + n_shards - 1) / n_shards : 0;
-    L.n_rows = owned * rpb;
-    L.rpb = rpb;
-    L.n_shards = n_shards;
-    L.shard = shard;
-    L.pix_begin = 0;
-    L.pix_end = cam->size;
-    L.counters = opts ? reinterpret_cast<unsigned long long*>(opts->counters) : nullptr;
-    set_tiles(L);
-    uint32_t batch = opts && opts->spp_batch ? opts->spp_batch : auto_batch(ctx, (uint64_t)rows * cam->image_width, spp_end - spp_begin);
-    rtw_timer T;
-    T.stream = s;
-    T.pool.swap(ctx->ev_pool);
-    rtw_timer* tp = (opts && opts->timing) ? &T : nullptr;
-    int rc = run_batches(ctx, L, spp_begin, spp_end, batch, s, false, nullptr, nullptr, nullptr,
-                         (uint64_t)rows * cam->image_width, tp);
-    ctx->ev_pool.swap(T.pool);
-    if (int rl = stream_leave(ctx, s)) return rl;
-    if (tp && rc == RTW_OK) rc = harvest_timing(ctx, T, opts->timing);
-    if (rc) return rc;
-    if (!(opts && (opts->flags & RTW_RENDER_NO_SYNC))) HIP_TRY(hipStreamSynchronize(s));
-    return RTW_OK;
+    return render_rows_locked(ctx, cam, rpb, n_shards, shard, spp_begin, spp_end, seed, d_tile, s, opts, rows);
+}
+
+int rtw_render_rows(rtw_ctx* ctx, const rtw_camera* cam, uint32_t rpb, uint32_t n_shards, uint32_t shard,
+                    uint32_t spp_begin, uint32_t spp_end, uint64_t seed, float* tile, const rtw_render_opts* opts) {
+    if (!ctx || !tile) return fail(RTW_E_INVALID, "null ctx/tile");
+    if (int rc = validate_cam(cam)) return rc;
+    if (int rc = check_host_opts(opts)) return rc;
+    if (!rpb || !n_shards || shard >= n_shards) return fail(RTW_E_INVALID, "bad shard spec");
+    if (spp_begin > spp_end) return fail(RTW_E_INVALID, "bad sample range");
+    const uint32_t rows = rtw_shard_rows(cam->image_height, rpb, n_shards, shard);
+    if (rows == 0 || spp_begin == spp_end) return RTW_OK;
+    std::lock_guard<std::mutex> lock(ctx->mu);
+    const uint32_t W = cam->image_width;
+    if (ctx->device == RTW_DEVICE_CPU) {  // the shard on host threads (rtw_cpu.hip), tile rows in order
+        rtw_launch L = make_launch(ctx, cam, seed);
+        L.rpb = rpb;
+        L.n_shards = n_shards;
+        L.shard = shard;
+        return run_host(ctx, L, 0, rows * W, spp_begin, spp_end, opts ? opts->spp_batch : 0u, tile, opts,
+                        (uint64_t)rows * W);
+    }
+    HIP_TRY(hipSetDevice(ctx->device));
+    if (int rc = stream_enter(ctx, ctx->stream)) return rc;
+    const size_t nb = (size_t)rows * W * 16;
+    if (int rc = ensure_scratch(ctx, nb)) return rc;
+    HIP_TRY(hipMemcpyAsync(ctx->d_scratch, tile, nb, hipMemcpyHostToDevice, ctx->stream));
+    rtw_render_opts ctl{};
+    if (opts) ctl = *opts;
+    int rc = render_rows_locked(ctx, cam, rpb, n_shards, shard, spp_begin, spp_end, seed, ctx->d_scratch, ctx->stream,
+                                &ctl, rows);
+    hipError_t e = hipMemcpyAsync(tile, ctx->d_scratch, nb, hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    if (e != hipSuccess) return hip_fail(e, "rtw_render_rows copy back");
+    ctx->last_stream = nullptr;  // synchronised
+    return rc;
 }
 
 int rtw_texture_from_accum(const float* accum, uint32_t n, uint8_t* out) {

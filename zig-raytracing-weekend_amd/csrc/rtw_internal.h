@@ -105,9 +105,19 @@ int rtw_persistent_grid(uint32_t feat, uint32_t n_nodes, int waves, bool use_lds
 
 void rtw_launch_render(const rtw_launch& L, void* stream, int variant, int grid);
 void rtw_set_error(const char* msg);  // the thread's rtw_last_error() message (rtw_host.hip)
-// host backend (rtw_cpu.hip): samples [L.s0, L.s1) of pixels [pix_begin, pix_end) onto host float4 accum
-int rtw_cpu_render(const rtw_launch& L, uint32_t pix_begin, uint32_t pix_end, float* accum, uint32_t threads,
-                   const volatile int32_t* cancel);
+// ABI-5 stop flags of rtw_render_opts: RenderThread.running (a Zig bool, 0 = stop) or cancel (non-zero = stop)
+inline bool rtw_stop_requested(const rtw_render_opts* o) {
+    return o && ((o->running && *o->running == 0) || (o->cancel && *o->cancel != 0));
+}
+// does the caller poll between batches (stop flags or progress)?
+inline bool rtw_polled(const rtw_render_opts* o) { return o && (o->running || o->cancel || o->progress); }
+
+// host backend (rtw_cpu.hip): samples [L.s0, L.s1) of the logical pixels [begin, end) onto host float4 `out`.
+// Plain launches (L.n_shards == 0): logical pixel = image pixel, out = the frame.  Shard launches: logical
+// pixel r * W + x of the shard's tile (image row rtw_tile_row_image(L.rpb, L.n_shards, L.shard, r)), out =
+// the tile.  `stop` (may be null) is polled per pixel, as Camera.render polls `running` (camera.zig:107).
+int rtw_cpu_render(const rtw_launch& L, uint32_t begin, uint32_t end, float* out, uint32_t threads,
+                   const rtw_render_opts* stop);
 void rtw_launch_debug_rng(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t n, float* d_out, void* stream);
 void rtw_launch_debug_sample(const rtw_launch& L, uint32_t pixel, uint32_t sample, float* d_out, void* stream);
 

@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -53,6 +54,26 @@ int mfail(int code, const std::string& msg) {
         ncclResult_t _r = (expr);                                                            \
         if (_r != ncclSuccess) return mfail(RTW_E_HIP, std::string(#expr) + ": " + ncclGetErrorString(_r)); \
     } while (0)
+
+// The calls of one RCCL group: the first failure is kept and the group is always closed (an open
+// group would defer every later RCCL call of this thread).
+struct NcclGroup {
+    ncclResult_t first = ncclSuccess;
+    const char* what = "";
+    void add(ncclResult_t r, const char* w) {
+        if (first == ncclSuccess && r != ncclSuccess) {
+            first = r;
+            what = w;
+        }
+    }
+    bool ok() const { return first == ncclSuccess; }
+    int end() {
+        const ncclResult_t e = ncclGroupEnd();
+        if (first != ncclSuccess) return mfail(RTW_E_HIP, std::string(what) + ": " + ncclGetErrorString(first));
+        if (e != ncclSuccess) return mfail(RTW_E_HIP, std::string("ncclGroupEnd: ") + ncclGetErrorString(e));
+        return RTW_OK;
+    }
+};
 
 // dir 0: frame rows -> stacked tiles (pack); dir 1: stacked tiles -> frame rows (unpack).
 // One thread per float4; x fastest, so both sides are contiguous runs of W.
@@ -107,13 +128,17 @@ int ensure_buffers(rtw_multi* m, size_t tile_elems, size_t frame_elems) {
 
 // The device-side frame render; the caller holds m->mu.  Streams: every device's work
 // runs on its context's own stream; `stream` (device 0) is joined in and out by events.
+// Samples in batches of spp_batch (0: one batch unless the caller polls); when ctl polls, every
+// device finishes batch b before progress and the stop flags are read, and a stop ends the loop
+// after the last finished batch -- the gather below then brings the finished batches to the frame.
 int multi_render(rtw_multi* m, const rtw_camera* cam, uint32_t rpb, uint32_t s0, uint32_t s1, uint64_t seed,
-                 float4* frame, hipStream_t stream, uint32_t spp_batch, uint32_t flags) {
+                 float4* frame, hipStream_t stream, uint32_t spp_batch, uint32_t flags, const rtw_render_opts* ctl) {
     const uint32_t n = (uint32_t)m->ctx.size();
     const uint32_t W = cam->image_width, H = cam->image_height;
     const uint32_t nblk = (H + rpb - 1) / rpb;
     const uint32_t cap = (nblk + n - 1) / n * rpb;
     const size_t per = (size_t)cap * W;
+    if (rtw_stop_requested(ctl)) return mfail(RTW_E_CANCELLED, "cancelled");  // nothing touched
     if (int rc = ensure_buffers(m, per, 0)) return rc;
     hipStream_t s_root = m->ctx[0]->stream;
     MHIP(hipSetDevice(m->dev[0]));
@@ -135,26 +160,50 @@ int multi_render(rtw_multi* m, const rtw_camera* cam, uint32_t rpb, uint32_t s0,
                            cap, 0u);
         MHIP(hipGetLastError());
         MNCCL(ncclGroupStart());
-        for (uint32_t k = 0; k < n; k++) {
-            MNCCL(ncclSend(m->stacked + k * per, count, ncclFloat32, (int)k, m->comm[0], s_root));
-            MNCCL(ncclRecv(m->tile[k], count, ncclFloat32, 0, m->comm[k], m->ctx[k]->stream));
+        NcclGroup g;
+        for (uint32_t k = 0; k < n && g.ok(); k++) {
+            g.add(ncclSend(m->stacked + k * per, count, ncclFloat32, (int)k, m->comm[0], s_root), "ncclSend");
+            if (g.ok()) g.add(ncclRecv(m->tile[k], count, ncclFloat32, 0, m->comm[k], m->ctx[k]->stream), "ncclRecv");
         }
-        MNCCL(ncclGroupEnd());
+        if (int rc = g.end()) return rc;
     }
+    const bool polled = rtw_polled(ctl);
+    const uint64_t pixels = (uint64_t)W * H;
+    uint32_t batch = spp_batch ? spp_batch : s1 - s0;
+    if (!spp_batch && polled) {  // the single-context auto batch of the largest shard
+        const uint64_t target = m->ctx[0]->variant == 2 ? m->ctx[0]->wf_max_paths : (64ull << 20);
+        const uint64_t b = target / std::max<uint64_t>(1, per);
+        batch = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(b, 1), s1 - s0);
+    }
+    int stop = RTW_OK;
     rtw_render_opts o{};
-    o.spp_batch = spp_batch;
     o.flags = RTW_RENDER_NO_SYNC;
-    for (uint32_t k = 0; k < n; k++) {  // enqueue only: the N devices render concurrently
-        const int rc = rtw_render_rows_device(m->ctx[k], cam, rpb, n, k, s0, s1, seed,
-                                              reinterpret_cast<float*>(m->tile[k]), nullptr, &o);
-        if (rc) return mfail(rc, std::string("shard render: ") + rtw_last_error());
+    for (uint32_t b0 = s0; b0 < s1 && stop == RTW_OK; b0 += batch) {
+        const uint32_t b1 = (s1 - b0 < batch) ? s1 : b0 + batch;
+        o.spp_batch = b1 - b0;
+        for (uint32_t k = 0; k < n; k++) {  // enqueue only: the N devices render concurrently
+            const int rc = rtw_render_rows_device(m->ctx[k], cam, rpb, n, k, b0, b1, seed,
+                                                  reinterpret_cast<float*>(m->tile[k]), nullptr, &o);
+            if (rc) return mfail(rc, std::string("shard render: ") + rtw_last_error());
+        }
+        if (polled) {
+            for (uint32_t k = 0; k < n; k++) {
+                MHIP(hipSetDevice(m->dev[k]));
+                MHIP(hipStreamSynchronize(m->ctx[k]->stream));
+            }
+            if (ctl->progress && ctl->progress(pixels * (uint64_t)(b1 - s0), pixels * (uint64_t)(s1 - s0), ctl->user))
+                stop = mfail(RTW_E_CANCELLED, "cancelled by progress callback");
+            else if (b1 < s1 && rtw_stop_requested(ctl))
+                stop = mfail(RTW_E_CANCELLED, "cancelled");
+        }
     }
     MNCCL(ncclGroupStart());  // the tiles to device 0 (the gather)
-    for (uint32_t k = 0; k < n; k++) {
-        MNCCL(ncclSend(m->tile[k], count, ncclFloat32, 0, m->comm[k], m->ctx[k]->stream));
-        MNCCL(ncclRecv(m->stacked + k * per, count, ncclFloat32, (int)k, m->comm[0], s_root));
+    NcclGroup g;
+    for (uint32_t k = 0; k < n && g.ok(); k++) {
+        g.add(ncclSend(m->tile[k], count, ncclFloat32, 0, m->comm[k], m->ctx[k]->stream), "ncclSend");
+        if (g.ok()) g.add(ncclRecv(m->stacked + k * per, count, ncclFloat32, (int)k, m->comm[0], s_root), "ncclRecv");
     }
-    MNCCL(ncclGroupEnd());
+    if (int rc = g.end()) return rc;
     MHIP(hipSetDevice(m->dev[0]));
     hipLaunchKernelGGL(shard_rows_copy, dim3(blocks), dim3(256), 0, s_root, frame, m->stacked, W, H, rpb, n, cap,
                        1u);
@@ -163,7 +212,7 @@ int multi_render(rtw_multi* m, const rtw_camera* cam, uint32_t rpb, uint32_t s0,
         MHIP(hipEventRecord(m->ev_out, s_root));
         MHIP(hipStreamWaitEvent(stream, m->ev_out, 0));
     }
-    return RTW_OK;
+    return stop;
 }
 
 int check_args(rtw_multi* m, const rtw_camera* cam, uint32_t rpb, uint32_t s0, uint32_t s1) {
@@ -240,31 +289,52 @@ int rtw_render_multi_device(rtw_multi* m, const rtw_camera* cam, uint32_t rpb, u
     std::lock_guard<std::mutex> lock(m->mu);
     const uint32_t flags = opts ? opts->flags : 0u;
     int rc = multi_render(m, cam, rpb, s0, s1, seed, reinterpret_cast<float4*>(d_accum), (hipStream_t)stream,
-                          opts ? opts->spp_batch : 0u, flags);
-    if (rc) return rc;
+                          opts ? opts->spp_batch : 0u, flags, opts);
+    if (rc && rc != RTW_E_CANCELLED) return rc;
     if (!(flags & RTW_RENDER_NO_SYNC)) {
         MHIP(hipSetDevice(m->dev[0]));
         MHIP(hipStreamSynchronize(stream ? (hipStream_t)stream : m->ctx[0]->stream));
     }
-    return RTW_OK;
+    return rc;
 }
 
-int rtw_render_multi(rtw_multi* m, const rtw_camera* cam, uint32_t rpb, uint32_t s0, uint32_t s1, uint64_t seed,
-                     float* accum, const volatile int32_t* cancel) {
+int rtw_render_multi_ex(rtw_multi* m, const rtw_camera* cam, uint32_t rpb, uint32_t s0, uint32_t s1, uint64_t seed,
+                        float* accum, const rtw_render_opts* opts) {
     if (int rc = check_args(m, cam, rpb, s0, s1)) return rc;
     if (!accum) return mfail(RTW_E_INVALID, "null accum");
+    if (opts && (opts->flags || opts->counters || opts->timing))
+        return mfail(RTW_E_INVALID, "host-buffer render: flags, counters and timing must be 0/NULL");
     if (s0 == s1) return RTW_OK;
-    if (cancel && *cancel) return mfail(RTW_E_CANCELLED, "cancelled");
+    if (rtw_stop_requested(opts)) return mfail(RTW_E_CANCELLED, "cancelled");
     std::lock_guard<std::mutex> lock(m->mu);
     const size_t px = (size_t)cam->image_width * cam->image_height;
     if (int rc = ensure_buffers(m, 0, px)) return rc;
     hipStream_t s = m->ctx[0]->stream;
     MHIP(hipSetDevice(m->dev[0]));
     MHIP(hipMemcpyAsync(m->frame, accum, px * sizeof(float4), hipMemcpyHostToDevice, s));
-    if (int rc = multi_render(m, cam, rpb, s0, s1, seed, m->frame, nullptr, 0u, 0u)) return rc;
+    const int rc = multi_render(m, cam, rpb, s0, s1, seed, m->frame, nullptr, opts ? opts->spp_batch : 0u, 0u, opts);
+    if (rc && rc != RTW_E_CANCELLED) return rc;
     MHIP(hipSetDevice(m->dev[0]));
     MHIP(hipMemcpyAsync(accum, m->frame, px * sizeof(float4), hipMemcpyDeviceToHost, s));
     MHIP(hipStreamSynchronize(s));
+    return rc;  // RTW_E_CANCELLED: accum holds the finished batches
+}
+
+int rtw_render_multi(rtw_multi* m, const rtw_camera* cam, uint32_t rpb, uint32_t s0, uint32_t s1, uint64_t seed,
+                     float* accum, const volatile int32_t* cancel) {
+    rtw_render_opts o{};
+    o.cancel = cancel;
+    return rtw_render_multi_ex(m, cam, rpb, s0, s1, seed, accum, &o);
+}
+
+int rtw_multi_info(rtw_multi* m, uint32_t* n_devices, int* rccl_ranks) {
+    if (!m) return mfail(RTW_E_INVALID, "null rtw_multi");
+    if (n_devices) *n_devices = (uint32_t)m->ctx.size();
+    if (rccl_ranks) {
+        int c = 0;
+        MNCCL(ncclCommCount(m->comm[0], &c));
+        *rccl_ranks = c;
+    }
     return RTW_OK;
 }
 

@@ -251,12 +251,14 @@ __device__ __forceinline__ int traverse_wide2(const rtw_launch& L, const Ray& r,
     return hit < 0 ? hit : (int)L.w2leaf[hit];
 }
 
-// the walk of a static sphere scene through L1/L2: two-wide when the records exist
+// the walk of a static sphere scene through L1/L2: two-wide when the records exist and the FMA slab
+// test is allowed (its fp16 boxes are supersets only of boxes padded for |o| <= 7 * extent: make_launch
+// clears fast_box for a farther camera, and tuning.fast_box = 0 asks for the exact aabb.zig walk)
 template <uint32_t FEAT>
 __device__ __forceinline__ int wf_traverse_global(const rtw_launch& L, const Ray& r, float& t, Counters& cnt,
                                                   uint64_t mkey) {
     if constexpr ((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING)) == 0) {
-        if (L.w2nodes)
+        if (L.w2nodes && L.fast_box)
             return L.counters ? traverse_wide2<true>(L, r, t, cnt) : traverse_wide2<false>(L, r, t, cnt);
     }
     return traverse<FEAT>(L.nodes, L, r, t, cnt, mkey);
@@ -1123,7 +1125,7 @@ void wf_launch_tail(const rtw_launch& L, const rtw_wf& W, hipStream_t st, int n_
 template <uint32_t FEAT>
 size_t wf_w2_lds(const rtw_launch& L) {
     if constexpr ((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING)) == 0) {
-        if (L.w2nodes) return (size_t)256u * 4u * L.w2_stack;
+        if (L.w2nodes && L.fast_box) return (size_t)256u * 4u * L.w2_stack;
     }
     return 0;
 }

@@ -49,6 +49,20 @@ def reassembly_index(height: int, rows_per_block: int, n_shards: int) -> Tuple[L
     return src, dst
 
 
+def render_rows_host(world, cam, rows_per_block: int, n_shards: int, shard: int, spp_begin: int, spp_end: int,
+                     tile, seed: int = 0, running=None, progress=None, spp_batch: int = 0) -> None:
+    """rtw_render_rows: this shard's rows x samples [spp_begin, spp_end) onto a HOST float32 tile
+    [rows_in_shard * W, 4] (blocking), on a GPU context or a host context (RTW_DEVICE_CPU) -- one process
+    per rank renders its shard without a GPU (the gloo tests), bit-identical to the device path."""
+    assert tile.dtype.name == "float32" and tile.flags.c_contiguous
+    rows = _abi.lib().rtw_shard_rows(cam.derived.image_height, rows_per_block, n_shards, shard)
+    assert tile.size >= rows * cam.derived.image_width * 4
+    opts = _abi.render_opts(spp_batch=spp_batch, running=running, progress=progress)
+    rc = _abi.lib().rtw_render_rows(world.handle, C.byref(cam.derived), rows_per_block, n_shards, shard, spp_begin,
+                                    spp_end, seed, tile.ctypes.data, C.byref(opts))
+    _abi.check(rc, "rtw_render_rows")
+
+
 class ShardedRender:
     """Per-rank state of a row-interleaved render + gather (used by bench.py)."""
 
@@ -123,23 +137,34 @@ class MultiDeviceRender:
         self.handle = h
 
     def render_device(self, cam, spp_begin: int, spp_end: int, d_accum: int, seed: int = 0, stream=None,
-                      fresh: bool = False, sync: bool = True, spp_batch: int = 0) -> None:
+                      fresh: bool = False, sync: bool = True, spp_batch: int = 0, running=None,
+                      progress=None) -> None:
         """Frame float4[W*H] at device pointer d_accum (worlds[0]'s device): rgb += samples
-        [spp_begin, spp_end), w = spp_end (fresh: the range starts from zero)."""
+        [spp_begin, spp_end), w = spp_end (fresh: the range starts from zero).  running (a ctypes
+        c_uint8, 0 = stop) and progress(done, total) -> True are polled between spp batches; a stop
+        raises RtwError(RTW_E_CANCELLED) with the finished batches gathered into the frame."""
         flags = (0 if sync else _abi.RTW_RENDER_NO_SYNC) | (_abi.RTW_RENDER_FRESH if fresh else 0)
-        opts = _abi.RtwRenderOpts(spp_batch, flags, None, None)
+        opts = _abi.render_opts(spp_batch=spp_batch, flags=flags, running=running, progress=progress)
         rc = _abi.lib().rtw_render_multi_device(self.handle, C.byref(cam.derived), self.rpb, spp_begin, spp_end,
                                                 seed, d_accum,
                                                 C.c_void_p(stream.cuda_stream if stream is not None else 0),
                                                 C.byref(opts))
         _abi.check(rc, "rtw_render_multi_device")
 
-    def render_host(self, cam, spp_begin: int, spp_end: int, accum, seed: int = 0) -> None:
-        """Same on a host numpy float32 [W*H, 4] buffer (blocking)."""
+    def render_host(self, cam, spp_begin: int, spp_end: int, accum, seed: int = 0, spp_batch: int = 0,
+                    running=None, progress=None) -> None:
+        """Same on a host numpy float32 [W*H, 4] buffer (blocking, rtw_render_multi_ex)."""
         assert accum.dtype.name == "float32" and accum.flags.c_contiguous and accum.size == cam.size * 4
-        rc = _abi.lib().rtw_render_multi(self.handle, C.byref(cam.derived), self.rpb, spp_begin, spp_end, seed,
-                                         accum.ctypes.data, None)
-        _abi.check(rc, "rtw_render_multi")
+        opts = _abi.render_opts(spp_batch=spp_batch, running=running, progress=progress)
+        rc = _abi.lib().rtw_render_multi_ex(self.handle, C.byref(cam.derived), self.rpb, spp_begin, spp_end, seed,
+                                            accum.ctypes.data, C.byref(opts))
+        _abi.check(rc, "rtw_render_multi_ex")
+
+    def info(self) -> Tuple[int, int]:
+        """(devices, ranks of the RCCL communicator as ncclCommCount reports them)."""
+        n, r = C.c_uint32(), C.c_int()
+        _abi.check(_abi.lib().rtw_multi_info(self.handle, C.byref(n), C.byref(r)), "rtw_multi_info")
+        return int(n.value), int(r.value)
 
     def close(self) -> None:
         if getattr(self, "handle", None) and self.handle.value:
