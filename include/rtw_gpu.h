@@ -324,7 +324,8 @@ typedef struct rtw_tuning {
     uint32_t tile_lists;       /* camera rays of static sphere scenes (fused step) test per-8x8-tile candidate lists:
                                   0 = off, 1 = default (lists of <= 32 spheres, 64 for trees of > 4096 nodes),
                                   2..64 = that cap (ABI 4) */
-    uint32_t _pad1;
+    uint32_t hoist;            /* SAH sphere scenes: spheres whose box dwarfs the rest of the scene (a ground
+                                  sphere) are tested first by every walk, ahead of the tree (default 1; ABI 5) */
 } rtw_tuning;
 
 void rtw_tuning_defaults(rtw_tuning* out);
@@ -467,7 +468,8 @@ int rtw_scene_flatten(const rtw_scene_desc* desc, void* nodes_out, uint32_t cap,
 typedef struct rtw_scene_stats {
     uint32_t n_nodes, n_leaves, n_inner, depth;
     uint64_t device_bytes;
-    uint32_t axis_draws, _pad;
+    uint32_t axis_draws;
+    uint32_t n_hoisted;        /* spheres emitted ahead of the tree (rtw_tuning.hoist) */
 } rtw_scene_stats;
 int rtw_scene_stats_get(rtw_ctx* ctx, rtw_scene_stats* out);
 /* Copies the flattened node array (32 B per node) to host. */

@@ -133,7 +133,7 @@ class RtwTuning(C.Structure):
                 ("lds", C.c_uint32), ("fuse", C.c_uint32), ("wf_iters", C.c_uint32), ("mega_shade_min", C.c_uint32),
                 ("mega_waves", C.c_uint32), ("mega_tile_order", C.c_uint32), ("cpu_threads", C.c_uint32),
                 ("wide_walk", C.c_uint32), ("wf_paths", C.c_uint64),
-                ("tile_lists", C.c_uint32), ("_pad1", C.c_uint32)]
+                ("tile_lists", C.c_uint32), ("hoist", C.c_uint32)]
 
 
 def tuning(**fields) -> RtwTuning:
@@ -149,7 +149,7 @@ def tuning(**fields) -> RtwTuning:
 
 class RtwSceneStats(C.Structure):
     _fields_ = [("n_nodes", C.c_uint32), ("n_leaves", C.c_uint32), ("n_inner", C.c_uint32), ("depth", C.c_uint32),
-                ("device_bytes", C.c_uint64), ("axis_draws", C.c_uint32), ("_pad", C.c_uint32)]
+                ("device_bytes", C.c_uint64), ("axis_draws", C.c_uint32), ("n_hoisted", C.c_uint32)]
 
 
 # every symbol include/rtw_gpu.h declares: name -> (restype, argtypes)

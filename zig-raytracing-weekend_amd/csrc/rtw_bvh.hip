@@ -396,8 +396,9 @@ private:
 // first, so front-most geometry shrinks `closest` early in the fixed walk.
 class SahBuilder {
 public:
-    SahBuilder(const rtw_scene_desc& d, const Geometry& g, std::vector<rtw_node>& out, uint32_t max_leaf)
-        : geo_(g), nodes_(out), objs_(g.objects()) {
+    SahBuilder(const rtw_scene_desc& d, const Geometry& g, std::vector<rtw_node>& out, uint32_t max_leaf,
+               bool hoist = false)
+        : geo_(g), nodes_(out), objs_(g.objects()), hoist_(hoist) {
         const size_t n = objs_.size();
         cent_.resize(n);
         for (size_t i = 0; i < n; i++)
@@ -413,21 +414,35 @@ public:
     // component k), children ordered front-to-back along that octant's diagonal,
     // concatenated.  The walk of a ray uses the array of its own octant, so the
     // child nearer along the ray is visited first and shrinks `closest` early.
+    //
+    // Hoisted spheres (hoist_): a sphere whose box dwarfs everything else (Book-1's and the stress
+    // scene's ground, r = 1000) sits at the top of any tree, where rays of different octants test
+    // it at different steps of their walks -- every such test a divergent sphere step of its wave.
+    // Such spheres are emitted FIRST in every copy, as leaves with skip = i + 1, followed by the
+    // tree of the other objects: each walk starts at node 0, so every lane of a wave tests them at
+    // the same steps (0 .. h-1), with no box step interleaved, and the stackless format, the walks
+    // and the skip links are unchanged (a "forest" of h leaves and one tree).  Same closest hit:
+    // each ray still tests every hoisted sphere and walks the rest of the scene.
     void build(uint32_t orders) {
         nodes_.clear();
         tree_.clear();
         tree_.reserve(2 * objs_.size());
         depth_ = 0;
-        const int root = build_tree(0, idx_.size(), 1);
-        nodes_.reserve(orders * tree_.size());
+        const size_t h = hoist_ ? select_hoisted() : 0;
+        const int root = build_tree(h, idx_.size(), 1);
+        nodes_.reserve(orders * (tree_.size() + h));
         for (uint32_t o = 0; o < orders; o++) {
             float dir[3];
             for (int k = 0; k < 3; k++) dir[k] = orders == 1 ? dir_[k] : ((o >> k) & 1 ? -1.0f : 1.0f);
             base_ = (uint32_t)nodes_.size();
+            for (size_t k = 0; k < h; k++)
+                nodes_.push_back(geo_.leaf(objs_[idx_[k]], (uint32_t)nodes_.size() + 1 - base_));
             emit_tree(root, dir);
         }
+        n_hoisted_ = (uint32_t)h;
     }
     uint32_t depth() const { return depth_; }
+    uint32_t hoisted() const { return n_hoisted_; }
 
 private:
     struct TNode {
@@ -489,6 +504,34 @@ private:
         for (int i = 0; i < 3; i++) { o.a[i] = n.box.mn[i]; o.b[i] = n.box.mx[i]; }
         std::memcpy(&o.a[3], &skip, 4);
         o.b[3] = 0.0f;
+    }
+
+    // Moves the hoisted spheres to idx_[0, h): repeatedly the sphere with the largest box, while its box
+    // area exceeds 4x that of the union of all remaining objects' boxes (at most 4; a tree must remain).
+    size_t select_hoisted() {
+        size_t h = 0;
+        while (h < 4 && idx_.size() - h > 2) {
+            size_t best = idx_.size();
+            float best_a = -1.0f;
+            for (size_t i = h; i < idx_.size(); i++) {
+                const Obj& o = objs_[idx_[i]];
+                if (o.kind != RTW_OBJ_SPHERE) continue;
+                const float a = area(o.box);
+                if (a > best_a) { best_a = a; best = i; }
+            }
+            if (best == idx_.size()) break;
+            bool any = false;
+            Box rest{};
+            for (size_t i = h; i < idx_.size(); i++) {
+                if (i == best) continue;
+                rest = any ? box_union(rest, objs_[idx_[i]].box) : objs_[idx_[i]].box;
+                any = true;
+            }
+            if (!(best_a > 4.0f * area(rest))) break;
+            std::swap(idx_[h], idx_[best]);
+            h++;
+        }
+        return h;
     }
 
     static float area(const Box& b) {
@@ -571,20 +614,24 @@ private:
     uint32_t depth_ = 0;
     size_t max_leaf_ = 1;  // objects per leaf run
     float ci_ = 2.0f;      // cost of one leaf test relative to one box test
+    bool hoist_ = false;   // emit dominant spheres first, ahead of the tree (build)
+    uint32_t n_hoisted_ = 0;
 };
 
 }  // namespace
 
 int rtw_build_bvh(const rtw_scene_desc& desc, std::vector<rtw_node>& nodes, rtw_geometry& geom,
                   uint32_t* depth, uint32_t* axis_draws, float* box_pad, float* extent, uint32_t orders,
-                  uint32_t sah_max_leaf) {
+                  uint32_t sah_max_leaf, uint32_t hoist, uint32_t* n_hoisted) {
     if (box_pad) *box_pad = 0;
     if (extent) *extent = 0;
+    if (n_hoisted) *n_hoisted = 0;
     Geometry geo(desc, geom);
     if (int rc = geo.build()) return rc;
     if (desc.bvh_mode == RTW_BVH_SAH) {
-        SahBuilder b(desc, geo, nodes, sah_max_leaf);
+        SahBuilder b(desc, geo, nodes, sah_max_leaf, hoist != 0);
         b.build(orders);
+        if (n_hoisted) *n_hoisted = b.hoisted();
         if (depth) *depth = b.depth();
         if (axis_draws) *axis_draws = 0;
         // Pad the inner boxes for the FMA slab test: its t error for a plane P and
@@ -723,17 +770,60 @@ bool rtw_wide2_nodes(const std::vector<rtw_node>& nodes, uint32_t n_per, std::ve
         std::memcpy(&w, &nodes[i].a[3], 4);
         return w;
     };
-    if (n_per < 3 || nodes.size() < n_per || (word(0) & RTW_LEAF_BIT)) return false;
+    // a forest: h hoisted leaves (SahBuilder::build) ahead of the tree's root at node h.  Record k < h is
+    // a virtual inner node: slot 0 the hoisted sphere k, slot 1 record k + 1 (or the tree's root), whose
+    // box encloses everything after it -- the walk tests the hoisted spheres first, as the pre-order does.
+    uint32_t h = 0;
+    while (h < n_per && (word(h) & RTW_LEAF_BIT)) h++;
+    if (n_per < h + 3 || nodes.size() < n_per) return false;
     std::vector<uint32_t> widx(n_per, 0), depth(n_per, 0);
-    uint32_t n_inner = 0;
-    for (uint32_t i = 0; i < n_per; i++)
+    uint32_t n_inner = h;
+    for (uint32_t i = h; i < n_per; i++)
         if (!(word(i) & RTW_LEAF_BIT)) widx[i] = n_inner++;
     out.assign(2 * (size_t)n_inner, rtw_cnode{});
     leaf_id.assign(2 * (size_t)n_inner, 0u);
-    depth[0] = 1;
-    uint32_t dmax = 1;
+    auto sphere_slot = [&](uint32_t j, size_t slot) {
+        const rtw_node& n = nodes[j];
+        uint32_t mv;
+        std::memcpy(&mv, &n.b[3], 4);
+        const float rr = n.b[0] * n.b[0];
+        uint32_t rb;
+        std::memcpy(&rb, &rr, 4);
+        if (mv || !(rr >= 0) || !std::isfinite(rr) || (rb & RTW_LEAF_BIT)) return false;
+        std::memcpy(&out[slot].v[0], &n.a[0], 12);
+        out[slot].v[3] = rb | RTW_LEAF_BIT;
+        leaf_id[slot] = j;
+        return true;
+    };
+    auto box_slot = [&](const float* mn, const float* mx, uint32_t rec, size_t slot) {
+        for (int a = 0; a < 3; a++) {
+            if (!(std::fabs(mn[a]) <= 60000.0f) || !(std::fabs(mx[a]) <= 60000.0f)) return false;
+            out[slot].v[a] = (uint32_t)h_down(mn[a]) | ((uint32_t)h_up(mx[a]) << 16);
+        }
+        out[slot].v[3] = rec;
+        return true;
+    };
+    {   // the virtual records, from the last (its slot 1 is the tree's root) to the first
+        float mn[3], mx[3];
+        for (int a = 0; a < 3; a++) {
+            mn[a] = nodes[h].a[a];
+            mx[a] = nodes[h].b[a];
+        }
+        for (uint32_t k = h; k-- > 0;) {
+            if (!sphere_slot(k, 2 * (size_t)k) || !box_slot(mn, mx, k + 1 < h ? k + 1 : widx[h], 2 * (size_t)k + 1))
+                return false;
+            const float r = std::fabs(nodes[k].b[0]), pad = 1e-3f * (r + 1.0f);
+            for (int a = 0; a < 3; a++) {  // + sphere k: the box of record k's subtree, for record k - 1
+                mn[a] = std::min(mn[a], nodes[k].a[a] - r - pad);
+                mx[a] = std::max(mx[a], nodes[k].a[a] + r + pad);
+            }
+            depth[k] = k + 1;
+        }
+    }
+    depth[h] = h + 1;
+    uint32_t dmax = h + 1;
     auto next = [&](uint32_t j) { return (word(j) & RTW_LEAF_BIT) ? j + 1 : (word(j) & RTW_SKIP_MASK); };
-    for (uint32_t i = 0; i < n_per; i++) {
+    for (uint32_t i = h; i < n_per; i++) {
         if (word(i) & RTW_LEAF_BIT) continue;
         const uint32_t c[2] = {i + 1, next(i + 1)};
         if (c[1] >= n_per || next(c[1]) != (word(i) & RTW_SKIP_MASK)) return false;  // not a binary tree
@@ -742,23 +832,12 @@ bool rtw_wide2_nodes(const std::vector<rtw_node>& nodes, uint32_t n_per, std::ve
             const rtw_node& n = nodes[j];
             const size_t slot = 2 * (size_t)widx[i] + k;
             rtw_cnode& o = out[slot];
+            (void)o;
             if (word(j) & RTW_LEAF_BIT) {
-                uint32_t mv;
-                std::memcpy(&mv, &n.b[3], 4);
-                const float rr = n.b[0] * n.b[0];
-                uint32_t rb;
-                std::memcpy(&rb, &rr, 4);
-                if (mv || !(rr >= 0) || !std::isfinite(rr) || (rb & RTW_LEAF_BIT)) return false;
-                std::memcpy(&o.v[0], &n.a[0], 12);
-                o.v[3] = rb | RTW_LEAF_BIT;
-                leaf_id[slot] = j;
+                if (!sphere_slot(j, slot)) return false;
                 continue;
             }
-            for (int a = 0; a < 3; a++) {  // padded by rtw_build_bvh
-                if (!(std::fabs(n.a[a]) <= 60000.0f) || !(std::fabs(n.b[a]) <= 60000.0f)) return false;
-                o.v[a] = (uint32_t)h_down(n.a[a]) | ((uint32_t)h_up(n.b[a]) << 16);
-            }
-            o.v[3] = widx[j];
+            if (!box_slot(n.a, n.b, widx[j], slot)) return false;  // padded by rtw_build_bvh
             depth[j] = depth[i] + 1;
             dmax = std::max(dmax, depth[j]);
         }

@@ -316,6 +316,21 @@ struct Counters {
     uint32_t rays = 0, nodes = 0, leaves = 0, nans = 0, tail_rays = 0;
 };
 
+#if defined(RTW_DIAG_WALK) && defined(__HIP_DEVICE_COMPILE__)
+// Diagnostic build only (make diag -> build/rtw_diag.so; tools/diag_walk.py): how the wave steps of the
+// compact walk split into box / sphere-test / exact-root work.  w*: wave steps (counted once per wave by
+// the lowest active lane), l*: lane steps.  Summed per launch into rtw_diag_walk (rtw_wavefront.hip).
+struct WalkDiag {
+    uint32_t wsteps = 0, wleaf = 0, wexact = 0, lsteps = 0, lleaf = 0, lexact = 0, lexact_hit = 0, walks = 0;
+};
+#define RTW_DG_PARAM , WalkDiag* dg = nullptr
+#define RTW_DG_ARG(x) , x
+__device__ __forceinline__ bool dg_leader() { return __lane_id() == (uint32_t)__builtin_ctzll(__ballot(1)); }
+#else
+#define RTW_DG_PARAM
+#define RTW_DG_ARG(x)
+#endif
+
 // Per-ray constants of the traversal.
 struct RayTrav {
     f3 inv;      // 1 / d per axis (aabb.zig:87); fast box: clamped hardware reciprocal
@@ -543,7 +558,7 @@ RTW_DHD void load_node(const float4* __restrict__ nodes, uint32_t i, float4& A, 
 // Sphere.hit (objects.zig:116-136) of a sphere at `center` with rr = radius * radius
 // (the reference's product, evaluated by the caller or on the host) on (0.001, closest).
 RTW_DHD void sphere_leaf(const rtw_launch& L, const Ray& r, const RayTrav& rt, f3 center, float rr,
-                                            uint32_t i, float& closest, int& hit) {
+                                            uint32_t i, float& closest, int& hit RTW_DG_PARAM) {
     const f3 oc = r.o - center;
     const float half_b = dot(oc, r.d);
     const float c = length_squared(oc) - rr;
@@ -562,20 +577,43 @@ RTW_DHD void sphere_leaf(const rtw_launch& L, const Ray& r, const RayTrav& rt, f
     // miscompiled by hipcc 7.2 (numerator left undefined on the guard-false edge).
     {
         // The exact roots satisfy r1 <= r2 (a > 0), so one of them lies in (tmin, closest)
-        // only if r2 > tmin and r1 < closest: with |r - q| <= e, only if q2 + e > tmin and
-        // q1 - e < closest (a necessary condition; non-short-circuit & and |, no branches).
+        // only if r2 > tmin and r1 < closest: with |r - q| <= e, only if q2 + e2 > tmin and
+        // q1 - e1 < closest (a necessary condition; non-short-circuit & and |, no branches).
+        // Error of an estimated root, u = 2^-24: the reference's r = fl(fl(-hb -+ sq) / a) with sq
+        // the correctly rounded sqrt; the estimate q = fl(fl(-hb -+ sa) * rcp_a) with sa and rcp_a
+        // within 1 ulp (<= 2u relative) of sqrt(disc) and 1/a.  |sa - sq| <= 3.01u sa, so the
+        // numerators m, n differ by <= 3.02u sa + 2.01u |m|, and with the roundings of the
+        // division, the product and rcp_a: |q - r| <= (3.04u sa + 6.03u |m|) rcp_a
+        // < 6.1u (sa + |m|) rcp_a.  e = 2^-20 (sa + |m|) rcp_a is 2.6x that, which also covers
+        // the roundings of e itself; under the guard the quantities are normal (an underflowed
+        // e or q errs by <= 2^-149 absolute, far below the float gaps at kTmin and at closest
+        // >= kTmin).  r2 > kTmin means r2 >= nextafter(kTmin), so fl(q2 + e2) > kTmin, and
+        // likewise for r1 < closest.  Bounding each root by its own numerator keeps e2 tight
+        // where -hb + sa cancels -- the near-zero root of a ray leaving a large sphere's surface
+        // (the ground): a shared bound (|hb| + sa) * 2^-18 left those undecided (exact path).
         sa = RTW_SQRT_EST(disc);
-        const float e = (__builtin_fabsf(half_b) + sa) * rt.rcp_a * 3.8146973e-06f;
-        const float q1 = (-half_b - sa) * rt.rcp_a;
-        const float q2 = (-half_b + sa) * rt.rcp_a;
+        const float m1 = -half_b - sa, m2 = -half_b + sa;
+        const float q1 = m1 * rt.rcp_a, q2 = m2 * rt.rcp_a;
+        const float re = rt.rcp_a * 9.5367432e-07f;  // 2^-20 (a power of two: exact)
+        const float e1 = (sa + __builtin_fabsf(m1)) * re, e2 = (sa + __builtin_fabsf(m2)) * re;
         const bool guard = L.fast_reject & (rt.rcp_a != 0.0f) & (disc > 1e-30f) & (disc < 1e30f) &
                            (__builtin_fabsf(half_b) < 1e15f);
-        const bool plausible = (q2 + e > kTmin) & (q1 - e < closest);
+        const bool plausible = (q2 + e2 > kTmin) & (q1 - e1 < closest);
         exact = exact & (plausible | !guard);
         // under the guard |-hb -+ sq| < 2^51 and disc >= 2^-96; with a in [2^-40, 2^40] the
         // divisions are unscaled except for quotients below 2^-80, which kTmin rejects
         // either way
         quick = guard & (rt.ya != 0.0f) & (disc >= 0x1p-96f);
+    }
+#endif
+#if defined(RTW_DIAG_WALK) && defined(__HIP_DEVICE_COMPILE__)
+    const float closest_in = closest;
+    if (dg) {
+        const uint64_t m = __ballot(exact);
+        if (dg_leader()) {
+            dg->wexact += m ? 1u : 0u;
+            dg->lexact += (uint32_t)__popcll(m);
+        }
     }
 #endif
     if (exact) {
@@ -599,6 +637,9 @@ RTW_DHD void sphere_leaf(const rtw_launch& L, const Ray& r, const RayTrav& rt, f
             hit = (int)i;
         }
     }
+#if defined(RTW_DIAG_WALK) && defined(__HIP_DEVICE_COMPILE__)
+    if (dg && closest != closest_in) dg->lexact_hit++;
+#endif
 }
 
 template <uint32_t FEAT>
@@ -698,6 +739,26 @@ RTW_DHD int hit_with_order(int hit, uint32_t oct) {
 RTW_DHD float h_lo(uint32_t w) { return (float)__builtin_bit_cast(_Float16, (unsigned short)(w & 0xFFFFu)); }
 RTW_DHD float h_hi(uint32_t w) { return (float)__builtin_bit_cast(_Float16, (unsigned short)(w >> 16)); }
 
+#if defined(RTW_DIAG_WALK)
+__device__ unsigned long long rtw_diag_walk[8];
+#endif
+#if defined(RTW_DIAG_WALK) && defined(__HIP_DEVICE_COMPILE__)
+// sum the lanes' diag counters (the lanes that walked) and add them to rtw_diag_walk
+__device__ __forceinline__ void rtw_diag_flush(const WalkDiag& d) {
+    uint32_t v[8] = {d.wsteps, d.wleaf, d.wexact, d.lsteps, d.lleaf, d.lexact, d.lexact_hit, d.walks};
+    const uint64_t act = __ballot(1);
+    const bool lead = dg_leader();
+    for (int k = 0; k < 8; k++) {
+        uint32_t x = v[k];
+        for (int o = 32; o > 0; o >>= 1) {
+            const uint32_t y = __shfl_xor(x, o);
+            x += (act >> (__lane_id() ^ o)) & 1ull ? y : 0u;
+        }
+        if (lead && x) atomicAdd(&rtw_diag_walk[k], (unsigned long long)x);
+    }
+}
+#endif
+
 // `base`: L.cnodes, or their copy in LDS
 template <bool COUNT>
 RTW_DHD int traverse_compact(const rtw_launch& L, const uint4* base, const Ray& r, float& t_out,
@@ -717,12 +778,29 @@ RTW_DHD int traverse_compact(const rtw_launch& L, const uint4* base, const Ray& 
     int hit = -1;
     uint32_t i = 0;
     const uint32_t n = L.n_nodes;
+#if defined(RTW_DIAG_WALK) && defined(__HIP_DEVICE_COMPILE__)
+    WalkDiag dgv;
+    WalkDiag* dg = &dgv;
+    dgv.walks = 1;
+#endif
     while (i < n) {
         const uint4 c = cn[i];
+#if defined(RTW_DIAG_WALK) && defined(__HIP_DEVICE_COMPILE__)
+        {
+            const uint64_t a = __ballot(1), lf = __ballot((c.w & RTW_LEAF_BIT) != 0);
+            if (dg_leader()) {
+                dg->wsteps++;
+                dg->wleaf += lf ? 1u : 0u;
+            }
+            dg->lsteps++;
+            dg->lleaf += (c.w & RTW_LEAF_BIT) ? 1u : 0u;
+            (void)a;
+        }
+#endif
         if (c.w & RTW_LEAF_BIT) {
             if constexpr (COUNT) cnt.leaves++;
             sphere_leaf(L, r, rt, mk(ubits(c.x), ubits(c.y), ubits(c.z)),
-                        ubits(c.w & ~RTW_LEAF_BIT), i, closest, hit);
+                        ubits(c.w & ~RTW_LEAF_BIT), i, closest, hit RTW_DG_ARG(dg));
             i++;
         } else {
             if constexpr (COUNT) cnt.nodes++;
@@ -737,6 +815,9 @@ RTW_DHD int traverse_compact(const rtw_launch& L, const uint4* base, const Ray& 
             i = (hi <= lo) ? c.w : i + 1;
         }
     }
+#if defined(RTW_DIAG_WALK) && defined(__HIP_DEVICE_COMPILE__)
+    rtw_diag_flush(dgv);
+#endif
     t_out = closest;
     return hit_with_order(hit, oct);
 }

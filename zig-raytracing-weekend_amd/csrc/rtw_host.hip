@@ -155,6 +155,7 @@ void rtw_tuning_defaults(rtw_tuning* t) {
     t->cpu_threads = 0;
     t->wide_walk = 1;
     t->tile_lists = 1;
+    t->hoist = 1;
     t->wf_paths = 0;
 }
 
@@ -213,8 +214,9 @@ int rtw_scene_create_ex(const rtw_scene_desc* d, int device, const rtw_tuning* t
     const bool objects = d->n_quads || d->n_instances || d->n_media;
     uint32_t orders = (d->bvh_mode == RTW_BVH_SAH && !objects) ? 8u : 1u;
     if (tu.bvh_orders) orders = (d->bvh_mode == RTW_BVH_SAH && tu.bvh_orders == 8) ? 8u : 1u;
+    uint32_t n_hoisted = 0;
     int rc = rtw_build_bvh(*d, ctx->nodes_host, geom, &depth, &draws, &ctx->box_pad, &ctx->extent, orders,
-                           tu.sah_max_leaf);
+                           tu.sah_max_leaf, tu.hoist && !objects ? 1u : 0u, &n_hoisted);
     if (rc != RTW_OK) {
         delete ctx;
         return fail(rc, "BVH build failed (bad object graph or bvh_mode)");
@@ -436,6 +438,7 @@ int rtw_scene_create_ex(const rtw_scene_desc* d, int device, const rtw_tuning* t
     ctx->stats.depth = depth;
     ctx->stats.device_bytes = off;
     ctx->stats.axis_draws = draws;
+    ctx->stats.n_hoisted = n_hoisted;
     *out = ctx;
     return RTW_OK;
 }

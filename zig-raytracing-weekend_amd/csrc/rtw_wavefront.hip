@@ -1392,3 +1392,15 @@ uint32_t rtw_wavefront_max_waves(int n_cu) {
         m = g > m ? g : m;
     return 4 * m;
 }
+
+#if defined(RTW_DIAG_WALK)
+// diagnostic build only: the compact walk's step counters (rtw_device.h WalkDiag), read and optionally reset
+extern "C" int rtw_debug_walk_counters(uint64_t* out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(rtw_diag_walk), 8 * sizeof(uint64_t)) != hipSuccess) return RTW_E_HIP;
+    if (reset) {
+        const uint64_t z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(rtw_diag_walk), z, sizeof z) != hipSuccess) return RTW_E_HIP;
+    }
+    return RTW_OK;
+}
+#endif
