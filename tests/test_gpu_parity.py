@@ -316,7 +316,7 @@ def test_v1_knobs_invariant(rtw, book1, knob):
                                   {"lds": 127 & ~1}, {"sah_max_leaf": 4}, {"compact_nodes": 0}, {"lds": 127 & ~2},
                                   {"fuse": 0}, {"fuse": 1}, {"lds": 127 & ~4}, {"bvh_orders": 1}, {"tile_lists": 0}, {"tile_lists": 2}, {"tile_lists": 64},
                                   {"lds": 127 & ~2, "wide_walk": 0}, {"fuse": 5}, {"lds": 127 & ~2, "fuse": 5},
-                                  {"lds": 127 & ~2, "fuse": 5, "wide_walk": 0}])
+                                  {"lds": 127 & ~2, "fuse": 5, "wide_walk": 0}, {"hoist": 0}, {"hoist": 0, "fuse": 0}])
 def test_wavefront_knobs_invariant(rtw, book1, knob):
     """Wavefront tuning (rtw_tuning: bounces before the tail kernel, batch size ->
     many batches, FMA vs reference slab test, LDS-staged nodes, SAH leaf runs of up
@@ -324,7 +324,8 @@ def test_wavefront_knobs_invariant(rtw, book1, knob):
     gen+trace+shade kernel vs separate kernels, LDS vs L1/L2 tail, materials in LDS,
     one node ordering instead of 8, camera rays against per-tile candidate lists vs
     the walk, the two-wide stack walk through L1/L2 vs the
-    octant-ordered compact walk, the fused step through L1/L2) never changes a pixel."""
+    octant-ordered compact walk, the fused step through L1/L2, dominant spheres hoisted ahead of the
+    tree or not) never changes a pixel."""
     arr, world = book1
     cam = rtw.book1_camera(image_width=300, aspect_ratio=1.5, spp=5).init()
     ref = render_rows(rtw, world, cam, 0, 200, 0, 5, 4)
@@ -344,14 +345,15 @@ def test_compact_nodes_are_exact(rtw, n, seed):
     arr = rtw.flatten(rtw.worlds.stress_world(n, seed), bvh_mode=rtw._abi.RTW_BVH_SAH)
     cam = rtw.book1_camera(image_width=480, aspect_ratio=16 / 9, spp=4).init()
     outs = []
-    for tu in ({"compact_nodes": 0, "tile_lists": 0}, {"compact_nodes": 1, "wide_walk": 0},
-               {"compact_nodes": 1, "wide_walk": 1}):
+    for tu in ({"compact_nodes": 0, "tile_lists": 0, "hoist": 0}, {"compact_nodes": 1, "wide_walk": 0},
+               {"compact_nodes": 1, "wide_walk": 1}, {"compact_nodes": 1, "wide_walk": 0, "hoist": 0}):
         w = rtw.World(arr, tuning=tu)
         outs.append(render_rows(rtw, w, cam, 0, cam.derived.image_height, 0, 4, 6))
         w.close()
     assert np.isfinite(outs[1]).all()
     assert np.array_equal(outs[0], outs[1])
     assert np.array_equal(outs[0], outs[2])  # the two-wide stack walk (rtw_wide2_nodes): same hits
+    assert np.array_equal(outs[0], outs[3])  # the ground sphere inside the tree (no hoisting)
     # (the defaults also give camera rays the frustum-walked tile lists of large trees: same hits)
 
 
