@@ -675,7 +675,8 @@ int rtw_build_bvh(const rtw_scene_desc& desc, std::vector<rtw_node>& nodes, rtw_
 // array (hit ids and shading keep using it):
 //   inner: x = minx | miny << 16, y = minz | maxx << 16, z = maxy | maxz << 16
 //          (fp16, min rounded down and max up: a superset of the padded box,
-//          read by v_fma_mix_f32 at no conversion cost), w = skip
+//          read by v_fma_mix_f32 at no conversion cost), w = the skip target's byte
+//          offset from the start of the array (all 8 copies)
 //   leaf:  center.xyz (fp32), w = bits(radius * radius) | RTW_LEAF_BIT (the
 //          reference's `radius * radius`, objects.zig:126, evaluated once here
 //          with the same fp32 rounding); a leaf's successor is always i + 1
@@ -743,7 +744,11 @@ bool rtw_compact_nodes(const std::vector<rtw_node>& nodes, uint32_t orders, std:
         c.v[0] = (uint32_t)h[0] | ((uint32_t)h[1] << 16);
         c.v[1] = (uint32_t)h[2] | ((uint32_t)h[3] << 16);
         c.v[2] = (uint32_t)h[4] | ((uint32_t)h[5] << 16);
-        c.v[3] = w;
+        // the skip target as the BYTE offset of its node from the start of the whole array (all copies):
+        // the walk steps through byte addresses, with no index -> address multiply per step
+        const uint64_t skip_bytes = ((uint64_t)oct * per + (w & RTW_SKIP_MASK)) * 16u;
+        if (skip_bytes >= RTW_LEAF_BIT) return false;
+        c.v[3] = (uint32_t)skip_bytes;
     }
     return true;
 }

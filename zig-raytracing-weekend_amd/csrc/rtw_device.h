@@ -760,11 +760,32 @@ __device__ __forceinline__ void rtw_diag_flush(const WalkDiag& d) {
 #endif
 
 // `base`: L.cnodes, or their copy in LDS
-template <bool COUNT>
+// The walk steps through BYTE offsets (rtw_compact_nodes stores an inner node's skip target that
+// way), with no index -> address multiply per step; a sphere's hit id is its byte offset until the
+// walk ends.  LDS: `base` is the LDS stage, whose inner nodes stage_cnodes rebased to absolute LDS
+// addresses, so a step's address IS the offset (ds_read_b128 with no add); else the offsets are
+// from `base` (global memory).
+#if defined(__HIP_DEVICE_COMPILE__)
+typedef __attribute__((address_space(3))) const uint4 lds_uint4;
+#endif
+// the LDS address of a pointer into this block's LDS (device only; the host never walks an LDS stage)
+RTW_DHD uint32_t lds_addr(const void* p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const void*)p;
+#else
+    (void)p;
+    return 0;
+#endif
+}
+template <bool COUNT, bool LDS = false>
 RTW_DHD int traverse_compact(const rtw_launch& L, const uint4* base, const Ray& r, float& t_out,
                                                 Counters& cnt) {
     const uint32_t oct = order_of(L, r);
-    const uint4* __restrict__ cn = base + (size_t)oct * L.n_nodes;
+    const char* __restrict__ cb = reinterpret_cast<const char*>(base);
+    uint32_t a_base = 0;  // LDS: the stage's LDS address
+#if defined(__HIP_DEVICE_COMPILE__)
+    if constexpr (LDS) a_base = lds_addr(base);
+#endif
     // The copy's boxes are stored (near, far) per axis for its octant (rtw_compact_nodes),
     // so min(t0, t1) = t(near) without a min/max pair: fma(P, inv, c) is monotone in P,
     // non-decreasing for inv >= 0.  The sign of inv must then follow the octant, which
@@ -775,16 +796,21 @@ RTW_DHD int traverse_compact(const rtw_launch& L, const uint4* base, const Ray& 
                 (oct & 4u) ? -__builtin_fabsf(rt.inv.z) : __builtin_fabsf(rt.inv.z));
     rt.oinv = mk(-(r.o.x * rt.inv.x), -(r.o.y * rt.inv.y), -(r.o.z * rt.inv.z));
     float closest = kInf;
-    int hit = -1;
-    uint32_t i = 0;
-    const uint32_t n = L.n_nodes;
+    int hit = -1;  // the byte offset of the closest sphere's node
+    const uint32_t a0 = a_base + oct * L.n_nodes * 16u, end = a0 + L.n_nodes * 16u;
+    uint32_t i = a0;
 #if defined(RTW_DIAG_WALK) && defined(__HIP_DEVICE_COMPILE__)
     WalkDiag dgv;
     WalkDiag* dg = &dgv;
     dgv.walks = 1;
 #endif
-    while (i < n) {
-        const uint4 c = cn[i];
+    while (i < end) {
+        uint4 c;
+#if defined(__HIP_DEVICE_COMPILE__)
+        if constexpr (LDS) c = *(lds_uint4*)(uintptr_t)i;
+        else
+#endif
+            c = *reinterpret_cast<const uint4*>(cb + i);
 #if defined(RTW_DIAG_WALK) && defined(__HIP_DEVICE_COMPILE__)
         {
             const uint64_t a = __ballot(1), lf = __ballot((c.w & RTW_LEAF_BIT) != 0);
@@ -801,7 +827,7 @@ RTW_DHD int traverse_compact(const rtw_launch& L, const uint4* base, const Ray& 
             if constexpr (COUNT) cnt.leaves++;
             sphere_leaf(L, r, rt, mk(ubits(c.x), ubits(c.y), ubits(c.z)),
                         ubits(c.w & ~RTW_LEAF_BIT), i, closest, hit RTW_DG_ARG(dg));
-            i++;
+            i += 16u;
         } else {
             if constexpr (COUNT) cnt.nodes++;
             const float tnx = __builtin_fmaf(h_lo(c.x), rt.inv.x, rt.oinv.x);
@@ -812,14 +838,14 @@ RTW_DHD int traverse_compact(const rtw_launch& L, const uint4* base, const Ray& 
             const float tfz = __builtin_fmaf(h_hi(c.z), rt.inv.z, rt.oinv.z);
             const float lo = __builtin_fmaxf(__builtin_fmaxf(kTmin, tnx), __builtin_fmaxf(tny, tnz));
             const float hi = __builtin_fminf(__builtin_fminf(closest, tfx), __builtin_fminf(tfy, tfz));
-            i = (hi <= lo) ? c.w : i + 1;
+            i = (hi <= lo) ? c.w : i + 16u;
         }
     }
 #if defined(RTW_DIAG_WALK) && defined(__HIP_DEVICE_COMPILE__)
     rtw_diag_flush(dgv);
 #endif
     t_out = closest;
-    return hit_with_order(hit, oct);
+    return hit_with_order(hit < 0 ? hit : (int)(((uint32_t)hit - a0) >> 4), oct);
 }
 
 // mkey: the path's RNG state (keys ConstantMedium draws; unused without media).

@@ -178,6 +178,18 @@ __device__ __forceinline__ rtw_launch stage_geom(const rtw_launch& L, float4* ld
     return G;
 }
 
+// every octant copy of the compact nodes into this block's LDS, inner nodes' skip offsets rebased to
+// absolute LDS addresses (traverse_compact<.., true> steps through them as they are)
+__device__ __forceinline__ void stage_clds(const rtw_launch& L, uint4* lds) {
+    const uint32_t n4 = L.n_nodes * L.n_orders, lb = lds_addr(lds);
+    for (uint32_t k = threadIdx.x; k < n4; k += blockDim.x) {
+        uint4 c = L.cnodes[k];
+        if (!(c.w & RTW_LEAF_BIT)) c.w += lb;
+        lds[k] = c;
+    }
+    __syncthreads();
+}
+
 // The two-wide stack walk (rtw_bvh.hip rtw_wide2_nodes: large static sphere SAH trees
 // read through L1/L2).  Each step loads one 32-B record: a leaf child's sphere is
 // tested at once (Sphere.hit on (0.001, closest), objects.zig:116-136, no box:
@@ -579,9 +591,7 @@ __global__ __launch_bounds__(1024) void wf_trace_clds(rtw_launch L, rtw_wf W, ui
     static_assert((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING)) == 0, "static sphere scenes");
     if (blockIdx.x == 0 && threadIdx.x < RTW_WF_STRIPES) W.len[(it + 1u) % 3u][threadIdx.x * RTW_WF_LEN_STRIDE] = 0;
     extern __shared__ uint4 wf_clds[];
-    const uint32_t n4 = L.n_nodes * L.n_orders;
-    for (uint32_t k = threadIdx.x; k < n4; k += blockDim.x) wf_clds[k] = L.cnodes[k];
-    __syncthreads();
+    stage_clds(L, wf_clds);
     const rtw_wf_set& S = W.set[it & 1u];
     Counters cnt;
     for (WfIter e(W, it); e.more(); e.next()) {
@@ -591,8 +601,8 @@ __global__ __launch_bounds__(1024) void wf_trace_clds(rtw_launch L, rtw_wf W, ui
             const Ray r = wf_load_ray(S, slot, depth);
             if (depth) {
                 float t;
-                const int h = L.counters ? traverse_compact<true>(L, wf_clds, r, t, cnt)
-                                         : traverse_compact<false>(L, wf_clds, r, t, cnt);
+                const int h = L.counters ? traverse_compact<true, true>(L, wf_clds, r, t, cnt)
+                                         : traverse_compact<false, true>(L, wf_clds, r, t, cnt);
                 W.hit[slot] = make_float2(t, __int_as_float(h));
                 cnt.rays++;
             }
@@ -730,7 +740,8 @@ __device__ __forceinline__ void wf_tail_body(const rtw_launch& L, const rtw_wf& 
             float t;
             int hit;
             if constexpr (CLDS)
-                hit = L.counters ? traverse_compact<true>(L, lds, r, t, cnt) : traverse_compact<false>(L, lds, r, t, cnt);
+                hit = L.counters ? traverse_compact<true, true>(L, lds, r, t, cnt)
+                                 : traverse_compact<false, true>(L, lds, r, t, cnt);
             else
                 hit = nodes ? traverse<FEAT, false>(nodes, L, r, t, cnt, rng.s)  // the LDS stage
                             : wf_traverse_global<FEAT>(L, r, t, cnt, rng.s);
@@ -833,12 +844,6 @@ __global__ __launch_bounds__(256) void wf_tail_lds(rtw_launch L, rtw_wf W, uint3
     wf_tail_body<FEAT, false>(L, W, it, nullptr, wf_tail_nodes);
 }
 
-// every octant copy of the compact nodes into this block's LDS
-__device__ __forceinline__ void stage_clds(const rtw_launch& L, uint4* lds) {
-    const uint32_t n4 = L.n_nodes * L.n_orders;
-    for (uint32_t k = threadIdx.x; k < n4; k += blockDim.x) lds[k] = L.cnodes[k];
-    __syncthreads();
-}
 
 template <uint32_t FEAT>
 __global__ __launch_bounds__(1024) void wf_tail_clds(rtw_launch L, rtw_wf W, uint32_t it) {
@@ -859,7 +864,7 @@ __device__ __forceinline__ int wf_walk(const rtw_launch& L, const void* lds, con
                                        uint64_t mkey) {
     if constexpr (WALK == WALK_CLDS) {
         const uint4* cn = static_cast<const uint4*>(lds);
-        return L.counters ? traverse_compact<true>(L, cn, r, t, cnt) : traverse_compact<false>(L, cn, r, t, cnt);
+        return L.counters ? traverse_compact<true, true>(L, cn, r, t, cnt) : traverse_compact<false, true>(L, cn, r, t, cnt);
     } else if constexpr (WALK == WALK_LDS) {
         return traverse<FEAT, false>(static_cast<const float4*>(lds), L, r, t, cnt, mkey);  // the LDS stage
     } else {
