@@ -559,9 +559,22 @@ RTW_DHD void load_node(const float4* __restrict__ nodes, uint32_t i, float4& A, 
 // (the reference's product, evaluated by the caller or on the host) on (0.001, closest).
 RTW_DHD void sphere_leaf(const rtw_launch& L, const Ray& r, const RayTrav& rt, f3 center, float rr,
                                             uint32_t i, float& closest, int& hit RTW_DG_PARAM) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    // oc = o - center, dot(oc, d) and lengthSquared(oc) (objects.zig:123-126) with the x and y lanes as
+    // packed pairs: the same IEEE operations per component in the same order (x + y first, then + z),
+    // and the node's center.xy arrives as an aligned register pair (no moves before v_pk_add_f32)
+    typedef float f2v __attribute__((ext_vector_type(2)));
+    const f2v oxy = {r.o.x, r.o.y}, cxy = {center.x, center.y}, dxy = {r.d.x, r.d.y};
+    const f2v ocxy = oxy - cxy;
+    const float ocz = r.o.z - center.z;
+    const f2v p = ocxy * dxy, q = ocxy * ocxy;
+    const float half_b = (p.x + p.y) + ocz * r.d.z;
+    const float c = ((q.x + q.y) + ocz * ocz) - rr;
+#else
     const f3 oc = r.o - center;
     const float half_b = dot(oc, r.d);
     const float c = length_squared(oc) - rr;
+#endif
     const float disc = half_b * half_b - rt.a * c;
     bool exact = disc >= 0;
     bool quick = false;  // the exact roots by sqrt_refined / div_shared (operands in range)
