@@ -63,12 +63,26 @@ def main():
         if e["active_inst_valu"] > 0:
             e["lane_util"] = e["thread_cycles_valu"] / (64.0 * e["active_inst_valu"])
             e["lane_ops"] = e["insts_valu"] * 64.0 * e["lane_util"]
+        # every launch of the timed step in launch order (the fused step: one per wavefront iteration)
+        e["per_launch"] = [{"insts_valu": c.get("insts_valu", 0.0), "gui_active": c.get("gui_active", 0.0),
+                            "lane_util": (c.get("thread_cycles_valu", 0.0) / (64.0 * c["active_inst_valu"])
+                                          if c.get("active_inst_valu") else None),
+                            # GRBM_GUI_ACTIVE is summed over the 8 XCDs: per-XCD clocks x 1024 SIMDs
+                            "valu_busy": (c.get("active_inst_valu", 0.0) * 4.0 / (1024.0 * c["gui_active"] / 8.0)
+                                          if c.get("gui_active") else None)} for c, _ in keep]
         out[k] = e
     json.dump(out, open(os.path.join(d, "pmc_valu.json"), "w"), indent=1, sort_keys=True)
     for k, e in sorted(out.items(), key=lambda kv: -kv[1]["insts_valu"]):
         print(f"{k:10s} launches/step {e['launches']:3d}  VALU insts {e['insts_valu']:.4g}  "
               f"lane_util {e.get('lane_util', 0):.3f}  lane-ops {e.get('lane_ops', 0):.4g}  "
               f"GUI_ACTIVE {e['gui_active']:.4g}  ({', '.join(e['kernels'])})")
+        if e["launches"] > 1:
+            for j, pl in enumerate(e["per_launch"]):
+                lu = pl["lane_util"]
+                vb = pl["valu_busy"]
+                print(f"    launch {j}: VALU insts {pl['insts_valu']:.4g}  lane_util "
+                      f"{lu if lu is None else round(lu, 3)}  VALU busy (x4 / 1024 SIMD / per-XCD GUI_ACTIVE) "
+                      f"{vb if vb is None else round(vb, 3)}  GUI_ACTIVE {pl['gui_active']:.4g}")
 
 
 if __name__ == "__main__":
