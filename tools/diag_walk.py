@@ -37,19 +37,22 @@ def main():
     cam.samples_per_pixel = spp
     cam.init()
     acc = torch.zeros((cam.size, 4), dtype=torch.float32, device="cuda")
-    out = (C.c_uint64 * 8)()
+    out = (C.c_uint64 * 16)()
     fn(out, 1)
     rc = L.rtw_render_device(world.handle, C.byref(cam.derived), 0, cam.size, 0, spp, 0, acc.data_ptr(), None, None)
     pkg._abi.check(rc, "rtw_render_device")
     torch.cuda.synchronize()
     fn(out, 1)
-    ws, wl, we, ls, ll, le, leh, walks = list(out)
+    ws, wl, we, ls, ll, le, leh, walks = list(out)[:8]
+    lw, lc, lwalk, lex = list(out)[8:12]
     res = {"config": cfg_name, "spp": spp, "walks": walks, "wave_steps": ws, "lane_steps": ls,
            "lane_util_walk": ls / max(1, 64 * ws), "steps_per_walk": ls / max(1, walks),
            "leaf_share_of_wave_steps": wl / max(1, ws), "exact_share_of_wave_steps": we / max(1, ws),
            "leaf_share_of_lane_steps": ll / max(1, ls), "exact_lanes_per_walk": le / max(1, walks),
            "exact_lanes_that_hit": leh / max(1, le), "lanes_per_exact_step": le / max(1, we),
-           "lanes_per_leaf_step": ll / max(1, wl)}
+           "lanes_per_leaf_step": ll / max(1, wl),
+           "list_waves": lw, "list_waves_over_cap": lwalk, "list_candidates_per_wave": lc / max(1, lw),
+           "list_exact_candidates_per_wave": lex / max(1, lw)}
     print(json.dumps(res))
     world.close()
 

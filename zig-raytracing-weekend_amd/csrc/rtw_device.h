@@ -753,7 +753,9 @@ RTW_DHD float h_lo(uint32_t w) { return (float)__builtin_bit_cast(_Float16, (uns
 RTW_DHD float h_hi(uint32_t w) { return (float)__builtin_bit_cast(_Float16, (unsigned short)(w >> 16)); }
 
 #if defined(RTW_DIAG_WALK)
-__device__ unsigned long long rtw_diag_walk[8];
+// [0..7] the compact walk (WalkDiag); [8] camera-ray list waves, [9] list candidates tested (per wave),
+// [10] list waves over the cap (they walk), [11] list candidates tested with the exact path (per wave)
+__device__ unsigned long long rtw_diag_walk[16];
 #endif
 #if defined(RTW_DIAG_WALK) && defined(__HIP_DEVICE_COMPILE__)
 // sum the lanes' diag counters (the lanes that walked) and add them to rtw_diag_walk

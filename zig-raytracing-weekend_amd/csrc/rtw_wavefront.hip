@@ -501,17 +501,37 @@ __device__ __forceinline__ bool wf_tile_hit(const rtw_launch& L, const rtw_wf& W
                                             float& t_out, Counters& cnt) {
     tile = __builtin_amdgcn_readfirstlane(tile);
     const uint32_t n = W.tl_count[tile];
+#if defined(RTW_DIAG_WALK) && defined(__HIP_DEVICE_COMPILE__)
+    const bool dlead = dg_leader();
+    if (dlead) atomicAdd(&rtw_diag_walk[n == RTW_TL_WALK ? 10 : 8], 1ull);
+#endif
     if (n == RTW_TL_WALK) return false;
     const RayTrav rt = ray_trav(r, true);
     const uint4* __restrict__ e = W.tl + 2u * (size_t)tile * RTW_TL_MAX;
     float closest = kInf;
     hit = -1;
+#if defined(RTW_DIAG_WALK) && defined(__HIP_DEVICE_COMPILE__)
+    uint32_t tested = 0, exact = 0;
+#endif
     for (uint32_t k = 0; k < n; k++) {
         const uint4 a = e[2u * k], b = e[2u * k + 1u];
         if (!__ballot(!(closest < ubits(b.y)))) break;  // every lane's hit is nearer than the rest can be
         if constexpr (COUNT) cnt.leaves++;
+#if defined(RTW_DIAG_WALK) && defined(__HIP_DEVICE_COMPILE__)
+        WalkDiag dgl;
+        sphere_leaf(L, r, rt, mk(ubits(a.x), ubits(a.y), ubits(a.z)), ubits(a.w), b.x, closest, hit, &dgl);
+        tested++;
+        exact += __ballot(dgl.lexact != 0) ? 1u : 0u;
+#else
         sphere_leaf(L, r, rt, mk(ubits(a.x), ubits(a.y), ubits(a.z)), ubits(a.w), b.x, closest, hit);
+#endif
     }
+#if defined(RTW_DIAG_WALK) && defined(__HIP_DEVICE_COMPILE__)
+    if (dlead) {
+        atomicAdd(&rtw_diag_walk[9], (unsigned long long)tested);
+        atomicAdd(&rtw_diag_walk[11], (unsigned long long)exact);
+    }
+#endif
     t_out = closest;
     return true;
 }
@@ -1401,9 +1421,9 @@ uint32_t rtw_wavefront_max_waves(int n_cu) {
 #if defined(RTW_DIAG_WALK)
 // diagnostic build only: the compact walk's step counters (rtw_device.h WalkDiag), read and optionally reset
 extern "C" int rtw_debug_walk_counters(uint64_t* out, int reset) {
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(rtw_diag_walk), 8 * sizeof(uint64_t)) != hipSuccess) return RTW_E_HIP;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(rtw_diag_walk), 16 * sizeof(uint64_t)) != hipSuccess) return RTW_E_HIP;
     if (reset) {
-        const uint64_t z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        const uint64_t z[16] = {0};
         if (hipMemcpyToSymbol(HIP_SYMBOL(rtw_diag_walk), z, sizeof z) != hipSuccess) return RTW_E_HIP;
     }
     return RTW_OK;
