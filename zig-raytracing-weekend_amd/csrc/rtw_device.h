@@ -314,6 +314,9 @@ RTW_DHD float sqrt_refined(float x, float s /* v_sqrt_f32(x) */) {
 
 struct Counters {
     uint32_t rays = 0, nodes = 0, leaves = 0, nans = 0, tail_rays = 0;
+#if defined(RTW_DIAG_WALK)
+    uint32_t dsteps = 0, dleaves = 0;  // diagnostic build: steps / sphere tests of this lane's last compact walk
+#endif
 };
 
 #if defined(RTW_DIAG_WALK) && defined(__HIP_DEVICE_COMPILE__)
@@ -857,6 +860,8 @@ RTW_DHD int traverse_compact(const rtw_launch& L, const uint4* base, const Ray& 
         }
     }
 #if defined(RTW_DIAG_WALK) && defined(__HIP_DEVICE_COMPILE__)
+    cnt.dsteps = dgv.lsteps;
+    cnt.dleaves = dgv.lleaf;
     rtw_diag_flush(dgv);
 #endif
     t_out = closest;

@@ -25,6 +25,14 @@
 
 namespace {
 
+#if defined(RTW_DIAG_WALK)
+// diagnostic build: per-slot record of the compact walks of one wavefront iteration (tools/diag_sort.py):
+// rec[2 slot] = (steps | sphere tests << 16, bits(d.xyz)), rec[2 slot + 1] = (bits(o.xyz), 1)
+__device__ uint4* rtw_diag_rec;
+__device__ uint32_t rtw_diag_rec_cap;
+__device__ uint32_t rtw_diag_rec_it;
+#endif
+
 // logical pixel q of the batch -> image pixel / output slot (false = padding)
 __device__ __forceinline__ bool wf_pixel(const rtw_launch& L, const rtw_wf& W, uint32_t q, uint32_t& pixel,
                                          uint32_t& out_idx, uint32_t& x, uint32_t& y) {
@@ -961,6 +969,13 @@ __device__ __forceinline__ void wf_step_body(const rtw_launch& L, const rtw_wf& 
                     }
                 }
                 if (!listed) hit = wf_walk<FEAT, WALK>(L, lds, r, t, cnt, rng.s);
+#if defined(RTW_DIAG_WALK) && defined(__HIP_DEVICE_COMPILE__)
+                if (!listed && it == rtw_diag_rec_it && rtw_diag_rec && slot < rtw_diag_rec_cap) {
+                    rtw_diag_rec[2u * slot] = make_uint4(cnt.dsteps | (cnt.dleaves << 16), fbits(r.d.x), fbits(r.d.y),
+                                                         fbits(r.d.z));
+                    rtw_diag_rec[2u * slot + 1u] = make_uint4(fbits(r.o.x), fbits(r.o.y), fbits(r.o.z), 1u);
+                }
+#endif
                 cnt.rays++;
                 if (hit < 0) {
                     acc = acc + thr * background(L, r);
@@ -1419,6 +1434,14 @@ uint32_t rtw_wavefront_max_waves(int n_cu) {
 }
 
 #if defined(RTW_DIAG_WALK)
+// diagnostic build only: where the per-slot walk records of iteration `it` go (null: off)
+extern "C" int rtw_debug_walk_records(void* d_rec, uint32_t cap_slots, uint32_t it) {
+    uint4* p = static_cast<uint4*>(d_rec);
+    if (hipMemcpyToSymbol(HIP_SYMBOL(rtw_diag_rec), &p, sizeof p) != hipSuccess) return RTW_E_HIP;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(rtw_diag_rec_cap), &cap_slots, 4) != hipSuccess) return RTW_E_HIP;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(rtw_diag_rec_it), &it, 4) != hipSuccess) return RTW_E_HIP;
+    return RTW_OK;
+}
 // diagnostic build only: the compact walk's step counters (rtw_device.h WalkDiag), read and optionally reset
 extern "C" int rtw_debug_walk_counters(uint64_t* out, int reset) {
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(rtw_diag_walk), 16 * sizeof(uint64_t)) != hipSuccess) return RTW_E_HIP;
