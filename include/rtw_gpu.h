@@ -326,6 +326,10 @@ typedef struct rtw_tuning {
                                   2..64 = that cap (ABI 4) */
     uint32_t hoist;            /* SAH sphere scenes: spheres whose box dwarfs the rest of the scene (a ground
                                   sphere) are tested first by every walk, ahead of the tree (default 1; ABI 5) */
+    uint32_t sort_iters;       /* wavefront iterations 0 .. sort_iters-1 file their survivors into 64-slot blocks
+                                  by direction, so the next iteration's waves walk coherent rays (default 3;
+                                  0 = plain appends; ABI 5) */
+    uint32_t _pad2;
 } rtw_tuning;
 
 void rtw_tuning_defaults(rtw_tuning* out);

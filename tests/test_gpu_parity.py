@@ -316,7 +316,9 @@ def test_v1_knobs_invariant(rtw, book1, knob):
                                   {"lds": 127 & ~1}, {"sah_max_leaf": 4}, {"compact_nodes": 0}, {"lds": 127 & ~2},
                                   {"fuse": 0}, {"fuse": 1}, {"lds": 127 & ~4}, {"bvh_orders": 1}, {"tile_lists": 0}, {"tile_lists": 2}, {"tile_lists": 64},
                                   {"lds": 127 & ~2, "wide_walk": 0}, {"fuse": 5}, {"lds": 127 & ~2, "fuse": 5},
-                                  {"lds": 127 & ~2, "fuse": 5, "wide_walk": 0}, {"hoist": 0}, {"hoist": 0, "fuse": 0}])
+                                  {"lds": 127 & ~2, "fuse": 5, "wide_walk": 0}, {"hoist": 0}, {"hoist": 0, "fuse": 0},
+                                  {"sort_iters": 0}, {"sort_iters": 50}, {"sort_iters": 50, "fuse": 0},
+                                  {"sort_iters": 2, "wf_iters": 1}])
 def test_wavefront_knobs_invariant(rtw, book1, knob):
     """Wavefront tuning (rtw_tuning: bounces before the tail kernel, batch size ->
     many batches, FMA vs reference slab test, LDS-staged nodes, SAH leaf runs of up
@@ -325,7 +327,7 @@ def test_wavefront_knobs_invariant(rtw, book1, knob):
     one node ordering instead of 8, camera rays against per-tile candidate lists vs
     the walk, the two-wide stack walk through L1/L2 vs the
     octant-ordered compact walk, the fused step through L1/L2, dominant spheres hoisted ahead of the
-    tree or not) never changes a pixel."""
+    tree or not, survivors filed into direction-bucketed blocks or appended) never changes a pixel."""
     arr, world = book1
     cam = rtw.book1_camera(image_width=300, aspect_ratio=1.5, spp=5).init()
     ref = render_rows(rtw, world, cam, 0, 200, 0, 5, 4)

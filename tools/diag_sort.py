@@ -56,7 +56,7 @@ def main():
     pkg._abi.check(rc, "rtw_render_device")
     torch.cuda.synchronize()
     pkg._abi.check(L.rtw_debug_walk_records(None, 0, 0xFFFFFFFF), "rtw_debug_walk_records")
-    valid = rec[:, 7] == 1
+    valid = rec[:, 7] != 0
     slot = torch.nonzero(valid).squeeze(1)
     r = rec[slot]
     steps = (r[:, 0] & 0xFFFF).float()
@@ -73,6 +73,9 @@ def main():
     dkey = dbin[:, 0] * 64 + dbin[:, 1] * 8 + dbin[:, 2]
     elev = ((dn[:, 1] + 1) * 8).clamp(0, 15.999).long()               # 16 elevation bins
     cell = torch.floor(o).long()                                      # 1-unit origin cells
+    pid = (r[:, 7] - 1).long()
+    n_pix = paths // spp
+    tile = (pid % n_pix) // 64                                        # the camera tile the path started in
     ckey = ((cell[:, 0] + 2048) * 4096 + (cell[:, 1] + 2048)) * 4096 + (cell[:, 2] + 2048)
     keys = {
         "random": torch.randperm(n, device="cuda"),
@@ -83,14 +86,25 @@ def main():
         "origin_cell+octant": ckey * 8 + oct_,
         "origin_cell+direction512": ckey * 512 + dkey,
         "walk_length (bound)": steps.long(),
+        "tile": tile,
+        "tile+octant": tile * 8 + oct_,
+        "tile+direction512": tile * 512 + dkey,
+        "tile+direction64": tile * 64 + (dbin[:, 0] // 2) * 16 + (dbin[:, 1] // 2) * 4 + dbin[:, 2] // 2,
+        "tile4x4+direction512": ((tile // 150) // 4 * 38 + (tile % 150) // 4) * 512 + dkey,
+        "tile+direction16": tile * 16 + oct_ * 2 + (dbin[:, 1] >= 4).long(),
+        "tile+direction32": tile * 32 + oct_ * 4 + (dbin[:, 1] // 2) % 4,
     }
+    if os.environ.get("DIAG_SORT_KEYS"):
+        keep = set(os.environ["DIAG_SORT_KEYS"].split(","))
+        keys = {k: v for k, v in keys.items() if k in keep}
     glob_res, win_res = {}, {}
     for kname, k in keys.items():
-        order = torch.argsort(k * n + seq)           # stable: ties keep the queue order
+        k = torch.unique(k, return_inverse=True)[1]  # dense keys 0..m-1 (no overflow in the window key)
+        order = torch.argsort(k, stable=True)        # stable: ties keep the queue order
         glob_res[kname] = util(steps[order], seq // 64)
         # windowed: sort within consecutive 4096-slot windows of the queue (the round-1 experiment's form)
         wk = (slot // 4096) * (int(k.max().item()) + 1) + k
-        order = torch.argsort(wk * n + seq)
+        order = torch.argsort(wk, stable=True)
         win_res[kname] = util(steps[order], seq // 64)
     out["global_sort"] = glob_res
     out["window4096_sort"] = win_res

@@ -133,7 +133,8 @@ class RtwTuning(C.Structure):
                 ("lds", C.c_uint32), ("fuse", C.c_uint32), ("wf_iters", C.c_uint32), ("mega_shade_min", C.c_uint32),
                 ("mega_waves", C.c_uint32), ("mega_tile_order", C.c_uint32), ("cpu_threads", C.c_uint32),
                 ("wide_walk", C.c_uint32), ("wf_paths", C.c_uint64),
-                ("tile_lists", C.c_uint32), ("hoist", C.c_uint32)]
+                ("tile_lists", C.c_uint32), ("hoist", C.c_uint32), ("sort_iters", C.c_uint32),
+                ("_pad2", C.c_uint32)]
 
 
 def tuning(**fields) -> RtwTuning:

@@ -156,6 +156,7 @@ void rtw_tuning_defaults(rtw_tuning* t) {
     t->wide_walk = 1;
     t->tile_lists = 1;
     t->hoist = 1;
+    t->sort_iters = 3;
     t->wf_paths = 0;
 }
 
@@ -390,6 +391,7 @@ int rtw_scene_create_ex(const rtw_scene_desc* d, int device, const rtw_tuning* t
         ctx->wf_max_paths = tu.wf_paths ? tu.wf_paths : std::max<uint64_t>(cap, 1u << 20);
     }
     ctx->wf_iters = tu.wf_iters;
+    ctx->wf_sort_iters = tu.sort_iters;
     {
         int n_cu = 0;
         if (host || hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
@@ -566,8 +568,11 @@ int run_wavefront(rtw_ctx* ctx, rtw_launch L, hipStream_t stream, rtw_timer* T) 
     // stripe capacity: a stripe receives the survivors of nw/STRIPES waves that
     // each take <= ceil(chunks / nw) 64-path chunks (rtw_wavefront.h)
     const uint64_t max_waves = rtw_wavefront_max_waves(ctx->n_cu);
+    // + direction-bucketed iterations: every wave of a stripe may leave one partly filled 64-slot block per
+    //   bucket (wf_push_bucketed)
+    const uint64_t bucket_blocks = ctx->wf_sort_iters ? (max_waves / RTW_WF_STRIPES + 1) * RTW_WF_BUCKETS : 0;
     auto stripe_cap = [&](uint64_t paths) {
-        return ((paths + 63) / 64 / RTW_WF_STRIPES + 1 + max_waves / RTW_WF_STRIPES) * 64;
+        return ((paths + 63) / 64 / RTW_WF_STRIPES + 1 + max_waves / RTW_WF_STRIPES + bucket_blocks) * 64;
     };
     // slots per set: every path (iteration 0: slot = path id) or every stripe's capacity
     auto slots = [&](uint64_t paths) { return std::max<uint64_t>(paths, stripe_cap(paths) * RTW_WF_STRIPES); };
@@ -614,6 +619,7 @@ int run_wavefront(rtw_ctx* ctx, rtw_launch L, hipStream_t stream, rtw_timer* T) 
     for (int k = 0; k < 3; k++) W.len[k] = reinterpret_cast<uint32_t*>(take(RTW_WF_STRIPES * RTW_WF_LEN_STRIDE * 4));
     W.n_pix = (uint32_t)n_pix;
     W.iters = ctx->wf_iters;
+    W.sort_iters = ctx->wf_sort_iters;
     // camera-ray candidate lists (the compact-LDS fused step of static sphere scenes, rtw_tuning.tile_lists)
     if (L.tile_lists && L.cnodes && L.n_orders == 8) {
         const uint64_t tiles = n_pix / 64;

@@ -212,6 +212,7 @@ struct rtw_ctx {
     uint64_t wf_cap = 0;
     uint64_t wf_max_paths = 1u << 26;  // paths per wavefront batch (x RTW_WF_PATH_BYTES); set at scene creation
     uint32_t wf_iters = 9;         // wavefront bounces before the tail kernel (rtw_tuning.wf_iters)
+    uint32_t wf_sort_iters = 3;    // iterations whose survivors are filed by direction (rtw_tuning.sort_iters)
     uint32_t cpu_threads = 0;      // host context: worker threads (rtw_tuning.cpu_threads; 0 = all)
     int n_cu = 256;                // compute units of the device (wavefront grids)
     std::vector<hipEvent_t> ev_pool;  // recycled timing events

@@ -8,6 +8,9 @@
 #define RTW_WF_MAX_ITERS 100
 #define RTW_WF_STRIPES 256    // output queues (one atomic counter each)
 #define RTW_WF_LEN_STRIDE 16  // counters 64 B apart
+// coherent queues (wf_push_bucketed): a wave keeps one open 64-slot block per direction bucket
+#define RTW_WF_BUCKET_BITS 4
+#define RTW_WF_BUCKETS (1u << RTW_WF_BUCKET_BITS)
 #define RTW_TL_MAX 64          // camera-ray candidate list capacity per 8x8 tile (rtw_tuning.tile_lists caps it)
 #define RTW_TL_WALK 0xFFFFFFFFu
 #define RTW_TL_BYTES (RTW_TL_MAX * 32 + 4)  // per tile
@@ -51,6 +54,7 @@ struct rtw_wf {
     uint32_t n_pix, n_s, n_paths, n_tx;
     uint32_t stripe_cap;
     uint32_t iters;     // wavefront iterations before the tail kernel
+    uint32_t sort_iters;  // iterations it < sort_iters push their survivors into direction-bucketed blocks
 };
 
 // bytes of device state per path (two slot sets + hit + ls)

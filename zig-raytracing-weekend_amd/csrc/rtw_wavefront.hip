@@ -27,7 +27,7 @@ namespace {
 
 #if defined(RTW_DIAG_WALK)
 // diagnostic build: per-slot record of the compact walks of one wavefront iteration (tools/diag_sort.py):
-// rec[2 slot] = (steps | sphere tests << 16, bits(d.xyz)), rec[2 slot + 1] = (bits(o.xyz), 1)
+// rec[2 slot] = (steps | sphere tests << 16, bits(d.xyz)), rec[2 slot + 1] = (bits(o.xyz), path id + 1)
 __device__ uint4* rtw_diag_rec;
 __device__ uint32_t rtw_diag_rec_cap;
 __device__ uint32_t rtw_diag_rec_it;
@@ -50,19 +50,34 @@ __device__ __forceinline__ bool wf_pixel(const rtw_launch& L, const rtw_wf& W, u
 __device__ __forceinline__ uint32_t wf_wave() { return blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); }
 __device__ __forceinline__ uint32_t wf_nwaves() { return gridDim.x * (blockDim.x >> 6); }
 
+// Iteration 0 deals its chunks (64 paths = one 8x8 tile of one sample) in runs of RTW_WF_TILE_RUN
+// consecutive samples of one tile: in tile-major order c = tile * n_s + s_local, run R = c / RUN goes to
+// wave R % nw, so a wave takes RUN chunks of the same tile in a row (the blocks its survivors fill,
+// wf_push_bucketed, then hold rays that left one tile) while the runs, dealt round-robin, keep the waves'
+// shares of sky and ground even.  A wave's k-th chunk: c = ((k / RUN) * nw + w) * RUN + k % RUN, which grows
+// with k (false: past the last chunk).  slot0: the chunk's first path id.
+#define RTW_WF_TILE_RUN 16u
+__device__ __forceinline__ bool wf_chunk0(const rtw_wf& W, uint32_t w, uint32_t nw, uint32_t k, uint32_t& slot0) {
+    const uint32_t c = ((k / RTW_WF_TILE_RUN) * nw + w) * RTW_WF_TILE_RUN + k % RTW_WF_TILE_RUN;
+    if (c >= (W.n_paths >> 6)) return false;
+    const uint32_t t = c / W.n_s, s = c - t * W.n_s;
+    slot0 = (s * (W.n_pix >> 6) + t) << 6;
+    return true;
+}
+
 // The slots of iteration `it` handed to this wave, 64 at a time:
 //   for (WfIter e(W, it); e.more(); e.next()) { uint32_t slot; if (e.get(W, slot)) ... }
 // (wave-uniform loop; get() is per lane)
 struct WfIter {
-    uint32_t it, j, step, n, base, off;
+    uint32_t it, j, step, n, base, off, w, nw, slot0;
+    bool live0;  // iteration 0: chunk j exists
     __device__ WfIter(const rtw_wf& W, uint32_t it_) : it(it_) {
-        const uint32_t w = wf_wave(), nw = wf_nwaves();
+        w = wf_wave();
+        nw = wf_nwaves();
         if (it == 0) {
-            j = w;
-            step = nw;
-            n = (W.n_paths + 63u) >> 6;  // chunks
-            base = W.n_paths;
-            off = 0;
+            j = 0;
+            step = 1;
+            live0 = wf_chunk0(W, w, nw, 0, slot0);
         } else {
             const uint32_t s = w % RTW_WF_STRIPES;
             j = w / RTW_WF_STRIPES;
@@ -71,10 +86,19 @@ struct WfIter {
             n = (base + 63u) >> 6;
             off = s * W.stripe_cap;
         }
+        W_ = &W;
     }
-    __device__ bool more() const { return j < n; }
-    __device__ void next() { j += step; }
-    __device__ bool get(const rtw_wf&, uint32_t& slot) const {
+    const rtw_wf* W_;
+    __device__ bool more() const { return it == 0 ? live0 : j < n; }
+    __device__ void next() {
+        j += step;
+        if (it == 0) live0 = wf_chunk0(*W_, w, nw, j, slot0);
+    }
+    __device__ bool get(const rtw_wf& W, uint32_t& slot) const {
+        if (it == 0) {
+            slot = slot0 | __lane_id();
+            return true;
+        }
         const uint32_t k = (j << 6) | __lane_id();
         slot = off + k;
         return k < base;
@@ -86,10 +110,10 @@ struct WfIter {
 __device__ __forceinline__ bool wf_nth(const rtw_wf& W, uint32_t it, uint32_t m, uint32_t& slot, bool& end) {
     const uint32_t w = wf_wave(), nw = wf_nwaves();
     if (it == 0) {
-        const uint32_t chunk = w + (m >> 6) * nw;
-        slot = (chunk << 6) | (m & 63u);
-        end = chunk >= ((W.n_paths + 63u) >> 6);
-        return slot < W.n_paths;
+        uint32_t slot0 = 0;
+        end = !wf_chunk0(W, w, nw, m >> 6, slot0);
+        slot = slot0 | (m & 63u);
+        return !end;
     }
     const uint32_t s = w % RTW_WF_STRIPES, R = nw / RTW_WF_STRIPES;
     const uint32_t k = ((((m >> 6) * R) + w / RTW_WF_STRIPES) << 6) | (m & 63u);
@@ -111,6 +135,81 @@ __device__ __forceinline__ uint32_t wf_push(const rtw_wf& W, uint32_t it, bool p
     base = __shfl(base, 0);
     const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     return s * W.stripe_cap + base + (uint32_t)__popcll(m & lt);
+}
+
+// Coherent queues (iterations it < W.sort_iters).  A wave files its survivors into 64-slot blocks of its
+// output stripe, one open block per direction bucket (RTW_WF_BUCKETS: the signs of the scattered
+// direction's x and z and four levels of its elevation), so a block -- one chunk of the next iteration --
+// holds rays of similar direction that left the few tiles the wave worked on: the walks of a wave then
+// take similar paths through the tree (tools/diag_sort.py: C2 iteration 1 walk lane utilisation 0.60 as
+// appended, 0.78 tile + direction).  The open blocks live in the lanes: lane b holds
+// bucket b's block (first slot `bb`, slots used `bf`; 64 = none).  Per push: lanes with equal keys by
+// one ballot per key bit; each bucket's lanes take consecutive slots of its block, and buckets whose
+// block overflows take fresh blocks, all of them with one atomic on the stripe counter.  A partly filled
+// block's unused slots are marked dead (depth 0) when the wave's iteration ends (wf_close_blocks).
+__device__ __forceinline__ uint32_t wf_bucket(f3 d) {
+    const float ilen = __builtin_amdgcn_rsqf(d.x * d.x + d.y * d.y + d.z * d.z);  // approximate: a sort key only
+    const float uy = d.y * ilen;
+    const uint32_t qy = (uy > -0.5f ? 1u : 0u) + (uy > 0.0f ? 1u : 0u) + (uy > 0.5f ? 1u : 0u);
+    return (d.x < 0.0f ? 1u : 0u) | (d.z < 0.0f ? 2u : 0u) | (qy << 2);
+}
+
+__device__ __forceinline__ uint32_t wf_push_bucketed(const rtw_wf& W, uint32_t it, bool push, uint32_t key,
+                                                     uint32_t& bb, uint32_t& bf) {
+    const uint64_t act = __ballot(push);
+    if (!act) return 0;
+    const uint32_t lane = __lane_id();
+    key = push ? key : 0u;
+    uint64_t eq = act, eqh = act;  // eq: lanes with my key; eqh: lanes whose key is my lane (holder view)
+#pragma unroll
+    for (uint32_t k = 0; k < RTW_WF_BUCKET_BITS; k++) {
+        const uint64_t m = __ballot(push && ((key >> k) & 1u));
+        eq &= ((key >> k) & 1u) ? m : ~m;
+        eqh &= ((lane >> k) & 1u) ? m : ~m;
+    }
+    if (lane >= RTW_WF_BUCKETS) eqh = 0;
+    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    const uint32_t rank = (uint32_t)__popcll(eq & lt), cnt = (uint32_t)__popcll(eq);
+    const uint32_t leader = (uint32_t)__builtin_ctzll(eq | (1ull << 63));  // push lanes: eq != 0
+    const uint32_t base = __shfl(bb, (int)key), fill = __shfl(bf, (int)key);  // my bucket's open block
+    const uint32_t room = 64u - fill;
+    // buckets whose block cannot take all their lanes get a fresh block (one atomic for the wave)
+    const uint64_t need = __ballot(push && rank == 0 && cnt > room);
+    uint32_t b0 = 0;
+    if (need) {
+        const uint32_t s = wf_wave() % RTW_WF_STRIPES;
+        uint32_t* len = &W.len[(it + 1u) % 3u][s * RTW_WF_LEN_STRIDE];
+        if (lane == 0) b0 = atomicAdd(len, 64u * (uint32_t)__popcll(need));
+        b0 = s * W.stripe_cap + __shfl(b0, 0);
+    }
+    const uint64_t llt = leader >= 63 ? (need & ~(1ull << 63)) : (need & ((1ull << leader) - 1ull));
+    const uint32_t fresh = b0 + 64u * (uint32_t)__popcll(llt);  // my bucket's fresh block, if it took one
+    // holder lanes: the new state of their bucket
+    const uint32_t hc = (uint32_t)__popcll(eqh);
+    if (hc) {
+        const uint32_t hl = (uint32_t)__builtin_ctzll(eqh);
+        const uint64_t hlt = hl == 0 ? 0ull : (need & (~0ull >> (64 - hl)));
+        const uint32_t hroom = 64u - bf;
+        if (hc <= hroom) {
+            bf += hc;
+        } else {
+            bb = b0 + 64u * (uint32_t)__popcll(hlt);
+            bf = hc - hroom;
+        }
+    }
+    return rank < room ? base + fill + rank : fresh + (rank - room);
+}
+
+// the unused slots of the wave's partly filled blocks: dead (depth 0), so the next iteration skips them
+__device__ __forceinline__ void wf_close_blocks(const rtw_wf& W, uint32_t it, uint32_t bb, uint32_t bf) {
+    const rtw_wf_set& O = W.set[(it + 1u) & 1u];
+    uint64_t open = __ballot(__lane_id() < RTW_WF_BUCKETS && bf > 0u && bf < 64u);
+    while (open) {
+        const uint32_t h = (uint32_t)__builtin_ctzll(open);
+        open &= open - 1ull;
+        const uint32_t base = __shfl(bb, (int)h), fill = __shfl(bf, (int)h);
+        if (__lane_id() >= fill) O.ray_d[base + __lane_id()] = make_float4(0, 0, 0, 0);
+    }
 }
 
 __device__ __forceinline__ Ray wf_load_ray(const rtw_wf_set& S, uint32_t slot, uint32_t& depth) {
@@ -662,6 +761,8 @@ template <uint32_t FEAT>
 __device__ __forceinline__ void wf_shade_body(const rtw_launch& L, const rtw_wf& W, uint32_t it) {
     const rtw_wf_set& S = W.set[it & 1u];
     const rtw_wf_set& O = W.set[(it + 1u) & 1u];
+    const bool bucketed = it < W.sort_iters;
+    uint32_t bb = 0, bf = 64;  // lane b: bucket b's open block (wf_push_bucketed)
     for (WfIter e(W, it); e.more(); e.next()) {
         bool push = false;
         uint32_t slot = 0, pid = 0, depth = 0;
@@ -712,7 +813,8 @@ __device__ __forceinline__ void wf_shade_body(const rtw_launch& L, const rtw_wf&
             }
         }
         if (depth && !push) W.ls[pid] = make_float4(acc.x, acc.y, acc.z, 0);
-        const uint32_t out = wf_push(W, it, push);
+        const uint32_t out = bucketed ? wf_push_bucketed(W, it, push, push ? wf_bucket(sc.d) : 0u, bb, bf)
+                                      : wf_push(W, it, push);
         if (push) {
             wf_store_ray(O, out, sc, depth - 1);
             O.thr[out] = make_float4(thr.x, thr.y, thr.z, 0);
@@ -721,6 +823,7 @@ __device__ __forceinline__ void wf_shade_body(const rtw_launch& L, const rtw_wf&
             if constexpr ((FEAT & RTW_F_LIGHT) != 0) O.acc[out] = make_float4(acc.x, acc.y, acc.z, 0);
         }
     }
+    if (bucketed) wf_close_blocks(W, it, bb, bf);
 }
 
 // tail: the paths still queued after the last wavefront iteration, each to
@@ -915,6 +1018,8 @@ __device__ __forceinline__ void wf_step_body(const rtw_launch& L, const rtw_wf& 
     const rtw_wf_set& S = W.set[it & 1u];
     const rtw_wf_set& O = W.set[(it + 1u) & 1u];
     Counters cnt;
+    const bool bucketed = it < W.sort_iters;
+    uint32_t bb = 0, bf = 64;  // lane b: bucket b's open block (wf_push_bucketed)
     for (WfIter e(W, it); e.more(); e.next()) {  // wave-uniform: the body starts converged
         bool live = false, push = false;
         uint32_t slot = 0, pid = 0, depth = 0;
@@ -973,7 +1078,7 @@ __device__ __forceinline__ void wf_step_body(const rtw_launch& L, const rtw_wf& 
                 if (!listed && it == rtw_diag_rec_it && rtw_diag_rec && slot < rtw_diag_rec_cap) {
                     rtw_diag_rec[2u * slot] = make_uint4(cnt.dsteps | (cnt.dleaves << 16), fbits(r.d.x), fbits(r.d.y),
                                                          fbits(r.d.z));
-                    rtw_diag_rec[2u * slot + 1u] = make_uint4(fbits(r.o.x), fbits(r.o.y), fbits(r.o.z), 1u);
+                    rtw_diag_rec[2u * slot + 1u] = make_uint4(fbits(r.o.x), fbits(r.o.y), fbits(r.o.z), pid + 1u);
                 }
 #endif
                 cnt.rays++;
@@ -1014,7 +1119,8 @@ __device__ __forceinline__ void wf_step_body(const rtw_launch& L, const rtw_wf& 
             }
         }
         if (live && !push) W.ls[pid] = make_float4(acc.x, acc.y, acc.z, 0);
-        const uint32_t out = wf_push(W, it, push);
+        const uint32_t out = bucketed ? wf_push_bucketed(W, it, push, push ? wf_bucket(sc.d) : 0u, bb, bf)
+                                      : wf_push(W, it, push);
         if (push) {
             wf_store_ray(O, out, sc, depth - 1);
             O.thr[out] = make_float4(thr.x, thr.y, thr.z, 0);
@@ -1023,6 +1129,7 @@ __device__ __forceinline__ void wf_step_body(const rtw_launch& L, const rtw_wf& 
             if constexpr ((FEAT & RTW_F_LIGHT) != 0) O.acc[out] = make_float4(acc.x, acc.y, acc.z, 0);
         }
     }
+    if (bucketed) wf_close_blocks(W, it, bb, bf);
     flush_counters(L, cnt, 0);
 }
 
