@@ -326,9 +326,13 @@ typedef struct rtw_tuning {
                                   2..64 = that cap (ABI 4) */
     uint32_t hoist;            /* SAH sphere scenes: spheres whose box dwarfs the rest of the scene (a ground
                                   sphere) are tested first by every walk, ahead of the tree (default 1; ABI 5) */
-    uint32_t sort_iters;       /* wavefront iterations 0 .. sort_iters-1 file their survivors into 64-slot blocks
-                                  by direction, so the next iteration's waves walk coherent rays (default 3;
-                                  0 = plain appends; ABI 5) */
+    uint32_t sort_iters;       /* fused step (trees staged in LDS): wavefront iterations 0 .. sort_iters-1 file
+                                  their survivors into 64-slot blocks by direction, so the next iteration's
+                                  waves walk coherent rays (default 3; 0 = plain appends; ABI 5) */
+    uint32_t sort_bits;        /* direction-bucket key bits of those blocks: 0..4 (default 4 = 16 buckets: x, z signs,
+                                  4 elevation levels; 0 = one block per wave, appends in order; ABI 5) */
+    uint32_t sort_iters_split; /* the same for the split trace / shade kernels (trees through L1/L2: C4), whose
+                                  HBM-bound shade pays more for the scattered block stores (default 1; ABI 5) */
     uint32_t _pad2;
 } rtw_tuning;
 

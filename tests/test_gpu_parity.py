@@ -317,8 +317,8 @@ def test_v1_knobs_invariant(rtw, book1, knob):
                                   {"fuse": 0}, {"fuse": 1}, {"lds": 127 & ~4}, {"bvh_orders": 1}, {"tile_lists": 0}, {"tile_lists": 2}, {"tile_lists": 64},
                                   {"lds": 127 & ~2, "wide_walk": 0}, {"fuse": 5}, {"lds": 127 & ~2, "fuse": 5},
                                   {"lds": 127 & ~2, "fuse": 5, "wide_walk": 0}, {"hoist": 0}, {"hoist": 0, "fuse": 0},
-                                  {"sort_iters": 0}, {"sort_iters": 50}, {"sort_iters": 50, "fuse": 0},
-                                  {"sort_iters": 2, "wf_iters": 1}])
+                                  {"sort_iters": 0}, {"sort_iters": 50}, {"sort_iters_split": 50, "fuse": 0}, {"sort_iters_split": 0, "fuse": 0},
+                                  {"sort_iters": 2, "wf_iters": 1}, {"sort_bits": 0}, {"sort_bits": 2, "fuse": 0}])
 def test_wavefront_knobs_invariant(rtw, book1, knob):
     """Wavefront tuning (rtw_tuning: bounces before the tail kernel, batch size ->
     many batches, FMA vs reference slab test, LDS-staged nodes, SAH leaf runs of up

@@ -74,8 +74,7 @@ def main():
     elev = ((dn[:, 1] + 1) * 8).clamp(0, 15.999).long()               # 16 elevation bins
     cell = torch.floor(o).long()                                      # 1-unit origin cells
     pid = (r[:, 7] - 1).long()
-    n_pix = paths // spp
-    tile = (pid % n_pix) // 64                                        # the camera tile the path started in
+    tile = (pid // 64) // spp                                         # the camera tile (tile-major path ids)
     ckey = ((cell[:, 0] + 2048) * 4096 + (cell[:, 1] + 2048)) * 4096 + (cell[:, 2] + 2048)
     keys = {
         "random": torch.randperm(n, device="cuda"),

@@ -134,7 +134,8 @@ class RtwTuning(C.Structure):
                 ("mega_waves", C.c_uint32), ("mega_tile_order", C.c_uint32), ("cpu_threads", C.c_uint32),
                 ("wide_walk", C.c_uint32), ("wf_paths", C.c_uint64),
                 ("tile_lists", C.c_uint32), ("hoist", C.c_uint32), ("sort_iters", C.c_uint32),
-                ("_pad2", C.c_uint32)]
+                ("sort_bits", C.c_uint32),
+                ("sort_iters_split", C.c_uint32), ("_pad2", C.c_uint32)]
 
 
 def tuning(**fields) -> RtwTuning:

@@ -157,6 +157,8 @@ void rtw_tuning_defaults(rtw_tuning* t) {
     t->tile_lists = 1;
     t->hoist = 1;
     t->sort_iters = 3;
+    t->sort_bits = RTW_WF_BUCKET_BITS;
+    t->sort_iters_split = 1;  // C4: 1 -> 2577, 3 -> 2518, 0 -> 2523 Msamples/s
     t->wf_paths = 0;
 }
 
@@ -172,6 +174,7 @@ int rtw_scene_create_ex(const rtw_scene_desc* d, int device, const rtw_tuning* t
     if (tu.kernel > RTW_KERNEL_SIMPLE) return fail(RTW_E_INVALID, "tuning.kernel out of range");
     if (tu.bvh_orders != 0 && tu.bvh_orders != 1 && tu.bvh_orders != 8) return fail(RTW_E_INVALID, "tuning.bvh_orders must be 0, 1 or 8");
     if (tu.wf_iters < 1 || tu.wf_iters > RTW_WF_MAX_ITERS) return fail(RTW_E_INVALID, "tuning.wf_iters out of range");
+    if (tu.sort_bits > RTW_WF_BUCKET_BITS) return fail(RTW_E_INVALID, "tuning.sort_bits out of range");
     if (tu.mega_shade_min < 1 || tu.mega_shade_min > 64) return fail(RTW_E_INVALID, "tuning.mega_shade_min out of range");
     if (tu.mega_waves != 1 && tu.mega_waves != 6 && tu.mega_waves != 8) return fail(RTW_E_INVALID, "tuning.mega_waves must be 1, 6 or 8");
     if (tu.wf_paths && tu.wf_paths < 4096) return fail(RTW_E_INVALID, "tuning.wf_paths must be 0 or >= 4096");
@@ -392,6 +395,8 @@ int rtw_scene_create_ex(const rtw_scene_desc* d, int device, const rtw_tuning* t
     }
     ctx->wf_iters = tu.wf_iters;
     ctx->wf_sort_iters = tu.sort_iters;
+    ctx->wf_sort_iters_split = tu.sort_iters_split;
+    ctx->wf_sort_mask = (1u << tu.sort_bits) - 1u;
     {
         int n_cu = 0;
         if (host || hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
@@ -570,7 +575,7 @@ int run_wavefront(rtw_ctx* ctx, rtw_launch L, hipStream_t stream, rtw_timer* T) 
     const uint64_t max_waves = rtw_wavefront_max_waves(ctx->n_cu);
     // + direction-bucketed iterations: every wave of a stripe may leave one partly filled 64-slot block per
     //   bucket (wf_push_bucketed)
-    const uint64_t bucket_blocks = ctx->wf_sort_iters ? (max_waves / RTW_WF_STRIPES + 1) * RTW_WF_BUCKETS : 0;
+    const uint64_t bucket_blocks = (ctx->wf_sort_iters || ctx->wf_sort_iters_split) ? (max_waves / RTW_WF_STRIPES + 1) * RTW_WF_BUCKETS : 0;
     auto stripe_cap = [&](uint64_t paths) {
         return ((paths + 63) / 64 / RTW_WF_STRIPES + 1 + max_waves / RTW_WF_STRIPES + bucket_blocks) * 64;
     };
@@ -620,6 +625,8 @@ int run_wavefront(rtw_ctx* ctx, rtw_launch L, hipStream_t stream, rtw_timer* T) 
     W.n_pix = (uint32_t)n_pix;
     W.iters = ctx->wf_iters;
     W.sort_iters = ctx->wf_sort_iters;
+    W.sort_iters_split = ctx->wf_sort_iters_split;
+    W.sort_mask = ctx->wf_sort_mask;
     // camera-ray candidate lists (the compact-LDS fused step of static sphere scenes, rtw_tuning.tile_lists)
     if (L.tile_lists && L.cnodes && L.n_orders == 8) {
         const uint64_t tiles = n_pix / 64;

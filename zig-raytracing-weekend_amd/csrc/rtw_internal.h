@@ -212,6 +212,8 @@ struct rtw_ctx {
     uint64_t wf_cap = 0;
     uint64_t wf_max_paths = 1u << 26;  // paths per wavefront batch (x RTW_WF_PATH_BYTES); set at scene creation
     uint32_t wf_iters = 9;         // wavefront bounces before the tail kernel (rtw_tuning.wf_iters)
+    uint32_t wf_sort_mask = 15;    // their bucket key bits (rtw_tuning.sort_bits)
+    uint32_t wf_sort_iters_split = 1;  // the same for the split kernels (rtw_tuning.sort_iters_split)
     uint32_t wf_sort_iters = 3;    // iterations whose survivors are filed by direction (rtw_tuning.sort_iters)
     uint32_t cpu_threads = 0;      // host context: worker threads (rtw_tuning.cpu_threads; 0 = all)
     int n_cu = 256;                // compute units of the device (wavefront grids)

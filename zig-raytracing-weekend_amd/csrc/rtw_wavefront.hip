@@ -6,21 +6,23 @@
 // the same walk in a ~40-VGPR kernel runs 4-6x more node steps per second.
 // v2 therefore splits a batch of paths into kernels over HBM-resident SoA state:
 //
-//   gen    (pixel, sample) -> camera ray           Camera.getRay  camera.zig:169-180
+//   camera (pixel, sample) -> camera ray           Camera.getRay  camera.zig:169-180
+//          (in registers, by iteration 0's kernels: wf_camera)
 //   trace  ray -> closest hit (t, leaf)            BVHNode.hit    bvh.zig:122-136
 //   shade  hit -> emission/background, scatter     rayColor       camera.zig:182-208
 //          (survivors appended to the next queue)
 //   tail   the few paths still alive after RTW_WF_ITERS bounces, to completion
 //   reduce per pixel: accum += sample radiances in sample order (camera.zig:55-56)
 //
-// A batch holds n_pix logical pixels x n_s samples; path p = s_local * n_pix + q,
-// q in 8x8 pixel tiles so a wave's primary rays are one tile.  Every path runs
+// A batch holds n_pix logical pixels x n_s samples, q in 8x8 pixel tiles so a wave's
+// primary rays are one tile; path ids are tile-major (wf_path).  Every path runs
 // the same operations in the same order as in v0/v1 (same RNG stream, same
 // iterative radiance), and the reduce adds the samples of a pixel in sample
 // order onto the accumulator, so v2 is bit-identical to v0/v1.
 #include "rtw_device.h"
 #include "rtw_wavefront.h"
 
+#include <algorithm>
 #include <cstdlib>
 
 namespace {
@@ -60,9 +62,18 @@ __device__ __forceinline__ uint32_t wf_nwaves() { return gridDim.x * (blockDim.x
 __device__ __forceinline__ bool wf_chunk0(const rtw_wf& W, uint32_t w, uint32_t nw, uint32_t k, uint32_t& slot0) {
     const uint32_t c = ((k / RTW_WF_TILE_RUN) * nw + w) * RTW_WF_TILE_RUN + k % RTW_WF_TILE_RUN;
     if (c >= (W.n_paths >> 6)) return false;
-    const uint32_t t = c / W.n_s, s = c - t * W.n_s;
-    slot0 = (s * (W.n_pix >> 6) + t) << 6;
+    slot0 = c << 6;
     return true;
+}
+
+// Path ids are tile-major: path p is sample s_local of pixel q (in tile order) with
+// p = ((q / 64) * n_s + s_local) * 64 + q % 64, so chunk c = p / 64 is sample c % n_s of tile c / n_s and
+// the paths of one tile-run (wf_chunk0) are RUN consecutive chunks: the radiance stores of a block's rays
+// (W.ls[pid], pids of one run) stay within 16 KB, and the reduce reads 64 consecutive pixels per sample.
+__device__ __forceinline__ void wf_path(const rtw_wf& W, uint32_t p, uint32_t& s_local, uint32_t& q) {
+    const uint32_t c = p >> 6, t = c / W.n_s;
+    s_local = c - t * W.n_s;
+    q = (t << 6) | (p & 63u);
 }
 
 // The slots of iteration `it` handed to this wave, 64 at a time:
@@ -251,24 +262,44 @@ __device__ __forceinline__ void wf_load_state(const rtw_launch& L, const rtw_wf_
     }
 }
 
+// Iteration 0: path `slot`'s camera ray and RNG state (camera.zig:169-180 with the +1 pixel offset,
+// camera.zig:100-101), generated in registers by the kernel that needs them -- the fused step, and both
+// the split trace and the split shade (each recomputes it: no ray or RNG state goes through HBM before
+// the first bounce).  Called by the whole wave (sphere scenes: get_ray_wave's one disk rejection loop).
+// false: padding, or depth 0 (rayColor = 0).
 template <uint32_t FEAT>
-__global__ __launch_bounds__(256) void wf_gen(rtw_launch L, rtw_wf W) {
-    const uint32_t p = blockIdx.x * 256u + threadIdx.x;
-    if (p >= W.n_paths) return;
-    const uint32_t s_local = p / W.n_pix, q = p - s_local * W.n_pix;
-    uint32_t pixel, out_idx, x, y;
-    const rtw_wf_set& S = W.set[0];  // iteration 0: slot = path id
-    if (wf_pixel(L, W, q, pixel, out_idx, x, y) && L.max_depth > 0) {
-        const uint32_t s = L.s0 + s_local;
-        rtw_rng rng;
-        rng.s = rtw_mix64(L.key0 ^ (((uint64_t)pixel << 32) | (uint64_t)s));
-        const Ray r = get_ray(L, x + L.pixel_offset, y + L.pixel_offset, rng);  // camera.zig:100-101
-        wf_store_ray(S, p, r, L.max_depth);
-        S.rng[p] = rng.s;
-    } else {
-        S.ray_d[p] = make_float4(0, 0, 0, 0);  // depth 0: no path (padding / outside the range)
-        W.ls[p] = make_float4(0, 0, 0, 0);     // rayColor(r, 0) = 0
+__device__ __forceinline__ bool wf_camera(const rtw_launch& L, const rtw_wf& W, bool got, uint32_t slot, Ray& r,
+                                          rtw_rng& rng) {
+    uint32_t s_local = 0, q = 0, pixel = 0, out_idx, x = 0, y = 0;
+    bool live = false;
+    if (got) {
+        wf_path(W, slot, s_local, q);
+        live = wf_pixel(L, W, q, pixel, out_idx, x, y) && L.max_depth > 0;
     }
+    rng.s = live ? rtw_mix64(L.key0 ^ (((uint64_t)pixel << 32) | (uint64_t)(L.s0 + s_local))) : 0ull;
+    r.o = r.d = mk(0, 0, 0);
+    r.time = 0;
+    if constexpr ((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM)) == 0) {
+        r = get_ray_wave(L, live, x + L.pixel_offset, y + L.pixel_offset, rng);
+    } else {
+        if (live) r = get_ray(L, x + L.pixel_offset, y + L.pixel_offset, rng);
+    }
+    return live;
+}
+
+// a split kernel's input ray: the camera ray in iteration 0's instantiation (CAM, wf_camera: kept
+// out of the later iterations' kernels, whose walk would pay for its registers), else the input set's;
+// depth 0 = no path.  rng: the camera ray's RNG state (CAM).
+template <uint32_t FEAT, bool CAM>
+__device__ __forceinline__ Ray wf_input_ray(const rtw_launch& L, const rtw_wf& W, const rtw_wf_set& S,
+                                            uint32_t slot, uint32_t& depth, rtw_rng& rng) {
+    if constexpr (CAM) {
+        Ray r;
+        depth = wf_camera<FEAT>(L, W, true, slot, r, rng) ? L.max_depth : 0u;
+        return r;
+    }
+    rng.s = 0;
+    return wf_load_ray(S, slot, depth);
 }
 
 // L.geom_lds: copy the scene's quads | members | instances (one contiguous range of the scene
@@ -644,7 +675,7 @@ __device__ __forceinline__ bool wf_tile_hit(const rtw_launch& L, const rtw_wf& W
 }
 
 // trace: closest hit per ray of the input set (no shading state in registers)
-template <uint32_t FEAT, bool LDS>
+template <uint32_t FEAT, bool LDS, bool CAM = false>
 __global__ __launch_bounds__(256) void wf_trace(rtw_launch L, rtw_wf W, uint32_t it) {
     // the stripes shade(it) appends to start empty (they were iteration it-1's input)
     if (blockIdx.x == 0) W.len[(it + 1u) % 3u][threadIdx.x * RTW_WF_LEN_STRIDE] = 0;
@@ -661,10 +692,11 @@ __global__ __launch_bounds__(256) void wf_trace(rtw_launch L, rtw_wf W, uint32_t
                 uint32_t slot;
                 if (e.get(W, slot)) {
                     uint32_t depth;
-                    const Ray r = wf_load_ray(S, slot, depth);
+                    rtw_rng rng;
+                    const Ray r = wf_input_ray<FEAT, CAM>(G, W, S, slot, depth, rng);
                     if (depth) {
                         float t;
-                        const int h = traverse<FEAT>(wf_lds_nodes, G, r, t, cnt, wf_mkey<FEAT>(S, slot));
+                        const int h = traverse<FEAT>(wf_lds_nodes, G, r, t, cnt, CAM ? rng.s : wf_mkey<FEAT>(S, slot));
                         W.hit[slot] = make_float2(t, __int_as_float(h));
                         cnt.rays++;
                     }
@@ -689,19 +721,20 @@ __global__ __launch_bounds__(256) void wf_trace(rtw_launch L, rtw_wf W, uint32_t
         uint32_t slot;
         if (e.get(W, slot)) {
             uint32_t depth;
-            const Ray r = wf_load_ray(S, slot, depth);
+            rtw_rng rng;
+            const Ray r = wf_input_ray<FEAT, CAM>(L, W, S, slot, depth, rng);
             if (depth) {
                 float t = kInf;
                 int h = -1;
                 bool listed = false;
                 if constexpr ((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING)) == 0) {
                     if (it == 0 && W.tl_count) {  // camera rays (slot = path id): the tile's candidate list
-                        const uint32_t tile = (slot - (slot / W.n_pix) * W.n_pix) >> 6;
+                        const uint32_t tile = (slot >> 6) / W.n_s;
                         listed = L.counters ? wf_tile_hit<true>(L, W, tile, r, h, t, cnt)
                                             : wf_tile_hit<false>(L, W, tile, r, h, t, cnt);
                     }
                 }
-                if (!listed) h = wf_traverse_global<FEAT>(L, r, t, cnt, wf_mkey<FEAT>(S, slot));
+                if (!listed) h = wf_traverse_global<FEAT>(L, r, t, cnt, CAM ? rng.s : wf_mkey<FEAT>(S, slot));
                 W.hit[slot] = make_float2(t, __int_as_float(h));
                 cnt.rays++;
             }
@@ -713,7 +746,7 @@ __global__ __launch_bounds__(256) void wf_trace(rtw_launch L, rtw_wf W, uint32_t
 // trace over the compact nodes staged in LDS (all octant copies of a small tree,
 // e.g. BASELINE config 2: 8 x 969 x 16 B = 124 KB): 1024-thread blocks share one
 // copy (one block per CU), ds_read_b128 instead of vector-memory gathers
-template <uint32_t FEAT>
+template <uint32_t FEAT, bool CAM = false>
 __global__ __launch_bounds__(1024) void wf_trace_clds(rtw_launch L, rtw_wf W, uint32_t it) {
     static_assert((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING)) == 0, "static sphere scenes");
     if (blockIdx.x == 0 && threadIdx.x < RTW_WF_STRIPES) W.len[(it + 1u) % 3u][threadIdx.x * RTW_WF_LEN_STRIDE] = 0;
@@ -725,7 +758,8 @@ __global__ __launch_bounds__(1024) void wf_trace_clds(rtw_launch L, rtw_wf W, ui
         uint32_t slot;
         if (e.get(W, slot)) {
             uint32_t depth;
-            const Ray r = wf_load_ray(S, slot, depth);
+            rtw_rng rng;
+            const Ray r = wf_input_ray<FEAT, CAM>(L, W, S, slot, depth, rng);
             if (depth) {
                 float t;
                 const int h = L.counters ? traverse_compact<true, true>(L, wf_clds, r, t, cnt)
@@ -740,24 +774,24 @@ __global__ __launch_bounds__(1024) void wf_trace_clds(rtw_launch L, rtw_wf W, ui
 
 // shade: emission / background and Material.scatter; a surviving path's state
 // moves to its slot in the other set; an ending path stores its radiance by id
-template <uint32_t FEAT>
+template <uint32_t FEAT, bool CAM>
 __device__ __forceinline__ void wf_shade_body(const rtw_launch& L, const rtw_wf& W, uint32_t it);
 
-template <uint32_t FEAT>
+template <uint32_t FEAT, bool CAM = false>
 __global__ __launch_bounds__(256) void wf_shade(rtw_launch L, rtw_wf W, uint32_t it) {
     if constexpr ((FEAT & RTW_F_GEOM) != 0) {
         if (L.geom_lds) {  // quads / members / instances in LDS (hit records of object scenes)
             extern __shared__ float4 wf_shade_geom[];
             const rtw_launch G = stage_geom(L, wf_shade_geom);
             __syncthreads();
-            wf_shade_body<FEAT>(G, W, it);
+            wf_shade_body<FEAT, CAM>(G, W, it);
             return;
         }
     }
-    wf_shade_body<FEAT>(L, W, it);
+    wf_shade_body<FEAT, CAM>(L, W, it);
 }
 
-template <uint32_t FEAT>
+template <uint32_t FEAT, bool CAM>
 __device__ __forceinline__ void wf_shade_body(const rtw_launch& L, const rtw_wf& W, uint32_t it) {
     const rtw_wf_set& S = W.set[it & 1u];
     const rtw_wf_set& O = W.set[(it + 1u) & 1u];
@@ -773,16 +807,16 @@ __device__ __forceinline__ void wf_shade_body(const rtw_launch& L, const rtw_wf&
         HitPrep hp;
         bool hitp = false, need_uv = false;
         if (e.get(W, slot)) {
-            const Ray r = wf_load_ray(S, slot, depth);
+            const Ray r = wf_input_ray<FEAT, CAM>(L, W, S, slot, depth, rng);
             if (depth) {
-                pid = it == 0 ? slot : S.pid[slot];
+                pid = CAM ? slot : S.pid[slot];
                 const float2 h = W.hit[slot];
                 const int hit = __float_as_int(h.y);
                 wf_load_state<FEAT>(L, S, slot, depth, thr, acc);
                 if (hit < 0) {
                     acc = acc + thr * background(L, r);
                 } else {
-                    rng.s = S.rng[slot];
+                    if (!CAM) rng.s = S.rng[slot];
                     if constexpr ((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM)) == 0) {
                         // sphere scenes: the split form of the fused step (hit record, then one
                         // randomUnitVector rejection loop for the wave, then the material)
@@ -813,7 +847,8 @@ __device__ __forceinline__ void wf_shade_body(const rtw_launch& L, const rtw_wf&
             }
         }
         if (depth && !push) W.ls[pid] = make_float4(acc.x, acc.y, acc.z, 0);
-        const uint32_t out = bucketed ? wf_push_bucketed(W, it, push, push ? wf_bucket(sc.d) : 0u, bb, bf)
+        if (CAM && !depth) W.ls[slot] = make_float4(0, 0, 0, 0);  // padding, rayColor(r, 0) = 0
+        const uint32_t out = bucketed ? wf_push_bucketed(W, it, push, push ? wf_bucket(sc.d) & W.sort_mask : 0u, bb, bf)
                                       : wf_push(W, it, push);
         if (push) {
             wf_store_ray(O, out, sc, depth - 1);
@@ -1004,7 +1039,7 @@ __device__ __forceinline__ int wf_walk(const rtw_launch& L, const void* lds, con
 }
 
 // One fused wavefront iteration: iteration 0 generates the camera ray of path
-// p = slot in registers (wf_gen), every iteration walks the tree (wf_trace) and
+// p = slot in registers (wf_camera), every iteration walks the tree (wf_trace) and
 // shades (wf_shade) in the same kernel, appending the survivors to the next set.
 // The ray never round-trips through HBM between trace and shade (no hit records:
 // 48 B/ray less traffic, no gen pass), and the state streams of one wave overlap
@@ -1030,20 +1065,10 @@ __device__ __forceinline__ void wf_step_body(const rtw_launch& L, const rtw_wf& 
         rng.s = 0;
         f3 thr = mk(1, 1, 1), acc = mk(0, 0, 0);
         const bool got = e.get(W, slot);
-        if (it == 0) {  // wf_gen: camera.zig:169-180 with the +1 pixel offset (camera.zig:100-101)
-            uint32_t pixel = 0, out_idx, x = 0, y = 0;
-            if (got) {
-                pid = slot;
-                const uint32_t s_local = slot / W.n_pix, q = slot - s_local * W.n_pix;
-                live = wf_pixel(L, W, q, pixel, out_idx, x, y) && L.max_depth > 0;
-                if (live) rng.s = rtw_mix64(L.key0 ^ (((uint64_t)pixel << 32) | (uint64_t)(L.s0 + s_local)));
-                else W.ls[slot] = make_float4(0, 0, 0, 0);  // rayColor(r, 0) = 0
-            }
-            if constexpr ((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM)) == 0) {
-                r = get_ray_wave(L, live, x + L.pixel_offset, y + L.pixel_offset, rng);
-            } else {
-                if (live) r = get_ray(L, x + L.pixel_offset, y + L.pixel_offset, rng);
-            }
+        if (it == 0) {  // the camera ray in registers (wf_camera)
+            pid = slot;
+            live = wf_camera<FEAT>(L, W, got, slot, r, rng);
+            if (got && !live) W.ls[slot] = make_float4(0, 0, 0, 0);  // rayColor(r, 0) = 0
             depth = live ? L.max_depth : 0;
         } else if (got) {
             r = wf_load_ray(S, slot, depth);
@@ -1068,7 +1093,7 @@ __device__ __forceinline__ void wf_step_body(const rtw_launch& L, const rtw_wf& 
                 if constexpr (WALK != WALK_GLOBAL && (FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING)) == 0) {
                     // camera rays: the tile's candidate list
                     if (it == 0 && W.tl_count) {
-                        const uint32_t tile = (slot - (slot / W.n_pix) * W.n_pix) >> 6;
+                        const uint32_t tile = (slot >> 6) / W.n_s;
                         listed = L.counters ? wf_tile_hit<true>(L, W, tile, r, hit, t, cnt)
                                             : wf_tile_hit<false>(L, W, tile, r, hit, t, cnt);
                     }
@@ -1119,7 +1144,7 @@ __device__ __forceinline__ void wf_step_body(const rtw_launch& L, const rtw_wf& 
             }
         }
         if (live && !push) W.ls[pid] = make_float4(acc.x, acc.y, acc.z, 0);
-        const uint32_t out = bucketed ? wf_push_bucketed(W, it, push, push ? wf_bucket(sc.d) : 0u, bb, bf)
+        const uint32_t out = bucketed ? wf_push_bucketed(W, it, push, push ? wf_bucket(sc.d) & W.sort_mask : 0u, bb, bf)
                                       : wf_push(W, it, push);
         if (push) {
             wf_store_ray(O, out, sc, depth - 1);
@@ -1221,7 +1246,7 @@ __global__ __launch_bounds__(256) void wf_reduce(rtw_launch L, rtw_wf W) {
         if (wf_pixel(L, W, q, pixel, out_idx, x, y)) {
             float4 a = L.accum[out_idx];
             for (uint32_t s = 0; s < W.n_s; s++) {
-                const float4 c = W.ls[(size_t)s * W.n_pix + q];
+                const float4 c = W.ls[((((size_t)(q >> 6) * W.n_s) + s) << 6) | (q & 63u)];  // wf_path
                 if (is_nan3(mk(c.x, c.y, c.z))) cnt.nans++;
                 a.x += c.x;
                 a.y += c.y;
@@ -1296,21 +1321,20 @@ rtw_wf wf_lists(const rtw_launch& L, const rtw_wf& W, hipStream_t st) {
 
 template <uint32_t FEAT>
 struct WfGrids {
-    uint32_t trace, shade, tail;
+    uint32_t shade, shade0;  // shade0: iteration 0's instantiation (wf_camera)
     explicit WfGrids(int n_cu)
-        : trace(wf_grid(wf_trace<FEAT, false>, n_cu)), shade(wf_grid(wf_shade<FEAT>, n_cu)),
-          tail(wf_grid(wf_tail<FEAT>, n_cu)) {}
+        : shade(wf_grid(wf_shade<FEAT>, n_cu)), shade0(wf_grid(wf_shade<FEAT, true>, n_cu)) {}
 };
 
 // largest LDS stage of the wavefront trace (bytes); larger trees read L1/L2
 #define RTW_WF_LDS_MAX (64u * 1024u)
 #define RTW_WF_CLDS_MAX (150u * 1024u)  // compact-node LDS stage (one 1024-thread block per CU)
 
-template <uint32_t FEAT>
+template <uint32_t FEAT, bool CAM>
 uint32_t wf_lds_grid(int n_cu, size_t lds) {
     thread_local uint32_t cache[(RTW_WF_LDS_MAX + 16384) / 512 + 1] = {0};  // + geometry (L.geom_lds)
     uint32_t& g = cache[lds / 512];
-    if (!g) g = wf_grid(wf_trace<FEAT, true>, n_cu, lds);
+    if (!g) g = wf_grid(wf_trace<FEAT, true, CAM>, n_cu, lds);
     return g;
 }
 
@@ -1411,7 +1435,7 @@ void wf_run_fused(const rtw_launch& L, const rtw_wf& W, hipStream_t st, int n_cu
 }
 
 template <uint32_t FEAT>
-void wf_run(const rtw_launch& L, const rtw_wf& W, hipStream_t st, int n_cu, rtw_timer* T) {
+void wf_run(const rtw_launch& L, const rtw_wf& W0, hipStream_t st, int n_cu, rtw_timer* T) {
     const WfGrids<FEAT>& g = wf_grids<FEAT>(n_cu);
     if (L.wf_fuse & 1u) {
         size_t fclds = 0, flds = 0;
@@ -1427,56 +1451,75 @@ void wf_run(const rtw_launch& L, const rtw_wf& W, hipStream_t st, int n_cu, rtw_
         // through L1/L2 (C4, RTW_WF_FUSE bit 2) and with media (Cornell smoke) it loses 6 % / 1 %
         const bool media = (L.feat & RTW_F_MEDIUM) != 0;
         if (((fclds || flds) && !media) || (L.wf_fuse & 4u)) {
-            wf_run_fused<FEAT>(L, W, st, n_cu, fclds, flds, T);
+            wf_run_fused<FEAT>(L, W0, st, n_cu, fclds, flds, T);
             return;
         }
     }
-    RTW_TIME_BEGIN(T, RTW_K_GEN)
-    hipLaunchKernelGGL(wf_gen<FEAT>, dim3((W.n_paths + 255u) / 256u), dim3(256), 0, st, L, W);
-    RTW_TIME_END(T)
+    rtw_wf W = W0;  // the split kernels' coherent-queue iterations
+    W.sort_iters = W0.sort_iters_split;
     const uint32_t iters = L.max_depth < W.iters ? L.max_depth : W.iters;
+    // iteration 0's trace and shade generate the camera rays themselves (wf_camera); with no
+    // iteration (max_depth 0) nothing writes W.ls and the reduce must add zeros
+    if (iters == 0) (void)hipMemsetAsync(W.ls, 0, (size_t)W.n_paths * sizeof(float4), st);
     const rtw_wf Wt = iters ? wf_lists<FEAT>(L, W, st) : W;  // camera rays: iteration 0 of wf_trace (L1/L2)
     const size_t w2l = wf_w2_lds<FEAT>(L);  // the two-wide walk's stacks (trace / tail through L1/L2)
-    thread_local uint32_t wtrace[2] = {0, 0}, wtail[2] = {0, 0};
+    thread_local uint32_t wtrace[2] = {0, 0}, wtrace0[2] = {0, 0}, wtail[2] = {0, 0};
     const size_t lds_need = (size_t)L.n_nodes * L.n_orders * 32u;
     const size_t lds = (L.wf_lds && lds_need <= RTW_WF_LDS_MAX)
                            ? (lds_need + 511u) / 512u * 512u : 0;
     const size_t tlds = lds ? lds + ((FEAT & RTW_F_GEOM) ? L.geom_lds : 0u) : 0;  // + quads/members/instances
-    const uint32_t lds_grid = lds ? wf_lds_grid<FEAT>(n_cu, tlds) : 0;
+    const uint32_t lds_grid = lds ? wf_lds_grid<FEAT, false>(n_cu, tlds) : 0,
+                   lds_grid0 = lds ? wf_lds_grid<FEAT, true>(n_cu, tlds) : 0;
     // compact nodes of every octant copy in LDS (small static sphere trees)
     const size_t clds = (L.cnodes && L.fast_box && L.wf_clds)
                             ? (size_t)L.n_nodes * L.n_orders * 16u : 0;
-    thread_local uint32_t clds_grid_cache[2] = {0, 0};
-    uint32_t clds_grid = 0;
+    thread_local uint32_t clds_grid_cache[3] = {0, 0, 0};
+    uint32_t clds_grid = 0, clds_grid0 = 0;
     constexpr uint32_t clds_threads = 1024;  // one block per CU shares the stage (256 / 512: slower)
     if constexpr ((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING)) == 0) {
         if (clds && clds <= RTW_WF_CLDS_MAX) {
             if (!clds_grid_cache[0] || clds_grid_cache[1] != clds) {
                 clds_grid_cache[0] = wf_grid(wf_trace_clds<FEAT>, n_cu, clds, clds_threads);
+                clds_grid_cache[2] = wf_grid(wf_trace_clds<FEAT, true>, n_cu, clds, clds_threads);
                 clds_grid_cache[1] = (uint32_t)clds;
             }
             clds_grid = clds_grid_cache[0];
+            clds_grid0 = clds_grid_cache[2];
         }
     }
     for (uint32_t it = 0; it < iters; it++) {
         RTW_TIME_BEGIN(T, RTW_K_TRACE)
         if constexpr ((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING)) == 0) {
             if (clds_grid) {
-                hipLaunchKernelGGL(wf_trace_clds<FEAT>, dim3(clds_grid), dim3(clds_threads), clds, st, L, W, it);
+                if (it == 0)
+                    hipLaunchKernelGGL((wf_trace_clds<FEAT, true>), dim3(clds_grid0), dim3(clds_threads), clds, st, L,
+                                       W, it);
+                else
+                    hipLaunchKernelGGL(wf_trace_clds<FEAT>, dim3(clds_grid), dim3(clds_threads), clds, st, L, W, it);
                 RTW_TIME_END(T)
                 goto shade_step;
             }
         }
-        if (lds)
+        if (lds && it == 0)
+            hipLaunchKernelGGL((wf_trace<FEAT, true, true>), dim3(lds_grid0), dim3(256), tlds, st, L, W, it);
+        else if (lds)
             hipLaunchKernelGGL((wf_trace<FEAT, true>), dim3(lds_grid), dim3(256), tlds, st, L, W, it);
+        else if (it == 0)
+            hipLaunchKernelGGL((wf_trace<FEAT, false, true>),
+                               dim3(wf_grid_cached(wf_trace<FEAT, false, true>, n_cu, w2l, wtrace0)), dim3(256), w2l, st,
+                               L, Wt, it);
         else
             hipLaunchKernelGGL((wf_trace<FEAT, false>), dim3(wf_grid_cached(wf_trace<FEAT, false>, n_cu, w2l, wtrace)),
-                               dim3(256), w2l, st, L, it == 0 ? Wt : W, it);
+                               dim3(256), w2l, st, L, W, it);
         RTW_TIME_END(T)
     shade_step:
         RTW_TIME_BEGIN(T, RTW_K_SHADE)
-        hipLaunchKernelGGL(wf_shade<FEAT>, dim3(g.shade), dim3(256), (FEAT & RTW_F_GEOM) ? L.geom_lds : 0u, st, L,
-                           W, it);
+        if (it == 0)
+            hipLaunchKernelGGL((wf_shade<FEAT, true>), dim3(g.shade0), dim3(256), (FEAT & RTW_F_GEOM) ? L.geom_lds : 0u,
+                               st, L, W, it);
+        else
+            hipLaunchKernelGGL(wf_shade<FEAT>, dim3(g.shade), dim3(256), (FEAT & RTW_F_GEOM) ? L.geom_lds : 0u, st, L,
+                               W, it);
         RTW_TIME_END(T)
     }
     if (iters < L.max_depth) {
@@ -1532,11 +1575,14 @@ void rtw_wavefront_batch(const rtw_launch& L, const rtw_wf& W, void* stream, int
 
 uint32_t rtw_wavefront_max_waves(int n_cu) {
     uint32_t m = 0;
-    for (uint32_t g : {wf_grids<0u>(n_cu).shade, wf_grids<RTW_F_CHECKER>(n_cu).shade,
-                       wf_grids<RTW_F_SPHERES>(n_cu).shade, wf_grids<RTW_F_OBJECTS>(n_cu).shade,
-                       wf_grids<RTW_F_TEXTURED>(n_cu).shade, wf_grids<RTW_F_MEDIA>(n_cu).shade,
-                       wf_grids<RTW_F_ALL>(n_cu).shade})
-        m = g > m ? g : m;
+    auto mx = [&m](uint32_t a, uint32_t b) { m = std::max({m, a, b}); };
+    mx(wf_grids<0u>(n_cu).shade, wf_grids<0u>(n_cu).shade0);
+    mx(wf_grids<RTW_F_CHECKER>(n_cu).shade, wf_grids<RTW_F_CHECKER>(n_cu).shade0);
+    mx(wf_grids<RTW_F_SPHERES>(n_cu).shade, wf_grids<RTW_F_SPHERES>(n_cu).shade0);
+    mx(wf_grids<RTW_F_OBJECTS>(n_cu).shade, wf_grids<RTW_F_OBJECTS>(n_cu).shade0);
+    mx(wf_grids<RTW_F_TEXTURED>(n_cu).shade, wf_grids<RTW_F_TEXTURED>(n_cu).shade0);
+    mx(wf_grids<RTW_F_MEDIA>(n_cu).shade, wf_grids<RTW_F_MEDIA>(n_cu).shade0);
+    mx(wf_grids<RTW_F_ALL>(n_cu).shade, wf_grids<RTW_F_ALL>(n_cu).shade0);
     return 4 * m;
 }
 
