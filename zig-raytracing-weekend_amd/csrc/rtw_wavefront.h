@@ -17,7 +17,7 @@
 #define RTW_W2_STACK_MAX 32   // deepest per-lane LDS stack of the two-wide walk (256 threads x 32 x 4 B = 32 KiB)
 
 // One batch: n_pix logical pixels (8x8 tiles over the launch rows) x n_s samples.
-// Path p = s_local * n_pix + q.
+// Path p = ((q / 64) * n_s + s_local) * 64 + q % 64 (tile-major, wf_path).
 //
 // Path state lives in *slot space* and moves with the compaction: iteration it
 // reads set[it & 1] and shade writes each surviving path's state to its new slot
@@ -26,13 +26,14 @@
 // scattered 16-B pieces of 64-B lines).  Only the final radiance is stored by
 // path id (ls[p], once per path).
 //
-// Slots: iteration 0 deals the 64-path chunks round-robin over the waves of the
-// grid (slot = p; each chunk one 8x8 tile: coherent primary rays; every wave
-// samples the whole image: balanced).  shade appends the survivors of wave w to
-// stripe w % STRIPES of the other set (one wave-aggregated atomic per 64 paths,
-// 256 counters: no hot spot); later iterations give stripe s to the waves
-// w with w % STRIPES == s, which stride over its 64-slot chunks.  The grids are
-// multiples of STRIPES waves.
+// Slots: iteration 0 deals the 64-path chunks in runs of 16 samples of one tile
+// round-robin over the waves of the grid (slot = p; each chunk one 8x8 tile:
+// coherent primary rays; every wave samples the whole image: balanced).  shade
+// appends the survivors of wave w to stripe w % STRIPES of the other set (one
+// wave-aggregated atomic per push, 256 counters: no hot spot), in the first
+// sort_iters iterations into 64-slot blocks per direction bucket; later
+// iterations give stripe s to the waves w with w % STRIPES == s, which stride
+// over its 64-slot chunks.  The grids are multiples of STRIPES waves.
 struct rtw_wf_set {
     float4* ray_o;      // o.xyz, time
     float4* ray_d;      // d.xyz, bits(remaining depth); depth 0 = no path
