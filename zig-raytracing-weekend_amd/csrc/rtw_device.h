@@ -27,7 +27,7 @@
 #define RTW_STEPS 1
 #endif
 
-#if defined(RTW_ABLATE_MATH)
+#if defined(RTW_ABLATE_MATH) && defined(__HIP_DEVICE_COMPILE__)
 // timing ablation only (not IEEE): hardware sqrt / reciprocal
 #define __builtin_sqrtf(x) __builtin_amdgcn_sqrtf(x)
 #define RTW_DIV(a, b) ((a) * __builtin_amdgcn_rcpf(b))
@@ -405,7 +405,21 @@ RTW_DHD f3 member_sphere_center(const rtw_launch& L, const rtw_dev_sphere& s, ui
 }
 
 // Quad.hit t only (objects.zig:222-255), closed interval [tmin, tmax]
+#if defined(RTW_ABLATE_QUAD2) && defined(__HIP_DEVICE_COMPILE__)
+RTW_DHD bool quad_t_once(const rtw_dev_quad& q, const Ray& r, float tmin, float tmax, float& t);
 RTW_DHD bool quad_t(const rtw_dev_quad& q, const Ray& r, float tmin, float tmax, float& t) {
+    // timing ablation only: every quad test twice (the second is the same test)
+    float tm = tmax, t2 = 0.0f;
+    asm volatile("" : "+v"(tm));
+    const bool h2 = quad_t_once(q, r, tmin, tm, t2);
+    const bool h = quad_t_once(q, r, tmin, tmax, t);
+    if (h2 != h) t = t2;
+    return h;
+}
+RTW_DHD bool quad_t_once(const rtw_dev_quad& q, const Ray& r, float tmin, float tmax, float& t) {
+#else
+RTW_DHD bool quad_t(const rtw_dev_quad& q, const Ray& r, float tmin, float tmax, float& t) {
+#endif
     const f3 n = ld3(q.n);
     const float denom = dot(n, r.d);
     if (__builtin_fabsf(denom) < 1e-8f) return false;

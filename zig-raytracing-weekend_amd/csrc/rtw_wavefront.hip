@@ -1131,6 +1131,12 @@ __device__ __forceinline__ void wf_step_body(const rtw_launch& L, const rtw_wf& 
             if (live) {
                 float t;
                 const int hit = wf_walk<FEAT, WALK>(L, lds, r, t, cnt, rng.s);
+#if defined(RTW_ABLATE_WALK2)
+                {   // timing ablation only: the walk twice (the second result is the same)
+                    float t2;
+                    if (wf_walk<FEAT, WALK>(L, lds, r, t2, cnt, rng.s) != hit) t = t2;
+                }
+#endif
                 cnt.rays++;
                 if (hit < 0) {
                     acc = acc + thr * background(L, r);
