@@ -62,13 +62,49 @@ RTW_DHD f3 operator-(f3 a, f3 b) { return f3{a.x - b.x, a.y - b.y, a.z - b.z}; }
 RTW_DHD f3 operator*(f3 a, f3 b) { return f3{a.x * b.x, a.y * b.y, a.z * b.z}; }
 RTW_DHD f3 operator-(f3 a) { return f3{-a.x, -a.y, -a.z}; }
 RTW_DHD f3 splat(float s) { return f3{s, s, s}; }
-RTW_DHD f3 divs(f3 a, float s) { return f3{RTW_DIV(a.x, s), RTW_DIV(a.y, s), RTW_DIV(a.z, s)}; }
+RTW_DHD float rcp_refined(float d, float y0);
+RTW_DHD float div_shared(float x, float d, float y);
+RTW_DHD float sqrt_refined(float x, float s);
+#if defined(RTW_ABLATE_SHADE_MATH) && defined(__HIP_DEVICE_COMPILE__)
+// timing ablation only (not IEEE): hardware reciprocal / sqrt in divs and unit_vector (shading), the walk unchanged
+RTW_DHD f3 divs(f3 a, float s) {
+    const float y = __builtin_amdgcn_rcpf(s);
+    return f3{a.x * y, a.y * y, a.z * y};
+}
+RTW_DHD float unit_len(float ls) { return __builtin_amdgcn_sqrtf(ls); }
+#else
+// a / s per component, correctly rounded.  Device: one refined reciprocal of s shared by three div_shared
+// (the compiler's IEEE division sequence without its range scaling and special-case fix-up, below) when s
+// and every component lie in [2^-40, 2^40] in magnitude -- unscaled operands, normal quotients, no zero
+// (whose sign div_shared would not keep) and no inf / NaN, checked on the magnitude bits; otherwise, and on
+// the host, IEEE division.  (Hit normals (p - center) / radius, unit vectors.)
+RTW_DHD f3 divs(f3 a, float s) {
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(RTW_ABLATE_MATH)
+    const uint32_t ax = __builtin_bit_cast(uint32_t, a.x) & 0x7FFFFFFFu, ay = __builtin_bit_cast(uint32_t, a.y) & 0x7FFFFFFFu,
+                   az = __builtin_bit_cast(uint32_t, a.z) & 0x7FFFFFFFu, as = __builtin_bit_cast(uint32_t, s) & 0x7FFFFFFFu;
+    const uint32_t mx = __builtin_elementwise_max(__builtin_elementwise_max(ax, ay), __builtin_elementwise_max(az, as)),
+                   mn = __builtin_elementwise_min(__builtin_elementwise_min(ax, ay), __builtin_elementwise_min(az, as));
+    if (mn >= 0x2B800000u && mx <= 0x53800000u) {  // 2^-40, 2^40
+        const float y = rcp_refined(s, RTW_RCP_EST(s));
+        return f3{div_shared(a.x, s, y), div_shared(a.y, s, y), div_shared(a.z, s, y)};
+    }
+#endif
+    return f3{RTW_DIV(a.x, s), RTW_DIV(a.y, s), RTW_DIV(a.z, s)};
+}
+// sqrt(lengthSquared) of unit_vector, correctly rounded: sqrt_refined on [2^-96, 2^128) on the device
+RTW_DHD float unit_len(float ls) {
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(RTW_ABLATE_MATH)
+    if (ls >= 0x1p-96f && ls <= 0x1.fffffep127f) return sqrt_refined(ls, RTW_SQRT_EST(ls));
+#endif
+    return __builtin_sqrtf(ls);
+}
+#endif
 RTW_DHD float dot(f3 u, f3 v) { return u.x * v.x + u.y * v.y + u.z * v.z; }
 RTW_DHD f3 cross(f3 u, f3 v) {  // vec3.zig:31-33
     return f3{u.y * v.z - u.z * v.y, u.z * v.x - u.x * v.z, u.x * v.y - u.y * v.x};
 }
 RTW_DHD float length_squared(f3 u) { return u.x * u.x + u.y * u.y + u.z * u.z; }
-RTW_DHD f3 unit_vector(f3 v) { return divs(v, __builtin_sqrtf(length_squared(v))); }
+RTW_DHD f3 unit_vector(f3 v) { return divs(v, unit_len(length_squared(v))); }
 RTW_DHD f3 ld3(const float* p) { return f3{p[0], p[1], p[2]}; }
 RTW_DHD bool near_zero(f3 u) {  // vec3.zig:19-22
     const float s = 1e-8f;

@@ -1099,6 +1099,12 @@ __device__ __forceinline__ void wf_step_body(const rtw_launch& L, const rtw_wf& 
                     }
                 }
                 if (!listed) hit = wf_walk<FEAT, WALK>(L, lds, r, t, cnt, rng.s);
+#if defined(RTW_ABLATE_WALK2)
+                if (!listed) {  // timing ablation only: the walk twice (the second result is the same)
+                    float t2;
+                    if (wf_walk<FEAT, WALK>(L, lds, r, t2, cnt, rng.s) != hit) t = t2;
+                }
+#endif
 #if defined(RTW_DIAG_WALK) && defined(__HIP_DEVICE_COMPILE__)
                 if (!listed && it == rtw_diag_rec_it && rtw_diag_rec && slot < rtw_diag_rec_cap) {
                     rtw_diag_rec[2u * slot] = make_uint4(cnt.dsteps | (cnt.dleaves << 16), fbits(r.d.x), fbits(r.d.y),
