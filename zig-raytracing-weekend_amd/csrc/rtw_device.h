@@ -1021,6 +1021,31 @@ RTW_DHD HitPrep object_prep(const rtw_launch& L, const Ray& r, uint32_t kind, ui
     return h;
 }
 
+// The material kind of a walk's hit (the record hit_prep reads, without the hit record itself)
+template <uint32_t FEAT>
+RTW_DHD uint32_t hit_material_kind(const float4* __restrict__ nodes, const rtw_launch& L, int hit) {
+    if (L.n_orders > 1) {
+        nodes = order_base(nodes, L, (uint32_t)hit >> RTW_HIT_NODE_BITS);
+        hit &= (1 << RTW_HIT_NODE_BITS) - 1;
+    }
+    const uint32_t node = (uint32_t)hit & ((1u << RTW_HIT_NODE_BITS) - 1u);
+    const float4 B = nodes[2 * node + 1];
+    uint32_t mat = fbits(B.y);  // sphere leaf
+    if constexpr ((FEAT & RTW_F_GEOM) != 0) {
+        const uint32_t kind = RTW_LEAF_KIND(fbits(B.w)), idx = fbits(B.z);
+        if (kind == RTW_OBJ_QUAD) {
+            mat = L.quads[idx].mat;
+        } else if (kind == RTW_OBJ_INSTANCE) {
+            const uint32_t ref = L.members[L.insts[idx].first + ((uint32_t)hit >> RTW_HIT_NODE_BITS)];
+            const uint32_t mi = RTW_REF_INDEX(ref);
+            mat = RTW_REF_KIND(ref) == RTW_OBJ_SPHERE ? L.sph[mi].mat : L.quads[mi].mat;
+        } else if (kind != RTW_OBJ_SPHERE) {
+            mat = L.media[idx].mat;
+        }
+    }
+    return L.mats[mat].kind;
+}
+
 template <uint32_t FEAT>
 RTW_DHD HitPrep hit_prep(const float4* __restrict__ nodes, const rtw_launch& L, const Ray& r,
                                             int hit, float t) {

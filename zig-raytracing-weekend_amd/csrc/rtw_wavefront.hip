@@ -158,6 +158,88 @@ __device__ __forceinline__ uint32_t wf_push(const rtw_wf& W, uint32_t it, bool p
 // one ballot per key bit; each bucket's lanes take consecutive slots of its block, and buckets whose
 // block overflows take fresh blocks, all of them with one atomic on the stripe counter.  A partly filled
 // block's unused slots are marked dead (depth 0) when the wave's iteration ends (wf_close_blocks).
+// vec3.randomInUnitSphere (vec3.zig:40-45) for every lane of the wave with `need`, cooperatively: the
+// same accepted candidate and the same final RNG state as seq_reject<3> per lane.  The draws are
+// counter-based (rtw_path_float: the k-th draw after state s hashes s + k*G), so candidate c of a lane
+// -- draws 3c+1 .. 3c+3 -- can be evaluated on any lane from the owner's state.  Trip 0: every lane
+// evaluates its own candidate 0 (~52 % accept).  Then, while lanes are pending, each of the R pending
+// lanes gets a group of g = 64 / R (a power of two) lanes that evaluate its next g candidates at once
+// and it takes the first accepted one: ~3 trips for the wave instead of the ~7 the slowest of 64
+// independent loops takes, and the idle lanes do the work.  Called by the whole wave (converged).
+__device__ __forceinline__ void wf_cand3(uint64_t s, float& x, float& y, float& z) {
+    rtw_rng r;
+    r.s = s;
+    x = rtw_path_range(r, -1, 1);
+    y = rtw_path_range(r, -1, 1);
+    z = rtw_path_range(r, -1, 1);
+}
+__device__ __forceinline__ void wf_reject3(bool need, rtw_rng& rng, float (&out)[3]) {
+    const uint32_t lane = __lane_id();
+    const uint64_t s0 = rng.s;
+    float x = 0.0f, y = 0.0f, z = 0.0f;
+    bool ok = false;
+    if (need) {
+        wf_cand3(s0, x, y, z);
+        ok = x * x + y * y + z * z < 1;  // lengthSquared < 1 (vec3.zig:43)
+    }
+    if (ok) {
+        out[0] = x;
+        out[1] = y;
+        out[2] = z;
+        rng.s = s0 + 3ull * RTW_GOLDEN;
+    }
+    uint64_t pend = __ballot(need && !ok);
+    uint32_t kb = 1;  // candidates every pending lane has rejected so far
+    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    while (pend) {
+        const uint32_t R = (uint32_t)__popcll(pend);
+        const uint32_t lg = R > 32 ? 0u : R > 16 ? 1u : R > 8 ? 2u : R > 4 ? 3u : R > 2 ? 4u : R > 1 ? 5u : 6u;
+        const bool mine = (pend >> lane) & 1ull;
+        const uint32_t rank = (uint32_t)__popcll(pend & lt);
+        // the owner's state to the first lane of its group (forward permute), then to the whole group
+        const int dst = (int)((mine ? (rank << lg) : 63u) * 4u);
+        int lo = __builtin_amdgcn_ds_permute(dst, (int)(uint32_t)s0);
+        int hi = __builtin_amdgcn_ds_permute(dst, (int)(uint32_t)(s0 >> 32));
+        const int lead = (int)((lane & ~((1u << lg) - 1u)) * 4u);
+        lo = __builtin_amdgcn_ds_bpermute(lead, lo);
+        hi = __builtin_amdgcn_ds_bpermute(lead, hi);
+        const bool act = (lane >> lg) < R;
+        const uint32_t c = kb + (lane & ((1u << lg) - 1u));
+        float cx = 0.0f, cy = 0.0f, cz = 0.0f;
+        bool acc = false;
+        if (act) {
+            const uint64_t so = ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
+            wf_cand3(so + (uint64_t)(3u * c) * RTW_GOLDEN, cx, cy, cz);
+            acc = cx * cx + cy * cy + cz * cz < 1;
+        }
+        const uint64_t A = __ballot(act && acc);
+        int src = (int)(lane * 4u);
+        uint32_t idx = 0;
+        bool got = false;
+        if (mine) {
+            const uint64_t gm = lg == 6u ? ~0ull : ((1ull << (1u << lg)) - 1ull);
+            const uint64_t grp = (A >> (rank << lg)) & gm;
+            if (grp) {
+                const uint32_t o = (uint32_t)__builtin_ctzll(grp);
+                src = (int)(((rank << lg) + o) * 4u);
+                idx = kb + o;
+                got = true;
+            }
+        }
+        const float gx = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(cx)));
+        const float gy = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(cy)));
+        const float gz = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(cz)));
+        if (got) {
+            out[0] = gx;
+            out[1] = gy;
+            out[2] = gz;
+            rng.s = s0 + (uint64_t)(3u * (idx + 1u)) * RTW_GOLDEN;
+        }
+        pend = __ballot(mine && !got);
+        kb += 1u << lg;
+    }
+}
+
 __device__ __forceinline__ uint32_t wf_bucket(f3 d) {
     const float ilen = __builtin_amdgcn_rsqf(d.x * d.x + d.y * d.y + d.z * d.z);  // approximate: a sort key only
     const float uy = d.y * ilen;
@@ -900,6 +982,8 @@ __device__ __forceinline__ void wf_tail_body(const rtw_launch& L, const rtw_wf& 
         }
         bool done = true, hitp = false, need_uv = false;
         HitPrep hp;
+        int ohit = -1;  // object scenes: the hit shaded after the wave's rejection loop
+        float ot = 0.0f;
         if (active) {  // one more iteration of rayColor
             cnt.rays++;
             cnt.tail_rays++;
@@ -920,10 +1004,32 @@ __device__ __forceinline__ void wf_tail_body(const rtw_launch& L, const rtw_wf& 
                 hp = hit_prep<FEAT>(L.nodes, L, r, hit, t);
                 hitp = true;
                 need_uv = needs_unit_vector<FEAT>(hp.m.kind);
+            } else if constexpr ((FEAT & RTW_F_GEOM) != 0) {
+                // object scenes: as the fused step's object path, the wave's shared rejection loop
+                // (wf_reject3) before the hit record, on the material kind alone
+                ohit = hit;
+                ot = t;
+                need_uv = needs_unit_vector<FEAT>(hit_material_kind<FEAT>(L.nodes, L, hit));
             } else {
                 f3 att;
                 Ray sc;
                 if (shade<FEAT>(L.nodes, L, r, hit, t, rng, thr, acc, att, sc) && depth > 1) {
+                    thr = thr * att;
+                    r = sc;
+                    depth--;
+                    done = false;
+                }
+            }
+        }
+        if constexpr ((FEAT & RTW_F_GEOM) != 0) {
+            float uv3[3] = {0.0f, 0.0f, 0.0f};
+            wf_reject3(need_uv, rng, uv3);  // the whole wave
+            if (ohit >= 0) {
+                const HitPrep h = hit_prep<FEAT>(L.nodes, L, r, ohit, ot);
+                const f3 ruv = need_uv ? unit_vector(mk(uv3[0], uv3[1], uv3[2])) : mk(0, 0, 0);
+                f3 att;
+                Ray sc;
+                if (scatter_finish<FEAT>(L, r, h, ruv, rng, thr, acc, att, sc) && depth > 1) {
                     thr = thr * att;
                     r = sc;
                     depth--;
@@ -1132,11 +1238,13 @@ __device__ __forceinline__ void wf_step_body(const rtw_launch& L, const rtw_wf& 
                 }
             }
         } else {
-            // object scenes: Material.scatter inline (the split form's live hit record
-            // costs a wave per SIMD here: Cornell -12 %)
+            // object scenes: the walk, then the randomUnitVector draw of every lane whose material
+            // starts with one (wf_reject3: the wave's lanes share the rejection loop; it only needs the
+            // material kind, so no hit record is live across it), then the hit record and the material
+            float t = 0.0f;
+            int hit = -1;
             if (live) {
-                float t;
-                const int hit = wf_walk<FEAT, WALK>(L, lds, r, t, cnt, rng.s);
+                hit = wf_walk<FEAT, WALK>(L, lds, r, t, cnt, rng.s);
 #if defined(RTW_ABLATE_WALK2)
                 {   // timing ablation only: the walk twice (the second result is the same)
                     float t2;
@@ -1144,11 +1252,18 @@ __device__ __forceinline__ void wf_step_body(const rtw_launch& L, const rtw_wf& 
                 }
 #endif
                 cnt.rays++;
+            }
+            const bool need_uv = hit >= 0 && needs_unit_vector<FEAT>(hit_material_kind<FEAT>(L.nodes, L, hit));
+            float uv3[3] = {0.0f, 0.0f, 0.0f};
+            wf_reject3(need_uv, rng, uv3);
+            if (live) {
                 if (hit < 0) {
                     acc = acc + thr * background(L, r);
                 } else {
+                    const HitPrep hp = hit_prep<FEAT>(L.nodes, L, r, hit, t);
+                    const f3 ruv = need_uv ? unit_vector(mk(uv3[0], uv3[1], uv3[2])) : mk(0, 0, 0);
                     f3 att;
-                    if (shade<FEAT>(L.nodes, L, r, hit, t, rng, thr, acc, att, sc) && depth > 1) {
+                    if (scatter_finish<FEAT>(L, r, hp, ruv, rng, thr, acc, att, sc) && depth > 1) {
                         thr = thr * att;
                         push = true;
                     }
