@@ -627,6 +627,7 @@ int run_wavefront(rtw_ctx* ctx, rtw_launch L, hipStream_t stream, rtw_timer* T) 
     W.sort_iters = ctx->wf_sort_iters;
     W.sort_iters_split = ctx->wf_sort_iters_split;
     W.sort_mask = ctx->wf_sort_mask;
+    W.run_log2 = 4;  // set per launch grid by wf_coherence (rtw_wavefront.hip)
     // camera-ray candidate lists (the compact-LDS fused step of static sphere scenes, rtw_tuning.tile_lists)
     if (L.tile_lists && L.cnodes && L.n_orders == 8) {
         const uint64_t tiles = n_pix / 64;

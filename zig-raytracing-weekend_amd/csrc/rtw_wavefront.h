@@ -57,7 +57,8 @@ struct rtw_wf {
     uint32_t iters;     // wavefront iterations before the tail kernel
     uint32_t sort_iters;  // iterations it < sort_iters push their survivors into direction-bucketed blocks
     uint32_t sort_iters_split;  // the same for the split trace / shade kernels (wf_run copies it to sort_iters)
-    uint32_t sort_mask;   // the bucket key bits they use ((1 << rtw_tuning.sort_bits) - 1)
+    uint32_t sort_mask;
+    uint32_t run_log2;    // iteration 0's tile runs: 2^run_log2 samples of one tile per run (wf_coherence)   // the bucket key bits they use ((1 << rtw_tuning.sort_bits) - 1)
 };
 
 // bytes of device state per path (two slot sets + hit + ls)

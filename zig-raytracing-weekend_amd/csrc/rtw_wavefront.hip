@@ -52,15 +52,15 @@ __device__ __forceinline__ bool wf_pixel(const rtw_launch& L, const rtw_wf& W, u
 __device__ __forceinline__ uint32_t wf_wave() { return blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); }
 __device__ __forceinline__ uint32_t wf_nwaves() { return gridDim.x * (blockDim.x >> 6); }
 
-// Iteration 0 deals its chunks (64 paths = one 8x8 tile of one sample) in runs of RTW_WF_TILE_RUN
-// consecutive samples of one tile: in tile-major order c = tile * n_s + s_local, run R = c / RUN goes to
+// Iteration 0 deals its chunks (64 paths = one 8x8 tile of one sample) in runs of RUN = 2^W.run_log2 (<= 16,
+// wf_coherence) consecutive samples of one tile: in tile-major order c = tile * n_s + s_local, run R = c / RUN goes to
 // wave R % nw, so a wave takes RUN chunks of the same tile in a row (the blocks its survivors fill,
 // wf_push_bucketed, then hold rays that left one tile) while the runs, dealt round-robin, keep the waves'
 // shares of sky and ground even.  A wave's k-th chunk: c = ((k / RUN) * nw + w) * RUN + k % RUN, which grows
 // with k (false: past the last chunk).  slot0: the chunk's first path id.
-#define RTW_WF_TILE_RUN 16u
 __device__ __forceinline__ bool wf_chunk0(const rtw_wf& W, uint32_t w, uint32_t nw, uint32_t k, uint32_t& slot0) {
-    const uint32_t c = ((k / RTW_WF_TILE_RUN) * nw + w) * RTW_WF_TILE_RUN + k % RTW_WF_TILE_RUN;
+    const uint32_t lg = W.run_log2;
+    const uint32_t c = ((((k >> lg) * nw + w)) << lg) + (k & ((1u << lg) - 1u));
     if (c >= (W.n_paths >> 6)) return false;
     slot0 = c << 6;
     return true;
@@ -1446,6 +1446,22 @@ rtw_wf wf_lists(const rtw_launch& L, const rtw_wf& W, hipStream_t st) {
     return Wt;
 }
 
+// Coherent-queue settings of a launch whose grid has nw waves.  Iteration 0 deals runs of
+// up to 16 samples per tile, shorter when a wave would get fewer than 64 runs (a small batch: whole runs
+// would leave the waves' shares of work uneven); direction bucketing only when a wave's iteration 0 has at
+// least RTW_WF_SORT_MIN_CHUNKS chunks -- each open block ends its iteration partly dead, which only a large
+// share of survivors per wave amortises (simple_light, 137 chunks per wave: -10 % with bucketing).
+#define RTW_WF_SORT_MIN_CHUNKS 192u
+rtw_wf wf_coherence(const rtw_wf& W, uint32_t nw, uint32_t sort_iters) {
+    rtw_wf C = W;
+    const uint32_t per_wave = nw ? (W.n_paths >> 6) / nw : 0u;
+    uint32_t lg = 0;
+    while (lg < 4 && (per_wave >> (lg + 1)) >= 64u) lg++;
+    C.run_log2 = lg;
+    C.sort_iters = per_wave >= RTW_WF_SORT_MIN_CHUNKS ? sort_iters : 0u;
+    return C;
+}
+
 template <uint32_t FEAT>
 struct WfGrids {
     uint32_t shade, shade0;  // shade0: iteration 0's instantiation (wf_camera)
@@ -1480,7 +1496,7 @@ const WfGrids<FEAT>& wf_grids(int n_cu) {
 // dynamic LDS of the fused kernels: tree stage + what is staged after it
 
 template <uint32_t FEAT>
-void wf_run_fused(const rtw_launch& L, const rtw_wf& W, hipStream_t st, int n_cu, size_t clds, size_t lds,
+void wf_run_fused(const rtw_launch& L, const rtw_wf& W0, hipStream_t st, int n_cu, size_t clds, size_t lds,
                   rtw_timer* T) {
     const size_t cdyn0 = clds,
                  cdyn = cdyn0 + L.mat_lds <= 160u * 1024u ? cdyn0 + L.mat_lds : cdyn0,
@@ -1510,7 +1526,8 @@ void wf_run_fused(const rtw_launch& L, const rtw_wf& W, hipStream_t st, int n_cu
     }
     // iteration 0 appends to len[1]; every later iteration's output counters are
     // zeroed by the kernel two iterations before (wf_step_zero_next)
-    (void)hipMemsetAsync(W.len[1], 0, RTW_WF_STRIPES * RTW_WF_LEN_STRIDE * 4, st);
+    (void)hipMemsetAsync(W0.len[1], 0, RTW_WF_STRIPES * RTW_WF_LEN_STRIDE * 4, st);
+    const rtw_wf W = wf_coherence(W0, grid * (clds ? 16u : 4u), W0.sort_iters);
     const uint32_t iters = L.max_depth < W.iters ? L.max_depth : W.iters;
     rtw_wf Wt = W;  // the camera-ray lists serve the LDS-staged steps of static sphere scenes
     if ((clds || lds) && iters) Wt = wf_lists<FEAT>(L, W, st);
@@ -1582,8 +1599,7 @@ void wf_run(const rtw_launch& L, const rtw_wf& W0, hipStream_t st, int n_cu, rtw
             return;
         }
     }
-    rtw_wf W = W0;  // the split kernels' coherent-queue iterations
-    W.sort_iters = W0.sort_iters_split;
+    const rtw_wf W = wf_coherence(W0, g.shade * 4u, W0.sort_iters_split);  // the split kernels' queues
     const uint32_t iters = L.max_depth < W.iters ? L.max_depth : W.iters;
     // iteration 0's trace and shade generate the camera rays themselves (wf_camera); with no
     // iteration (max_depth 0) nothing writes W.ls and the reduce must add zeros
