@@ -333,7 +333,10 @@ typedef struct rtw_tuning {
                                   4 elevation levels; 0 = one block per wave, appends in order; ABI 5) */
     uint32_t sort_iters_split; /* the same for the split trace / shade kernels (trees through L1/L2: C4), whose
                                   HBM-bound shade pays more for the scattered block stores (default 1; ABI 5) */
-    uint32_t _pad2;
+    uint32_t object_tree;      /* SAH trees of object scenes (quads / instances / media): inner nodes whose box has
+                                  >= this % of the area of the node above are not emitted (their children take
+                                  their place: box tests that almost always pass); 0 = the plain SAH tree,
+                                  default 90 (ABI 5, formerly padding) */
 } rtw_tuning;
 
 void rtw_tuning_defaults(rtw_tuning* out);

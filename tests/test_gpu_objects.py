@@ -148,3 +148,29 @@ def test_object_counters_equal_reference_traversal(rtw, oracle):
     assert g[rtw._abi.RTW_STAT_RAYS] == oc.rays
     assert g[rtw._abi.RTW_STAT_NODES] == oc.nodes
     assert g[rtw._abi.RTW_STAT_LEAVES] == oc.leaves
+
+
+@pytest.mark.parametrize("name", ["cornell", "cornell_smoke", "quads"])
+def test_object_tree_bit_identical(rtw, name):
+    """Object-scene trees with inner nodes flattened away (rtw_tuning.object_tree: nodes whose box has
+    >= that % of the area above are not emitted) render exactly what the plain SAH tree renders: at
+    the default (90), at 50 and 100, in the fused step and the separate kernels, with the exact slab
+    test, and from a camera beyond 7x the scene extent (the launch falls back to the exact test)."""
+    arr = rtw.flatten(SCENES[name][0](rtw.worlds))
+    kw = dict(SCENES[name][1])
+    far_at = (278.0, 278.0, -4500.0) if name != "quads" else (0.0, 0.0, 80.0)  # |o| > 7 * extent
+    outs = {}
+    for tag, tu, far in (("plain", {"object_tree": 0}, False), ("default", {}, False),
+                         ("50", {"object_tree": 50}, False), ("100", {"object_tree": 100}, False),
+                         ("split", {"fuse": 0}, False), ("exact", {"fast_box": 0}, False),
+                         ("far_plain", {"object_tree": 0}, True), ("far", {}, True)):
+        k = dict(kw)
+        if far:
+            k.update(lookfrom=far_at, vfov=7.0)
+        cam = rtw.Camera(image_width=72, samples_per_pixel=6, max_depth=50, **k).init()
+        world = rtw.World(arr, tuning=tu)
+        outs[tag] = render_all(rtw, world, cam, 6, 11)
+        world.close()
+    for k in ("default", "50", "100", "split", "exact"):
+        assert np.array_equal(outs["plain"], outs[k]), k
+    assert np.array_equal(outs["far_plain"], outs["far"])

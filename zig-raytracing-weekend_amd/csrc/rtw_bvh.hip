@@ -397,8 +397,8 @@ private:
 class SahBuilder {
 public:
     SahBuilder(const rtw_scene_desc& d, const Geometry& g, std::vector<rtw_node>& out, uint32_t max_leaf,
-               bool hoist = false)
-        : geo_(g), nodes_(out), objs_(g.objects()), hoist_(hoist) {
+               bool hoist = false, float flatten = 0.0f)
+        : geo_(g), nodes_(out), objs_(g.objects()), hoist_(hoist), flatten_(flatten) {
         const size_t n = objs_.size();
         cent_.resize(n);
         for (size_t i = 0; i < n; i++)
@@ -437,7 +437,7 @@ public:
             base_ = (uint32_t)nodes_.size();
             for (size_t k = 0; k < h; k++)
                 nodes_.push_back(geo_.leaf(objs_[idx_[k]], (uint32_t)nodes_.size() + 1 - base_));
-            emit_tree(root, dir);
+            emit_tree(root, dir, -1.0f);
         }
         n_hoisted_ = (uint32_t)h;
     }
@@ -475,12 +475,21 @@ private:
         return me;
     }
 
-    // pre-order with skip links (relative to the array start base_)
-    void emit_tree(int t, const float dir[3]) {
+    // pre-order with skip links (relative to the array start base_).  parent_area: the area of the
+    // emitted inner node above (< 0 at the root).  Object scenes (flatten_ > 0): an inner node whose box
+    // has >= flatten_ of the area of the emitted node above is not emitted -- its children follow in its
+    // place, in the same order, and the skip link of the node above still ends past them.  A ray then
+    // visits a superset of the plain tree's leaves in the same order, and every box is conservative, so
+    // the closest hit (ties included) is the plain tree's.  (Cornell: the walls' thin boxes make every
+    // union of two of them the whole room, so four inner nodes under the root tested the room again on
+    // every ray.)
+    void emit_tree(int t, const float dir[3], float parent_area) {
         const TNode& n = tree_[t];
         if (n.left < 0) {
-            for (uint32_t i = 0; i < n.count; i++)
-                nodes_.push_back(geo_.leaf(objs_[idx_[n.first + i]], (uint32_t)nodes_.size() + 1 - base_));
+            for (uint32_t i = 0; i < n.count; i++) {
+                const Obj& o = objs_[idx_[n.first + i]];
+                nodes_.push_back(geo_.leaf(o, (uint32_t)nodes_.size() + 1 - base_));
+            }
             return;
         }
         const Box& lb = tree_[n.left].box;
@@ -490,15 +499,19 @@ private:
             pl += dir[k] * (lb.mn[k] + lb.mx[k]);
             pr += dir[k] * (rb.mn[k] + rb.mx[k]);
         }
+        const float a = area(n.box);
+        const bool emit = !(flatten_ > 0 && parent_area >= 0 && a >= flatten_ * parent_area);
         const size_t me = nodes_.size();
-        nodes_.push_back(rtw_node{});
+        if (emit) nodes_.push_back(rtw_node{});
+        const float below = emit ? a : parent_area;
         if (pr < pl) {  // right child is nearer along dir: walk it first
-            emit_tree(n.right, dir);
-            emit_tree(n.left, dir);
+            emit_tree(n.right, dir, below);
+            emit_tree(n.left, dir, below);
         } else {
-            emit_tree(n.left, dir);
-            emit_tree(n.right, dir);
+            emit_tree(n.left, dir, below);
+            emit_tree(n.right, dir, below);
         }
+        if (!emit) return;
         rtw_node& o = nodes_[me];
         const uint32_t skip = (uint32_t)nodes_.size() - base_;
         for (int i = 0; i < 3; i++) { o.a[i] = n.box.mn[i]; o.b[i] = n.box.mx[i]; }
@@ -615,6 +628,7 @@ private:
     size_t max_leaf_ = 1;  // objects per leaf run
     float ci_ = 2.0f;      // cost of one leaf test relative to one box test
     bool hoist_ = false;   // emit dominant spheres first, ahead of the tree (build)
+    float flatten_ = 0.0f;  // > 0: inner nodes with >= this fraction of the area above are not emitted (emit_tree)
     uint32_t n_hoisted_ = 0;
 };
 
@@ -622,14 +636,14 @@ private:
 
 int rtw_build_bvh(const rtw_scene_desc& desc, std::vector<rtw_node>& nodes, rtw_geometry& geom,
                   uint32_t* depth, uint32_t* axis_draws, float* box_pad, float* extent, uint32_t orders,
-                  uint32_t sah_max_leaf, uint32_t hoist, uint32_t* n_hoisted) {
+                  uint32_t sah_max_leaf, uint32_t hoist, uint32_t* n_hoisted, uint32_t flatten_pct) {
     if (box_pad) *box_pad = 0;
     if (extent) *extent = 0;
     if (n_hoisted) *n_hoisted = 0;
     Geometry geo(desc, geom);
     if (int rc = geo.build()) return rc;
     if (desc.bvh_mode == RTW_BVH_SAH) {
-        SahBuilder b(desc, geo, nodes, sah_max_leaf, hoist != 0);
+        SahBuilder b(desc, geo, nodes, sah_max_leaf, hoist != 0, (float)flatten_pct / 100.0f);
         b.build(orders);
         if (n_hoisted) *n_hoisted = b.hoisted();
         if (depth) *depth = b.depth();

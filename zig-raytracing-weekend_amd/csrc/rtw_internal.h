@@ -185,9 +185,12 @@ bool rtw_wide2_nodes(const std::vector<rtw_node>& nodes, uint32_t n_per, std::ve
                      std::vector<uint32_t>& leaf_id, uint32_t* max_stack);
 
 // hoist (SAH sphere scenes): emit spheres whose box dwarfs the rest ahead of the tree (*n_hoisted of them)
+// flatten_pct (SAH trees): inner nodes with >= that % of the area of the node above are not emitted
+// (0 = off; SahBuilder::emit_tree)
 int rtw_build_bvh(const rtw_scene_desc& desc, std::vector<rtw_node>& nodes, rtw_geometry& geom,
                   uint32_t* depth, uint32_t* axis_draws, float* box_pad = nullptr, float* extent = nullptr,
-                  uint32_t orders = 1, uint32_t sah_max_leaf = 1, uint32_t hoist = 0, uint32_t* n_hoisted = nullptr);
+                  uint32_t orders = 1, uint32_t sah_max_leaf = 1, uint32_t hoist = 0, uint32_t* n_hoisted = nullptr,
+                  uint32_t flatten_pct = 0);
 
 // One scene on one device (the opaque rtw_ctx of include/rtw_gpu.h).
 struct rtw_ctx {
