@@ -182,3 +182,23 @@ def test_host_render_ex_stop_and_progress(rtw):
                                    C.byref(o)), "rtw_render_ex")
     assert np.array_equal(buf, host_render(rtw, arr, cam, 6, 2))
     world.close()
+
+
+def test_scene_hash_independent_of_tree_layout(rtw):
+    """rtw_scene_hash (the checkpoint's scene key) names the scene, not the node layout the tuning
+    picks: equal under orderings, hoisting and object-tree flattening; different for another tree
+    kind, another reference-topology seed and another scene."""
+    def h(arr, tu=None):
+        world = rtw.World(arr, device=CPU, tuning=tu)
+        out = C.c_uint64()
+        rtw._abi.check(rtw.lib().rtw_scene_hash(world.handle, C.byref(out)), "rtw_scene_hash")
+        world.close()
+        return out.value
+
+    book = rtw.flatten(rtw.worlds.generate_world(0, "book1"))
+    base = h(book)
+    assert h(book, {"bvh_orders": 1}) == base and h(book, {"hoist": 0}) == base
+    assert h(rtw.flatten(rtw.worlds.generate_world(0, "book1"), bvh_mode=rtw._abi.RTW_BVH_REFERENCE)) != base
+    assert h(rtw.flatten(rtw.worlds.generate_world(1, "book1"))) != base
+    cornell = rtw.flatten(rtw.worlds.cornell_box())
+    assert h(cornell, {"object_tree": 0}) == h(cornell) == h(cornell, {"object_tree": 50})

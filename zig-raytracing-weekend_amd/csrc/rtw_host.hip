@@ -276,7 +276,8 @@ int rtw_scene_create_ex(const rtw_scene_desc* d, int device, const rtw_tuning* t
     }
     off = align(off + img_bytes + 16);
     // the scene image: the walks' derived records below (compact nodes, two-wide records) depend on the
-    // backend and the tuning, so a checkpoint's hash matches on every context of the same scene
+    // backend and the tuning, so a checkpoint's hash matches on every context of the same scene (the
+    // node array, whose layout also follows the tuning, is left out of the hash as well)
     const size_t hashed = off;
     const size_t o_cnod = off; off = align(off + cnodes.size() * sizeof(rtw_cnode));
     const size_t o_w2 = off; off = align(off + w2.size() * sizeof(rtw_cnode));
@@ -350,9 +351,14 @@ int rtw_scene_create_ex(const rtw_scene_desc* d, int device, const rtw_tuning* t
         }
     }
     ctx->blob_bytes = off;
-    {   // FNV-1a 64 of the scene image (rtw_scene_hash)
+    {   // FNV-1a 64 of the scene image (rtw_scene_hash): the tree kind (and the reference topology's seed),
+        // then every section after the nodes -- the node array's layout depends on the tuning (orderings,
+        // hoisting, object_tree), the image does not
         uint64_t h = 0xCBF29CE484222325ull;
-        for (size_t i = 0; i < hashed; i++) h = (h ^ blob[i]) * 0x100000001B3ull;
+        const uint64_t key[2] = {(uint64_t)d->bvh_mode, d->bvh_mode == RTW_BVH_REFERENCE ? (uint64_t)d->bvh_seed : 0ull};
+        const unsigned char* kb = reinterpret_cast<const unsigned char*>(key);
+        for (size_t i = 0; i < sizeof key; i++) h = (h ^ kb[i]) * 0x100000001B3ull;
+        for (size_t i = o_cvec; i < hashed; i++) h = (h ^ blob[i]) * 0x100000001B3ull;
         ctx->scene_hash = h;
     }
     if (host) ctx->host_blob = blob;  // the launch pointers address the host copy
