@@ -305,6 +305,7 @@ enum {  /* rtw_tuning.fuse */
     RTW_FUSE_TAIL_LDS = 2u,    /* the tail kernel walks the LDS stage */
     RTW_FUSE_GLOBAL = 4u       /* the fused step also for trees read through L1/L2 */
 };
+#define RTW_OTREE_NO_CULL 0x100u  /* rtw_tuning.object_tree */
 typedef struct rtw_tuning {
     uint32_t kernel;           /* rtw_kernel_kind (default WAVEFRONT) */
     uint32_t bvh_orders;       /* 0 = auto (8 octant-ordered copies for SAH sphere scenes, else 1), 1 or 8 */
@@ -333,10 +334,12 @@ typedef struct rtw_tuning {
                                   4 elevation levels; 0 = one block per wave, appends in order; ABI 5) */
     uint32_t sort_iters_split; /* the same for the split trace / shade kernels (trees through L1/L2: C4), whose
                                   HBM-bound shade pays more for the scattered block stores (default 1; ABI 5) */
-    uint32_t object_tree;      /* SAH trees of object scenes (quads / instances / media): inner nodes whose box has
-                                  >= this % of the area of the node above are not emitted (their children take
-                                  their place: box tests that almost always pass); 0 = the plain SAH tree,
-                                  default 90 (ABI 5, formerly padding) */
+    uint32_t object_tree;      /* SAH trees of object scenes (quads / instances / media), bits 0..7: inner nodes
+                                  whose box has >= this % of the area of the node above are not emitted (their
+                                  children take their place: box tests that almost always pass), 0 = the plain
+                                  SAH tree, default 90; | RTW_OTREE_NO_CULL: instance and medium leaves do not
+                                  test the instance's world box before its transforms and members (ABI 5,
+                                  formerly padding) */
 } rtw_tuning;
 
 void rtw_tuning_defaults(rtw_tuning* out);

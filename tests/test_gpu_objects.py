@@ -153,15 +153,18 @@ def test_object_counters_equal_reference_traversal(rtw, oracle):
 @pytest.mark.parametrize("name", ["cornell", "cornell_smoke", "quads"])
 def test_object_tree_bit_identical(rtw, name):
     """Object-scene trees with inner nodes flattened away (rtw_tuning.object_tree: nodes whose box has
-    >= that % of the area above are not emitted) render exactly what the plain SAH tree renders: at
-    the default (90), at 50 and 100, in the fused step and the separate kernels, with the exact slab
-    test, and from a camera beyond 7x the scene extent (the launch falls back to the exact test)."""
+    >= that % of the area above are not emitted) and instance / medium leaves that test the instance's
+    padded world box first (off with RTW_OTREE_NO_CULL = 256) render exactly what the plain SAH tree
+    renders: at the default (90), at 50 and 100, without the leaf box test, in the fused step and the
+    separate kernels, with the exact slab test, and from a camera beyond 7x the scene extent (the
+    launch falls back to the exact test)."""
     arr = rtw.flatten(SCENES[name][0](rtw.worlds))
     kw = dict(SCENES[name][1])
     far_at = (278.0, 278.0, -4500.0) if name != "quads" else (0.0, 0.0, 80.0)  # |o| > 7 * extent
     outs = {}
     for tag, tu, far in (("plain", {"object_tree": 0}, False), ("default", {}, False),
                          ("50", {"object_tree": 50}, False), ("100", {"object_tree": 100}, False),
+                         ("nocull", {"object_tree": 90 | 256}, False), ("plain_nocull", {"object_tree": 256}, False),
                          ("split", {"fuse": 0}, False), ("exact", {"fast_box": 0}, False),
                          ("far_plain", {"object_tree": 0}, True), ("far", {}, True)):
         k = dict(kw)
@@ -171,6 +174,6 @@ def test_object_tree_bit_identical(rtw, name):
         world = rtw.World(arr, tuning=tu)
         outs[tag] = render_all(rtw, world, cam, 6, 11)
         world.close()
-    for k in ("default", "50", "100", "split", "exact"):
+    for k in ("default", "50", "100", "nocull", "plain_nocull", "split", "exact"):
         assert np.array_equal(outs["plain"], outs[k]), k
     assert np.array_equal(outs["far_plain"], outs["far"])

@@ -112,6 +112,7 @@ public:
         // quads: Quad.init (objects.zig:201-210)
         g_.quads.assign(d.n_quads, rtw_dev_quad{});
         qbox_.resize(d.n_quads);
+        qtrue_.resize(d.n_quads);
         for (uint32_t i = 0; i < d.n_quads; i++) {
             const rtw_quad& q = d.quads[i];
             if (q.material >= d.n_materials) return RTW_E_INVALID;
@@ -135,6 +136,13 @@ public:
             }
             o.mat = q.material;
             qbox_[i] = box_pad(box_from_points(q.q, far));
+            // the reference's box spans one diagonal only (objects.zig:210): a quad whose u, v are not
+            // axis-aligned can reach outside it.  qtrue_: the box of all four corners.
+            float qu[3], qv[3];
+            for (int k = 0; k < 3; k++) { qu[k] = q.q[k] + q.u[k]; qv[k] = q.q[k] + q.v[k]; }
+            qtrue_[i] = box_union(box_from_points(q.q, far), box_from_points(qu, qv));
+            for (int k = 0; k < 3; k++)
+                if (qtrue_[i].mn[k] < qbox_[i].mn[k] || qtrue_[i].mx[k] > qbox_[i].mx[k]) loose_ = true;
         }
         if (d.n_quads) g_.feat |= RTW_F_GEOM;
         // instance members
@@ -148,6 +156,7 @@ public:
         // instances: HittableList box then the transform chain (innermost first)
         g_.insts.assign(d.n_instances, rtw_dev_instance{});
         ibox_.resize(d.n_instances);
+        itrue_.resize(d.n_instances);
         for (uint32_t i = 0; i < d.n_instances; i++) {
             const rtw_instance& in = d.instances[i];
             if (in.count == 0 || in.count > 127 || in.first > d.n_members || in.count > d.n_members - in.first ||
@@ -157,13 +166,19 @@ public:
             o.first = in.first;
             o.count = in.count;
             o.n_xf = in.n_xf;
-            Box b;
+            for (int k = 0; k < 3; k++) {  // no culling unless rtw_build_bvh pads the box (SAH trees)
+                o.box[0][k] = -__builtin_inff();
+                o.box[1][k] = __builtin_inff();
+            }
+            Box b, tb;  // the reference's box; a true bound of the members (for the leaf's own box test)
             if (in.flags & RTW_INST_LIST) {  // HittableList: bounding_box starts as Aabb{} = [0,0]^3
                 for (int k = 0; k < 3; k++) b.mn[k] = b.mx[k] = 0.0f;
                 for (uint32_t m = 0; m < in.count; m++) b = box_union(b, member_box(d.members[in.first + m]));
             } else {
                 b = member_box(d.members[in.first]);
             }
+            tb = member_true_box(d.members[in.first]);
+            for (uint32_t m = 1; m < in.count; m++) tb = box_union(tb, member_true_box(d.members[in.first + m]));
             for (uint32_t k = 0; k < in.n_xf; k++) {
                 const rtw_transform& x = in.xf[k];
                 uint32_t kind = x.kind;
@@ -173,6 +188,8 @@ public:
                         o.xf[k][1 + c] = x.v[c];
                         b.mn[c] = b.mn[c] + x.v[c];
                         b.mx[c] = b.mx[c] + x.v[c];
+                        tb.mn[c] = tb.mn[c] + x.v[c];
+                        tb.mx[c] = tb.mx[c] + x.v[c];
                     }
                 } else if (x.kind == RTW_XF_ROTATE_Y) {  // RotateY.init
                     const float pi = 3.1415926535897932385f;
@@ -182,11 +199,13 @@ public:
                     o.xf[k][2] = cs;
                     o.xf[k][3] = 0.0f;
                     b = rotate_y_box(b, sn, cs);
+                    tb = rotate_y_box(tb, sn, cs);
                 } else {
                     return RTW_E_INVALID;
                 }
             }
             ibox_[i] = b;
+            itrue_[i] = tb;
         }
         if (d.n_instances) g_.feat |= RTW_F_GEOM;
         // media: ConstantMedium (objects.zig:445-464)
@@ -225,6 +244,11 @@ public:
     }
 
     const std::vector<Obj>& objects() const { return objs_; }
+    // a bound of every point of instance i's members in world space (up to rounding)
+    const Box& instance_true_box(uint32_t i) const { return itrue_[i]; }
+    // some quad reaches outside its reference box (objects.zig:210): boxes are then not bounds, and a walk
+    // that skips inner nodes (object_tree flattening) could find hits the plain tree's boxes cull
+    bool loose_boxes() const { return loose_; }
 
     // leaf record of a world object (rtw_layout.h)
     rtw_node leaf(const Obj& o, uint32_t skip) const {
@@ -252,6 +276,7 @@ public:
 
 private:
     Box member_box(const rtw_object& m) const { return m.kind == RTW_OBJ_SPHERE ? sbox_[m.index] : qbox_[m.index]; }
+    Box member_true_box(const rtw_object& m) const { return m.kind == RTW_OBJ_SPHERE ? sbox_[m.index] : qtrue_[m.index]; }
     Box object_box(const rtw_object& r) const {
         switch (r.kind) {
         case RTW_OBJ_SPHERE: return sbox_[r.index];
@@ -284,7 +309,8 @@ private:
 
     const rtw_scene_desc& d_;
     rtw_geometry& g_;
-    std::vector<Box> sbox_, qbox_, ibox_, mbox_;
+    std::vector<Box> sbox_, qbox_, ibox_, mbox_, qtrue_, itrue_;
+    bool loose_ = false;
     std::vector<Obj> objs_;
 };
 
@@ -643,7 +669,7 @@ int rtw_build_bvh(const rtw_scene_desc& desc, std::vector<rtw_node>& nodes, rtw_
     Geometry geo(desc, geom);
     if (int rc = geo.build()) return rc;
     if (desc.bvh_mode == RTW_BVH_SAH) {
-        SahBuilder b(desc, geo, nodes, sah_max_leaf, hoist != 0, (float)flatten_pct / 100.0f);
+        SahBuilder b(desc, geo, nodes, sah_max_leaf, hoist != 0, geo.loose_boxes() ? 0.0f : (float)flatten_pct / 100.0f);
         b.build(orders);
         if (n_hoisted) *n_hoisted = b.hoisted();
         if (depth) *depth = b.depth();
@@ -668,6 +694,21 @@ int rtw_build_bvh(const rtw_scene_desc& desc, std::vector<rtw_node>& nodes, rtw_
             for (int k = 0; k < 3; k++) {
                 n.a[k] -= pad;
                 n.b[k] += pad;
+            }
+        }
+        // Instance leaves test their own world box before the transforms and member tests (object_leaf):
+        // a hit the leaf accepts at t in [0.001, closest] is a point computed through the transform chain
+        // (Translate / RotateY, objects.zig:314-326, 401-435) and the member tests -- or, for a medium whose
+        // boundary is the instance, a point between two boundary hits (objects.zig:470-507) -- so it lies
+        // within a few ulp of (|o| + t|d|) <= 15E of the box, not exactly inside it.  E * 2^-12 on top of the
+        // slab test's pad covers 273 ulp of 15E for every origin the fast test admits (|o| <= 7E); the
+        // exact test (far origins, tuning.fast_box = 0) never culls.
+        const float ipad = pad + e * 2.4414062e-04f;  // + 2^-12
+        for (uint32_t i = 0; i < (uint32_t)geom.insts.size(); i++) {
+            const Box& b = geo.instance_true_box(i);
+            for (int k = 0; k < 3; k++) {
+                geom.insts[i].box[0][k] = b.mn[k] - ipad;
+                geom.insts[i].box[1][k] = b.mx[k] + ipad;
             }
         }
         if (box_pad) *box_pad = pad;

@@ -175,7 +175,8 @@ int rtw_scene_create_ex(const rtw_scene_desc* d, int device, const rtw_tuning* t
     if (tu.kernel > RTW_KERNEL_SIMPLE) return fail(RTW_E_INVALID, "tuning.kernel out of range");
     if (tu.bvh_orders != 0 && tu.bvh_orders != 1 && tu.bvh_orders != 8) return fail(RTW_E_INVALID, "tuning.bvh_orders must be 0, 1 or 8");
     if (tu.wf_iters < 1 || tu.wf_iters > RTW_WF_MAX_ITERS) return fail(RTW_E_INVALID, "tuning.wf_iters out of range");
-    if (tu.object_tree > 100) return fail(RTW_E_INVALID, "tuning.object_tree out of range (0..100)");
+    if ((tu.object_tree & 0xFFu) > 100 || (tu.object_tree & ~(0xFFu | RTW_OTREE_NO_CULL)))
+        return fail(RTW_E_INVALID, "tuning.object_tree: 0..100 [| RTW_OTREE_NO_CULL]");
     if (tu.sort_bits > RTW_WF_BUCKET_BITS) return fail(RTW_E_INVALID, "tuning.sort_bits out of range");
     if (tu.mega_shade_min < 1 || tu.mega_shade_min > 64) return fail(RTW_E_INVALID, "tuning.mega_shade_min out of range");
     if (tu.mega_waves != 1 && tu.mega_waves != 6 && tu.mega_waves != 8) return fail(RTW_E_INVALID, "tuning.mega_waves must be 1, 6 or 8");
@@ -222,7 +223,7 @@ int rtw_scene_create_ex(const rtw_scene_desc* d, int device, const rtw_tuning* t
     if (tu.bvh_orders) orders = (d->bvh_mode == RTW_BVH_SAH && tu.bvh_orders == 8) ? 8u : 1u;
     uint32_t n_hoisted = 0;
     int rc = rtw_build_bvh(*d, ctx->nodes_host, geom, &depth, &draws, &ctx->box_pad, &ctx->extent, orders,
-                           tu.sah_max_leaf, tu.hoist && !objects ? 1u : 0u, &n_hoisted, objects ? tu.object_tree : 0u);
+                           tu.sah_max_leaf, tu.hoist && !objects ? 1u : 0u, &n_hoisted, objects ? (tu.object_tree & 0xFFu) : 0u);
     if (rc != RTW_OK) {
         delete ctx;
         return fail(rc, "BVH build failed (bad object graph or bvh_mode)");
@@ -440,6 +441,7 @@ int rtw_scene_create_ex(const rtw_scene_desc* d, int device, const rtw_tuning* t
     // SAH trees: FMA slab test on the padded boxes (only enlarges the set of visited nodes;
     // reference trees keep the exact aabb.zig walk)
     L.fast_box = ctx->box_pad > 0 && tu.fast_box ? 1u : 0u;
+    L.inst_cull = (tu.object_tree & RTW_OTREE_NO_CULL) ? 0u : 1u;  // consulted only with fast_box
     if (host) {  // the exact aabb.zig slab test and IEEE sphere test (the hardware estimates are device-only)
         L.fast_box = 0;
         L.fast_reject = 0;

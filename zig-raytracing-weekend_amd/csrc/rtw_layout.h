@@ -57,13 +57,16 @@ struct rtw_dev_quad {
 };
 static_assert(sizeof(rtw_dev_quad) == 80, "quad record must be 80 bytes");
 
-// 64 B: members[first .. first+count) (RTW_REF), xf[k] = {bits(kind), a, b, c}:
+// 96 B: members[first .. first+count) (RTW_REF), xf[k] = {bits(kind), a, b, c}:
 // translate (a, b, c) = offset; rotate_y a = sin, b = cos.  xf[0] innermost.
+// box: the instance's world box (RotateY/Translate.init) padded for the leaf's own FMA slab test
+// (rtw_build_bvh; SAH trees only, else +-inf): box[0] = min.xyz, box[1] = max.xyz
 struct rtw_dev_instance {
     uint32_t first, count, n_xf, _p;
     float xf[3][4];
+    float box[2][4];
 };
-static_assert(sizeof(rtw_dev_instance) == 64, "instance record must be 64 bytes");
+static_assert(sizeof(rtw_dev_instance) == 96, "instance record must be 96 bytes");
 
 // 16 B: ConstantMedium
 struct rtw_dev_medium {
