@@ -177,3 +177,30 @@ def test_object_tree_bit_identical(rtw, name):
     for k in ("default", "50", "100", "nocull", "plain_nocull", "split", "exact"):
         assert np.array_equal(outs["plain"], outs[k]), k
     assert np.array_equal(outs["far_plain"], outs["far"])
+
+
+def tilted_instance_world(rtw):
+    """Cornell plus an instance with a skewed quad (u, v not axis-aligned): its reference box (one diagonal,
+    objects.zig:210) does not bound it, so flattening stays off and the leaf's box test uses the
+    four-corner bound."""
+    S = rtw.scene
+    objs = rtw.worlds.cornell_box()
+    mat = S.Lambertian.init(S.SolidColor.init([0.2, 0.4, 0.8]))
+    roof = S.HittableList.init()
+    roof.add(S.Quad.init([0, 0, 0], [100, 100, 0], [-50, 0, 120], mat))
+    roof.add(S.Quad.init([100, 100, 0], [100, -100, 0], [0, 0, 120], mat))
+    roof.add(S.Sphere.init([100, 40, 60], 30, mat))
+    objs.append(S.Translate.init(S.RotateY.init(roof, 25), [150, 300, 250]))
+    return objs
+
+
+def test_object_tree_bit_identical_tilted_instance(rtw):
+    arr = rtw.flatten(tilted_instance_world(rtw))
+    cam = rtw.Camera(image_width=72, samples_per_pixel=6, max_depth=50, **SCENES["cornell"][1]).init()
+    outs = []
+    for tu in ({"object_tree": 0}, {}, {"object_tree": 90 | 256}, {"object_tree": 256}, {"fuse": 0}):
+        world = rtw.World(arr, tuning=tu)
+        outs.append(render_all(rtw, world, cam, 6, 13))
+        world.close()
+    for k in range(1, len(outs)):
+        assert np.array_equal(outs[0], outs[k]), k

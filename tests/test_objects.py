@@ -155,3 +155,29 @@ def test_oracle_object_scene_renders(oracle, rtw, scene):
                              lookfrom=(278, 278, -800), lookat=(278, 278, 0), defocus_angle=0.0)
     out = ow.render_pixels(ocam, 0, np.arange(32 * 32, dtype=np.uint32), 0, 4, threads=4)
     assert np.isfinite(out).all() and out[:, :3].max() > 0
+
+
+def test_object_tree_flattening_node_counts(rtw):
+    """rtw_tuning.object_tree: Cornell's walls make four inner nodes under the root the whole room
+    again; the default (90 %) leaves them out.  A scene with a quad that reaches outside its reference
+    box (not axis-aligned) keeps the plain tree."""
+    import ctypes as C
+    import numpy as np
+
+    def n_nodes(objs, tu):
+        world = rtw.World(rtw.flatten(objs), device=-1, tuning=tu)
+        buf = np.zeros((256, 8), np.float32)
+        n = C.c_uint32()
+        rtw._abi.check(rtw.lib().rtw_scene_nodes(world.handle, buf.ctypes.data, 256, C.byref(n)), "rtw_scene_nodes")
+        world.close()
+        return n.value
+
+    assert n_nodes(rtw.worlds.cornell_box(), {"object_tree": 0}) == 15
+    assert n_nodes(rtw.worlds.cornell_box(), None) == 11
+    S = rtw.scene
+    objs = rtw.worlds.cornell_box()
+    mat = S.Lambertian.init(S.SolidColor.init([0.2, 0.4, 0.8]))
+    roof = S.HittableList.init()
+    roof.add(S.Quad.init([0, 0, 0], [100, 100, 0], [-50, 0, 120], mat))
+    objs.append(S.Translate.init(S.RotateY.init(roof, 25), [150, 300, 250]))
+    assert n_nodes(objs, None) == n_nodes(objs, {"object_tree": 0})
