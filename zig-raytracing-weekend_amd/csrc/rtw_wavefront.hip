@@ -1592,7 +1592,7 @@ void wf_run(const rtw_launch& L, const rtw_wf& W0, hipStream_t st, int n_cu, rtw
         const size_t need = (size_t)L.n_nodes * L.n_orders * 32u;
         if (!fclds && L.wf_lds && need <= RTW_WF_LDS_MAX) flds = (need + 511u) / 512u * 512u;
         // measured: fused wins on C2 (+8.5 %), C5 (+24 %), Cornell (+2 %) and, since the
-        // round-3 queues and object trees, Cornell smoke (media: +15 %); through L1/L2 (C4, RTW_WF_FUSE
+        // round-3 queues and object trees, Cornell smoke (media: +23 %); through L1/L2 (C4, RTW_WF_FUSE
         // bit 2) it loses (-13 %)
         if ((fclds || flds) || (L.wf_fuse & 4u)) {
             wf_run_fused<FEAT>(L, W0, st, n_cu, fclds, flds, T);
