@@ -559,8 +559,17 @@ RTW_DHD bool medium_t(const rtw_launch& L, uint32_t idx, const Ray& r, float tmi
                                          uint64_t mkey, float& t) {
     const rtw_dev_medium m = L.media[idx];
     float t1, t2;
-    if (!boundary_t<FEAT>(L, m.boundary, r, -kInf, kInf, t1)) return false;  // intervals.universe
-    if (!boundary_t<FEAT>(L, m.boundary, r, t1 + 0.0001f, kInf, t2)) return false;
+    if (RTW_REF_KIND(m.boundary) == RTW_OBJ_INSTANCE) {
+        // both boundary queries see the same object-space ray: transform it once
+        const rtw_dev_instance* in = L.insts + RTW_REF_INDEX(m.boundary);
+        const Ray ro = inst_to_object(in, r);
+        uint32_t sub;
+        if (!list_t<FEAT>(L, in, ro, -kInf, kInf, t1, sub)) return false;  // intervals.universe
+        if (!list_t<FEAT>(L, in, ro, t1 + 0.0001f, kInf, t2, sub)) return false;
+    } else {
+        if (!boundary_t<FEAT>(L, m.boundary, r, -kInf, kInf, t1)) return false;  // intervals.universe
+        if (!boundary_t<FEAT>(L, m.boundary, r, t1 + 0.0001f, kInf, t2)) return false;
+    }
     if (t1 < tmin) t1 = tmin;
     if (t2 > tmax) t2 = tmax;
     if (t1 >= t2) return false;
