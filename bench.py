@@ -28,9 +28,13 @@ sys.path.insert(0, REPO)
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 N_SIMD = 256 * 4               # 256 CUs x 4 SIMDs
 CLOCK_HZ = 2.4e9               # max engine clock (MI355X_MICROARCH.md)
-# one non-packed wave64 VALU instruction per SIMD per quad-cycle (measured: SQ_ACTIVE_INST_VALU, in
-# quad-cycles, equals SQ_INSTS_VALU on these kernels) -> 16 lane-ops per SIMD per clock
-VALU_PEAK_TLOPS = round(N_SIMD * 16 * CLOCK_HZ / 1e12, 3)   # 39.322 T lane-op/s
+# VALU issue ceiling, measured on the box (diag/valu_peak.hip -> profiles/r4_valu_peak/): independent
+# v_fma_f32 / v_add_f32 chains at 8 waves/SIMD issue one wave64 instruction per SIMD every 2.09 / 2.06
+# clocks (74.7 / 75.8 T lane-op/s at the 2.37-2.38 GHz the chip holds), as MI355X_MICROARCH.md:54,473
+# state; v_pk_fma_f32 takes 4 clocks (the same lane-FMA rate).  Peak = 32 lanes per SIMD per clock.
+VALU_CYCLES_PER_INST = 2.0
+VALU_PEAK_TLOPS = round(N_SIMD * 64 / VALU_CYCLES_PER_INST * CLOCK_HZ / 1e12, 3)   # 78.643 T lane-op/s
+VALU_PEAK_SRC = "profiles/r4_valu_peak/summary.txt"
 NODE_BYTES = 32                # one BVH node / leaf record (rtw_layout.h)
 ROWS_PER_BLOCK = 8   # row blocks interleaved over ranks: C2 at 8 GPUs 6.97x predicted (16: 6.87x; tools/shard_sim.py)
 
@@ -51,6 +55,12 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline duration")
     ap.add_argument("--cpu-threads", type=int, default=8, help="reference uses 8 render threads (main.zig:41)")
+    ap.add_argument("--host-backend", action="store_true",
+                    help="render every rank's shard on a host context (RTW_DEVICE_CPU, rtw_render_rows) and gather "
+                         "over gloo: the same torchrun flow (shards, gather, reassembly, timing, JSON line) with no "
+                         "GPU, for the CPU tests; never a headline number")
+    ap.add_argument("--host-threads", type=int, default=2, help="--host-backend: render threads per rank")
+    ap.add_argument("--dump-image", default="", help="rank 0 saves the reassembled float4 frame (.npy)")
     return ap.parse_args()
 
 
@@ -70,20 +80,34 @@ def main():
         raise SystemExit("--gpus N > 1: launch one process per GPU with torchrun (the driver's scaling run), or "
                          "pass --single-process for the one-process rtw_multi path")
     n_shards = args.gpus if single else world_size
-    torch.cuda.set_device(local_rank)
+    host = args.host_backend
+    if host and single:
+        raise SystemExit("--host-backend is the torchrun (one process per rank) flow")
+    if not host:
+        torch.cuda.set_device(local_rank)
     distributed = world_size > 1
-    if distributed:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    if distributed:  # backend "nccl" is RCCL on ROCm; gloo carries the host-backend rehearsal
+        if host:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    def sync():
+        if not host:
+            torch.cuda.synchronize()
 
     pkg = importlib.import_module("zig-raytracing-weekend_amd")
     L = pkg.lib()
+    build_id = L.rtw_build_id().decode()
     cfg = pkg.configs.CONFIGS[args.config]
     objs = cfg.objects()
     bvh_mode = {"sah": pkg._abi.RTW_BVH_SAH, "reference": pkg._abi.RTW_BVH_REFERENCE}[args.bvh]
     arr = pkg.flatten(objs, bvh_mode=bvh_mode)
     t0 = time.time()
     tun = json.loads(args.tuning) if args.tuning else None
-    world = pkg.World(arr, device=local_rank, tuning=tun)
+    if host:
+        tun = dict(tun or {}, cpu_threads=args.host_threads)
+    world = pkg.World(arr, device=pkg._abi.RTW_DEVICE_CPU if host else local_rank, tuning=tun)
     # single-process multi-GPU: one context per device + the RCCL communicators of rtw_multi
     worlds = [world] + [pkg.World(arr, device=k, tuning=tun) for k in range(1, n_shards)] if single else [world]
     multi = pkg.distributed.MultiDeviceRender(worlds, ROWS_PER_BLOCK) if single else None
@@ -97,7 +121,7 @@ def main():
         rccl = {"mode": "single_gpu", "rccl_ranks": None, "backend": None}
     build_s = time.time() - t0
     # the reference topology (bvh.zig) defines the algorithmic bytes
-    world_ref = pkg.World(pkg.flatten(objs, bvh_mode=pkg._abi.RTW_BVH_REFERENCE), device=local_rank)
+    world_ref = None if host else pkg.World(pkg.flatten(objs, bvh_mode=pkg._abi.RTW_BVH_REFERENCE), device=local_rank)
     cam = cfg.camera()
     if args.spp:
         cam.samples_per_pixel = args.spp
@@ -105,10 +129,12 @@ def main():
     W, H, spp = cam.derived.image_width, cam.derived.image_height, cam.samples_per_pixel
     stats = world.stats()
 
-    stream = torch.cuda.Stream()          # explicit stream: the kernels and the timing events share it
-    torch.cuda.set_stream(stream)
+    stream = None if host else torch.cuda.Stream()  # explicit stream: the kernels and the timing events share it
+    if not host:
+        torch.cuda.set_stream(stream)
     # the shard this process renders (single-process mode: device 0's, for the counted and timing passes)
-    shard = pkg.distributed.ShardedRender(world, cam, rank, n_shards, ROWS_PER_BLOCK)
+    shard = pkg.distributed.ShardedRender(world, cam, rank, n_shards, ROWS_PER_BLOCK,
+                                          device=torch.device("cpu") if host else None)
     my_rows = shard.rows
     assert my_rows == L.rtw_shard_rows(H, ROWS_PER_BLOCK, n_shards, rank)
     frame = torch.zeros((W * H, 4), dtype=torch.float32, device="cuda") if single else None
@@ -134,15 +160,18 @@ def main():
     # ---- algorithmic bytes of one step: counted pass on the reference topology (the device
     # walk of a reference-topology tree visits exactly the nodes bvh.zig's recursion visits)
     def counted(w):
+        keys = ("nodes", "leaves", "rays", "samples", "nan", "tail_rays")
+        if host:  # host contexts keep no device counters
+            return dict.fromkeys(keys, 0)
         cnt = torch.zeros(8, dtype=torch.int64, device="cuda")
         render_step(cnt.data_ptr(), w)
         torch.cuda.synchronize()
         c = cnt.cpu().numpy()
-        return {k: int(c[getattr(pkg._abi, "RTW_STAT_" + k.upper())]) for k in ("nodes", "leaves", "rays", "samples",
-                                                                                 "nan", "tail_rays")}
+        return {k: int(c[getattr(pkg._abi, "RTW_STAT_" + k.upper())]) for k in keys}
     cref = counted(world_ref)
     cdev = counted(world)
-    world_ref.close()
+    if world_ref is not None:
+        world_ref.close()
     nodes, leaves, rays, samples = cref["nodes"], cref["leaves"], cref["rays"], cref["samples"]
     nan_count = cdev["nan"]
     pixels = my_rows * W
@@ -151,36 +180,47 @@ def main():
     for _ in range(args.warmup):
         frame_step()
         gather_step()
-    torch.cuda.synchronize()
+    sync()
 
     # per-kernel HIP events, recorded by the library on the render stream around every launch
     timings = [pkg._abi.RtwKernelTiming() for _ in range(args.steps)]
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    ev = ([] if host else
+          [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)])
+    host_ms = []
     if distributed:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     t_start = time.perf_counter()
     for k in range(args.steps):
-        ev[k][0].record(stream)
-        if single:
-            frame_step()
+        if host:
+            t0k = time.perf_counter()
+            render_step()
+            host_ms.append((time.perf_counter() - t0k) * 1e3)
         else:
-            render_step(timing=timings[k])
-        ev[k][1].record(stream)
+            ev[k][0].record(stream)
+            if single:
+                frame_step()
+            else:
+                render_step(timing=timings[k])
+            ev[k][1].record(stream)
         gather_step()
-    torch.cuda.synchronize()
+    sync()
     if distributed:
         dist.barrier()
     elapsed = time.perf_counter() - t_start
-    kernel_ms = [a.elapsed_time(b) for a, b in ev]
+    kernel_ms = host_ms if host else [a.elapsed_time(b) for a, b in ev]
     if single:  # per-kernel HIP events of device 0's shard, rendered alone after the timed region
         for k in range(args.steps):
             render_step(timing=timings[k])
         torch.cuda.synchronize()
     if distributed:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if host else "cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    if args.dump_image and rank == 0:  # the reassembled frame (world size 1: this rank's tile is the frame)
+        if not distributed:
+            shard.gather()
+        np.save(args.dump_image, shard.image.cpu().numpy())
 
     if single:
         multi.close()
@@ -205,8 +245,9 @@ def main():
     # fused path (compact LDS stage): one gen+trace+shade kernel per iteration, timed as "trace"
     fused = kcalls["trace"] > 0 and kcalls["shade"] == 0
     knames = {"trace": "wf_step_clds" if fused else "wf_trace", "tail": "wf_tail", "mega": "render_persistent_v1"}
-    traffic, traffic_src = pmc_traffic(args, {"trace": "wf_step" if fused else "wf_trace", "tail": "wf_tail",
-                                              "mega": "render_"}.get(dom, dom))
+    traffic, traffic_src = (None, None) if host else pmc_traffic(
+        args, {"trace": "wf_step" if fused else "wf_trace", "tail": "wf_tail", "mega": "render_"}.get(dom, dom),
+        build_id)
 
     # ---- roofline of the dominant kernel: VALU issue.  The kernel is VALU-bound
     # (C2: VALU busy 0.85 of the quad-cycles, HBM 0.18 of peak), so `frac` = useful lane-instructions
@@ -215,10 +256,12 @@ def main():
     # the launch time is this run's HIP events.  HBM traffic (PMC) and the SURVEY §8d algorithmic
     # bytes are reported beside it; the latter is a diagnostic, not a fraction of any peak.
     dom_kind = {"trace": "wf_step" if fused else "wf_trace", "tail": "wf_tail", "mega": "render_"}.get(dom, dom)
-    valu, valu_src = pmc_valu(args, dom_kind, single)
+    valu, valu_src = (None, None) if host else pmc_valu(args, dom_kind, build_id, single)
     lane_ops = valu.get("lane_ops") if valu else None
     achieved_valu = lane_ops / dom_launch_s / 1e12 if (lane_ops and dom_launch_s > 0) else None
-    issue = (valu["active_inst_valu"] * 4 / (N_SIMD * dom_launch_s * CLOCK_HZ)) if (valu and dom_launch_s > 0) else None
+    # fraction of the SIMD cycles spent issuing VALU at the measured 2-clock wave64 rate
+    issue = (valu["insts_valu"] * VALU_CYCLES_PER_INST / (N_SIMD * dom_launch_s * CLOCK_HZ)
+             if (valu and dom_launch_s > 0) else None)
     hbm_achieved = traffic / dom_launch_s / 1e9 if (traffic and dom_launch_s > 0) else None
     roofline = {
         "bound": "valu",
@@ -235,13 +278,15 @@ def main():
         "valu": {"source": valu_src, "kind": dom_kind, "lane_ops_per_launch": lane_ops,
                  "lane_util": round(valu["lane_util"], 4) if valu else None,
                  "issue_busy": round(issue, 4) if issue is not None else None,
-                 "peak_def": "256 CU x 4 SIMD x 16 lanes x 2.4 GHz: one non-packed VALU wave-instruction per "
-                             "SIMD per quad-cycle (SQ_ACTIVE_INST_VALU); the 157.3 TFLOP/s datasheet figure counts "
-                             "packed FMAs (x4)",
-                 "frac_of_packed_fp32_peak": round(achieved_valu * 2 / 157.3, 4) if achieved_valu else None},
+                 "peak_def": "256 CU x 4 SIMD x 32 lanes x 2.4 GHz: one wave64 VALU instruction per SIMD every 2 "
+                             "clocks, measured at 8 waves/SIMD (v_fma_f32 2.09, v_add_f32 2.06 clocks); = the "
+                             "157.3 TFLOP/s datasheet figure / 2 flops per FMA",
+                 "peak_source": VALU_PEAK_SRC,
+                 "build_id": build_id,
+                 "frac_of_fp32_fma_peak": round(achieved_valu * 2 / 157.3, 4) if achieved_valu else None},
         "hbm": {"achieved": round(hbm_achieved, 2) if hbm_achieved is not None else None, "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(hbm_achieved / HBM_PEAK_GBS, 4) if hbm_achieved is not None else None,
-                "traffic_per_launch": traffic, "source": traffic_src, "kind": dom_kind},
+                "traffic_per_launch": traffic, "source": traffic_src, "kind": dom_kind, "build_id": build_id},
         "kernel_ms_per_step": {n: round(v / args.steps, 3) for n, v in kms.items() if kcalls[n]},
         "launches": {n: v // args.steps for n, v in kcalls.items() if v},
         "algorithmic": {"note": "SURVEY 8d bytes of the reference-topology walk (53 nodes/ray x 32 B) per second; "
@@ -282,15 +327,18 @@ def main():
             "config": {"workload": cfg.description, "config_id": args.config, "width": W, "height": H,
                        "spp": spp, "max_depth": cam.max_depth, "objects": len(objs), "bvh_nodes": stats["n_nodes"],
                        "bvh_depth": stats["depth"], "parallelism": f"row-interleaved tiles x{n_shards}"
-                       + (" + RCCL gather" if distributed else "")
+                       + ((" + gloo gather (host backend)" if host else " + RCCL gather") if distributed else "")
                        + (" (one process, rtw_multi: grouped RCCL send/recv)" if single else ""),
                        "rows_per_block": ROWS_PER_BLOCK, "exchange": rccl,
-                       "timed_scope": "device API (rtw_render_rows_device / rtw_render_multi_device) into an "
-                                      "HBM-resident float4 accumulator; no host copy inside the timed region"},
+                       "timed_scope": ("host contexts (rtw_render_rows) into host tiles, gathered over gloo: the "
+                                       "CPU rehearsal of the torchrun flow" if host else
+                                       "device API (rtw_render_rows_device / rtw_render_multi_device) into an "
+                                       "HBM-resident float4 accumulator; no host copy inside the timed region")},
             "roofline": roofline,
             "cpu_baseline": cpu,
             "nan_samples": nan_count,
             "scene_build_s": round(build_s, 4),
+            "build_id": build_id,
         }
         print(json.dumps(line), flush=True)
     world.close()
@@ -298,30 +346,43 @@ def main():
         dist.destroy_process_group()
 
 
-def pmc_traffic(args, kernel_prefix):
+def pmc_build_id(data):
+    """The rtw_build_id() of the library a committed PMC pass was taken on (tools/pmc_*_summary.py)."""
+    b = data.get("_build") if isinstance(data, dict) else None
+    return b.get("build_id") if isinstance(b, dict) else None
+
+
+def pmc_traffic(args, kernel_prefix, build_id):
     """HBM bytes per launch of the dominant kernel from the committed PMC pass
     (tools/pmc_traffic.sh -> profiles/pmc_traffic_<config>_<bvh>.json; FETCH_SIZE x2 + WRITE_SIZE,
-    MI355X_MICROARCH.md § HBM).  PMC counters cannot be read inside the timed run."""
+    MI355X_MICROARCH.md § HBM).  PMC counters cannot be read inside the timed run.  A pass taken on
+    another build of the library (its _build.build_id differs from rtw_build_id()) is not used."""
     f = os.path.join(REPO, "profiles", f"pmc_traffic_{args.config}_{args.bvh}.json")
     if args.spp or args.tuning or os.environ.get("RTW_LIB") or not os.path.exists(f):
         return None, None
     data = json.load(open(f))
+    if pmc_build_id(data) != build_id:
+        return None, f"{os.path.relpath(f, REPO)}: build {pmc_build_id(data)} != loaded {build_id} (stale, unused)"
     for name, e in data.items():
-        if name.startswith(kernel_prefix):
+        if name.startswith(kernel_prefix) and isinstance(e, dict):
             return round(e["traffic_bytes"]), os.path.relpath(f, REPO)
     return None, None
 
 
-def pmc_valu(args, kind, single=False):
+def pmc_valu(args, kind, build_id, single=False):
     """VALU counters per launch of the dominant kernel kind from the committed SQ pass
     (tools/pmc_valu.sh -> profiles/pmc_valu_<config>_<bvh>.json).  Returns (entry, path).
     The pass was taken with the product defaults on one device: an A/B build (--tuning, RTW_LIB) or the
-    single-process multi path runs other kernels, so no roofline is derived from it there."""
+    single-process multi path runs other kernels, so no roofline is derived from it there; nor from a
+    pass of another build of the library (roofline.frac is then null)."""
     f = os.path.join(REPO, "profiles", f"pmc_valu_{args.config}_{args.bvh}.json")
     if args.spp or args.tuning or single or os.environ.get("RTW_LIB") or not os.path.exists(f):
         return None, None
-    for name, e in json.load(open(f)).items():
-        if name.startswith(kind) and e.get("lane_ops"):
+    data = json.load(open(f))
+    if pmc_build_id(data) != build_id:
+        return None, f"{os.path.relpath(f, REPO)}: build {pmc_build_id(data)} != loaded {build_id} (stale, unused)"
+    for name, e in data.items():
+        if name.startswith(kind) and isinstance(e, dict) and e.get("lane_ops"):
             return e, os.path.relpath(f, REPO)
     return None, None
 

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define RTW_ABI_VERSION 5
+#define RTW_ABI_VERSION 6
 
 enum rtw_status {
     RTW_OK = 0,
@@ -265,6 +265,9 @@ enum { RTW_STAT_RAYS = 0, RTW_STAT_NODES = 1, RTW_STAT_LEAVES = 2, RTW_STAT_SAMP
        RTW_STAT_COUNT = 8 };
 
 int rtw_version(void);
+/* ABI 6: the library's build id, the first 16 hex digits of the sha256 of its sources (csrc/Makefile);
+ * PMC passes under profiles/ record it, and bench.py derives no roofline from a pass of another build. */
+const char* rtw_build_id(void);
 const char* rtw_last_error(void);
 int rtw_device_count(int* out);
 
@@ -484,6 +487,8 @@ typedef struct rtw_scene_stats {
     uint64_t device_bytes;
     uint32_t axis_draws;
     uint32_t n_hoisted;        /* spheres emitted ahead of the tree (rtw_tuning.hoist) */
+    float extent;              /* ABI 6: E = max |coordinate| over every object box and inner node (SAH) */
+    float box_pad;             /* ABI 6: E * 2^-19, the inner-box pad of the FMA slab test (0: exact walk) */
 } rtw_scene_stats;
 int rtw_scene_stats_get(rtw_ctx* ctx, rtw_scene_stats* out);
 /* Copies the flattened node array (32 B per node) to host. */

@@ -161,3 +161,41 @@ def test_gather_of_rendered_shards_gloo(rtw, world_size, rpb):
     world.close()
     assert (ref[:, 3] == spp).all()
     assert np.array_equal(img, ref)
+
+
+def _bench_line(out):
+    import json
+    return json.loads([ln for ln in out.splitlines() if ln.startswith("{")][-1])
+
+
+@pytest.mark.parametrize("world_size", [2, 3])
+def test_bench_torchrun_flow_on_host_backend(tmp_path, world_size):
+    """bench.py's own N > 1 code path, end to end without a GPU: torchrun starts one process per rank,
+    each renders its row-interleaved shard (--host-backend: a host context, rtw_render_rows), the tiles
+    meet on rank 0 in one dist.gather (gloo), rank 0 reassembles the frame, the ranks' times are maxed and
+    one JSON line is printed.  The frame equals bench.py's one-process frame bit for bit."""
+    import subprocess
+    import sys
+
+    from conftest import REPO
+    common = ["--host-backend", "--config", "c1", "--spp", "2", "--steps", "1", "--warmup", "0",
+              "--no-cpu-baseline"]
+    one = tmp_path / "one.npy"
+    r1 = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), *common, "--dump-image", str(one)],
+                        capture_output=True, text=True, timeout=300, cwd=REPO)
+    assert r1.returncode == 0, r1.stderr[-2000:]
+    many = tmp_path / "many.npy"
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    rn = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world_size}",
+                         "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+                         os.path.join(REPO, "bench.py"), "--gpus", str(world_size), *common,
+                         "--dump-image", str(many)], capture_output=True, text=True, timeout=300, cwd=REPO, env=env)
+    assert rn.returncode == 0, rn.stderr[-2000:]
+    d = _bench_line(rn.stdout)
+    assert d["n_gpus"] == world_size and d["value"] > 0 and d["ms_per_step"] > 0
+    assert d["config"]["exchange"] == {"mode": "torchrun", "rccl_ranks": world_size, "backend": "gloo"}
+    assert (d["config"]["width"], d["config"]["height"]) == (400, 225)
+    assert abs(d["value"] - 400 * 225 * 2 / (d["ms_per_step"] / 1e3) / 1e6) <= 0.01 * d["value"]
+    a, b = np.load(one), np.load(many)
+    assert a.shape == (225, 400, 4) and (a[..., 3] == 2).all()
+    assert np.array_equal(a, b)

@@ -46,14 +46,20 @@ def load(dirname, counter):
     return per, names
 
 
-def bench_launches(dirname, counter):
+def bench_line(dirname, counter):
     for line in open(os.path.join(dirname, f"{counter}.log"), errors="replace"):
         if line.startswith("{"):
             try:
-                return json.loads(line)["roofline"]["launches"]
+                bl = json.loads(line)
+                bl["roofline"]["launches"]
+                return bl
             except (ValueError, KeyError):
                 pass
     return {}
+
+
+def bench_launches(dirname, counter):
+    return bench_line(dirname, counter).get("roofline", {}).get("launches", {})
 
 
 def main():
@@ -74,8 +80,14 @@ def main():
             e[key] = sum(b for b, _ in keep) / max(1, len(keep))
     for k, e in out.items():
         e["traffic_bytes"] = e.get("fetch_bytes", 0) + e.get("write_bytes", 0)
+    # the library build of both passes (bench.py uses no pass of another build)
+    ids = {bench_line(d, c).get("build_id") for c in ("FETCH_SIZE", "WRITE_SIZE")}
+    bl = bench_line(d, "FETCH_SIZE")
+    out["_build"] = {"build_id": ids.pop() if len(ids) == 1 else None, "config": bl.get("config", {}).get("config_id"),
+                     "value": bl.get("value")}
     json.dump(out, open(os.path.join(d, "pmc_traffic.json"), "w"), indent=1, sort_keys=True)
-    for k, e in sorted(out.items(), key=lambda kv: -kv[1]["traffic_bytes"]):
+    print(f"build {out['_build']['build_id']}")
+    for k, e in sorted(((k, e) for k, e in out.items() if not k.startswith("_")), key=lambda kv: -kv[1]["traffic_bytes"]):
         print(f"{k:10s} launches/step {e['launches']:3d}  fetch {e.get('fetch_bytes', 0) / 1e9:8.3f} GB  "
               f"write {e.get('write_bytes', 0) / 1e9:8.3f} GB per launch  ({', '.join(e['kernels'])})")
 

@@ -41,11 +41,14 @@ def main():
                 disp = int(r["Dispatch_Id"])
                 per[disp][FIELDS[c]] += float(r["Counter_Value"])
                 names[disp] = r["Kernel_Name"]
-    launches = {}
+    launches, build = {}, None
     for line in open(os.path.join(d, "valu.log"), errors="replace"):
         if line.startswith("{"):
             try:
-                launches = json.loads(line)["roofline"]["launches"]
+                bl = json.loads(line)
+                launches = bl["roofline"]["launches"]
+                build = {"build_id": bl.get("build_id"), "config": bl["config"].get("config_id"),
+                         "value": bl.get("value")}
             except (ValueError, KeyError):
                 pass
     byk = defaultdict(list)
@@ -67,12 +70,16 @@ def main():
         e["per_launch"] = [{"insts_valu": c.get("insts_valu", 0.0), "gui_active": c.get("gui_active", 0.0),
                             "lane_util": (c.get("thread_cycles_valu", 0.0) / (64.0 * c["active_inst_valu"])
                                           if c.get("active_inst_valu") else None),
-                            # GRBM_GUI_ACTIVE is summed over the 8 XCDs: per-XCD clocks x 1024 SIMDs
-                            "valu_busy": (c.get("active_inst_valu", 0.0) * 4.0 / (1024.0 * c["gui_active"] / 8.0)
+                            # GRBM_GUI_ACTIVE is summed over the 8 XCDs: per-XCD clocks x 1024 SIMDs;
+                            # one wave64 VALU instruction per SIMD per 2 clocks (profiles/r4_valu_peak/)
+                            "valu_busy": (c.get("insts_valu", 0.0) * 2.0 / (1024.0 * c["gui_active"] / 8.0)
                                           if c.get("gui_active") else None)} for c, _ in keep]
         out[k] = e
+    # the library build the pass was taken on (bench.py uses no pass of another build)
+    out["_build"] = build or {"build_id": None}
     json.dump(out, open(os.path.join(d, "pmc_valu.json"), "w"), indent=1, sort_keys=True)
-    for k, e in sorted(out.items(), key=lambda kv: -kv[1]["insts_valu"]):
+    print(f"build {out['_build'].get('build_id')}")
+    for k, e in sorted(((k, e) for k, e in out.items() if not k.startswith("_")), key=lambda kv: -kv[1]["insts_valu"]):
         print(f"{k:10s} launches/step {e['launches']:3d}  VALU insts {e['insts_valu']:.4g}  "
               f"lane_util {e.get('lane_util', 0):.3f}  lane-ops {e.get('lane_ops', 0):.4g}  "
               f"GUI_ACTIVE {e['gui_active']:.4g}  ({', '.join(e['kernels'])})")
@@ -81,7 +88,7 @@ def main():
                 lu = pl["lane_util"]
                 vb = pl["valu_busy"]
                 print(f"    launch {j}: VALU insts {pl['insts_valu']:.4g}  lane_util "
-                      f"{lu if lu is None else round(lu, 3)}  VALU busy (x4 / 1024 SIMD / per-XCD GUI_ACTIVE) "
+                      f"{lu if lu is None else round(lu, 3)}  VALU issue busy (x2 / 1024 SIMD / per-XCD GUI_ACTIVE) "
                       f"{vb if vb is None else round(vb, 3)}  GUI_ACTIVE {pl['gui_active']:.4g}")
 
 

@@ -4,7 +4,8 @@
 
 VALU (the bound): lane-instructions per launch of the dominant kernel
 (profiles/pmc_valu_<config>_<bvh>.json, tools/pmc_valu.sh) / the bench's HIP-event
-average launch time / the non-packed VALU issue peak (bench.py VALU_PEAK_TLOPS).
+average launch time / the measured VALU issue peak (bench.py VALU_PEAK_TLOPS: one wave64 instruction
+per SIMD per 2 clocks, profiles/r4_valu_peak/).
 HBM: PMC traffic per launch (profiles/pmc_traffic_<config>_<bvh>.json,
 tools/pmc_traffic.sh) / the same launch time / 8 TB/s.
 Prints both and exits non-zero if the line's numbers disagree with the
@@ -31,9 +32,14 @@ def recompute(line):
     src = r["valu"]["source"]
     if src:
         e = json.load(open(os.path.join(REPO, src)))[r["valu"]["kind"]]
-        out["valu_frac"] = e["lane_ops"] / launch_s / 1e12 / bench.VALU_PEAK_TLOPS
+        # the peak the line was computed against: rounds 1-3 assumed 4 clocks per wave64 VALU instruction
+        # (39.3 T, issue busy from SQ_ACTIVE_INST_VALU); from round 4 the measured 2 clocks (78.6 T,
+        # profiles/r4_valu_peak/), issue busy from SQ_INSTS_VALU
+        cyc = bench.N_SIMD * 64 * bench.CLOCK_HZ / (r["peak"] * 1e12)
+        out["valu_frac"] = e["lane_ops"] / launch_s / 1e12 / r["peak"]
         out["valu_lane_util"] = e["thread_cycles_valu"] / (64 * e["active_inst_valu"])
-        out["valu_issue_busy"] = e["active_inst_valu"] * 4 / (bench.N_SIMD * launch_s * bench.CLOCK_HZ)
+        insts = e["active_inst_valu"] if round(cyc) == 4 else e["insts_valu"]
+        out["valu_issue_busy"] = insts * round(cyc) / (bench.N_SIMD * launch_s * bench.CLOCK_HZ)
     hsrc = r["hbm"]["source"]
     if hsrc:
         t = json.load(open(os.path.join(REPO, hsrc)))[r["hbm"]["kind"]]["traffic_bytes"]

@@ -151,12 +151,14 @@ def tuning(**fields) -> RtwTuning:
 
 class RtwSceneStats(C.Structure):
     _fields_ = [("n_nodes", C.c_uint32), ("n_leaves", C.c_uint32), ("n_inner", C.c_uint32), ("depth", C.c_uint32),
-                ("device_bytes", C.c_uint64), ("axis_draws", C.c_uint32), ("n_hoisted", C.c_uint32)]
+                ("device_bytes", C.c_uint64), ("axis_draws", C.c_uint32), ("n_hoisted", C.c_uint32),
+                ("extent", C.c_float), ("box_pad", C.c_float)]
 
 
 # every symbol include/rtw_gpu.h declares: name -> (restype, argtypes)
 SIGNATURES = {
     "rtw_version": (C.c_int, []),
+    "rtw_build_id": (C.c_char_p, []),
     "rtw_last_error": (C.c_char_p, []),
     "rtw_device_count": (C.c_int, [C.POINTER(C.c_int)]),
     "rtw_camera_init": (C.c_int, [C.POINTER(RtwCameraParams), C.POINTER(RtwCamera)]),

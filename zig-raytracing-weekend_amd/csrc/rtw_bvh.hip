@@ -679,6 +679,10 @@ int rtw_build_bvh(const rtw_scene_desc& desc, std::vector<rtw_node>& nodes, rtw_
         // (E = max |coordinate| of the scene) keeps the test conservative for
         // every origin with |o| <= 7E (checked per launch, else the exact test runs).
         // A superset of boxes is visited; sphere tests decide the hit.
+        // E spans every object's box, not only the inner nodes: hoisted spheres (Book-1's r = 1000
+        // ground) are leaves outside the tree, and secondary rays start anywhere on them -- ground
+        // hits near the horizon lie hundreds of units out, so an E of the tree alone would not
+        // cover their origins.
         float e = 0;
         for (const rtw_node& n : nodes) {
             uint32_t w;
@@ -686,6 +690,8 @@ int rtw_build_bvh(const rtw_scene_desc& desc, std::vector<rtw_node>& nodes, rtw_
             if (w & RTW_LEAF_BIT) continue;
             for (int k = 0; k < 3; k++) e = std::max(e, std::max(std::fabs(n.a[k]), std::fabs(n.b[k])));
         }
+        for (const Obj& o : geo.objects())
+            for (int k = 0; k < 3; k++) e = std::max(e, std::max(std::fabs(o.box.mn[k]), std::fabs(o.box.mx[k])));
         const float pad = e * 1.9073486e-06f;  // 2^-19
         for (rtw_node& n : nodes) {
             uint32_t w;

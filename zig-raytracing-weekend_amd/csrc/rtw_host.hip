@@ -456,6 +456,8 @@ int rtw_scene_create_ex(const rtw_scene_desc* d, int device, const rtw_tuning* t
     ctx->stats.device_bytes = off;
     ctx->stats.axis_draws = draws;
     ctx->stats.n_hoisted = n_hoisted;
+    ctx->stats.extent = ctx->extent;
+    ctx->stats.box_pad = ctx->box_pad;
     *out = ctx;
     return RTW_OK;
 }
@@ -704,12 +706,18 @@ int run_batches(rtw_ctx* ctx, rtw_launch L, uint32_t s0, uint32_t s1, uint32_t b
 // progress after each batch.  begin/end/out as rtw_cpu_render.
 int run_host(const rtw_ctx* ctx, rtw_launch L, uint32_t begin, uint32_t end, uint32_t s0, uint32_t s1,
              uint32_t batch, float* out, const rtw_render_opts* ctl, uint64_t pixels) {
+    // stop flags: with an explicit spp_batch they are polled between batches only, so a stopped render
+    // holds whole batches (every pixel's .w is the last finished batch's end, and a resume from it adds
+    // no sample twice); without one, per pixel as Camera.render polls `running` (camera.zig:107) --
+    // then each pixel's .w says how far that pixel got
+    const bool per_pixel = batch == 0;
     if (!batch) batch = s1 - s0;
     const uint64_t total = pixels * (uint64_t)(s1 - s0);
     for (uint32_t s = s0; s < s1; s += batch) {
+        if (!per_pixel && rtw_stop_requested(ctl)) return fail(RTW_E_CANCELLED, "cancelled");
         L.s0 = s;
         L.s1 = (s1 - s < batch) ? s1 : s + batch;
-        if (rtw_cpu_render(L, begin, end, out, ctx->cpu_threads, ctl) == RTW_E_CANCELLED)
+        if (rtw_cpu_render(L, begin, end, out, ctx->cpu_threads, per_pixel ? ctl : nullptr) == RTW_E_CANCELLED)
             return fail(RTW_E_CANCELLED, "cancelled");
         if (ctl && ctl->progress && ctl->progress(pixels * (uint64_t)(L.s1 - s0), total, ctl->user))
             return fail(RTW_E_CANCELLED, "cancelled by progress callback");
@@ -829,36 +837,93 @@ int rtw_render_ex(rtw_ctx* ctx, const rtw_camera* cam, uint32_t pix_begin, uint3
     if (spp_begin > spp_end) return fail(RTW_E_INVALID, "bad sample range");
     if (pix_begin == pix_end || spp_begin == spp_end) return RTW_OK;
     const uint32_t ubatch = opts ? opts->spp_batch : 0u;
-    std::lock_guard<std::mutex> lock(ctx->mu);
     if (ctx->device == RTW_DEVICE_CPU) {  // host context: Camera.render on host threads (rtw_cpu.hip)
-        rtw_launch L = make_launch(ctx, cam, seed);
+        rtw_launch L;
+        {
+            std::lock_guard<std::mutex> lock(ctx->mu);
+            L = make_launch(ctx, cam, seed);
+        }
+        // the scene image is read-only: concurrent callers (the 8 Tasks) render their ranges at once
         L.n_shards = 0;
         return run_host(ctx, L, pix_begin, pix_end, spp_begin, spp_end, ubatch, accum, opts, pix_end - pix_begin);
     }
-    HIP_TRY(hipSetDevice(ctx->device));
-    if (int rc = stream_enter(ctx, ctx->stream)) return rc;
+    // GPU context.  The context lock is held only while a call enqueues work, never while it waits for
+    // the device, so concurrent callers -- the reference's 8 Tasks on disjoint chunks (main.zig:314-326)
+    // -- interleave their spp batches on the context's stream and advance samples-outer together, as
+    // the 8 workers of camera.zig:98-111 do.  Each call stages only its own chunk of the shared
+    // full-frame device buffer, so the chunks never overlap.
     const size_t bytes = (size_t)cam->size * 16;
-    if (int rc = ensure_scratch(ctx, bytes)) return rc;
     const size_t o = (size_t)pix_begin * 16, nb = (size_t)(pix_end - pix_begin) * 16;
-    HIP_TRY(hipMemcpyAsync((char*)ctx->d_scratch + o, (char*)accum + o, nb, hipMemcpyHostToDevice, ctx->stream));
-    rtw_launch L = make_launch(ctx, cam, seed);
-    L.accum = reinterpret_cast<float4*>(ctx->d_scratch);
-    L.pix_begin = pix_begin;
-    L.pix_end = pix_end;
-    L.row0 = pix_begin / cam->image_width;
-    L.n_rows = (pix_end - 1) / cam->image_width - L.row0 + 1;
-    L.n_shards = 0;
-    L.counters = nullptr;
-    set_tiles(L);
-    const uint32_t batch = ubatch ? ubatch : auto_batch(ctx, pix_end - pix_begin, spp_end - spp_begin);
-    rtw_render_opts ctl{};  // the host API always reports progress per batch when asked, like rtw_render did
-    if (opts) ctl = *opts;
-    int rc = run_batches(ctx, L, spp_begin, spp_end, batch, ctx->stream, &ctl, pix_end - pix_begin);
+    const uint64_t pixels = pix_end - pix_begin;
+    hipEvent_t done = nullptr;
+    uint32_t batch = 0;
+    {
+        std::unique_lock<std::mutex> lock(ctx->mu);
+        HIP_TRY(hipSetDevice(ctx->device));
+        // the staging buffer grows only while no other host-buffer call has a chunk staged in it
+        ctx->host_cv.wait(lock, [&] { return ctx->scratch_bytes >= bytes || ctx->host_calls == 0; });
+        if (int rc = stream_enter(ctx, ctx->stream)) return rc;
+        if (int rc = ensure_scratch(ctx, bytes)) return rc;
+        HIP_TRY(hipEventCreateWithFlags(&done, hipEventDisableTiming));
+        HIP_TRY(hipMemcpyAsync((char*)ctx->d_scratch + o, (char*)accum + o, nb, hipMemcpyHostToDevice, ctx->stream));
+        if (int rc = stream_leave(ctx, ctx->stream)) return rc;
+        ctx->host_calls++;
+        batch = ubatch ? ubatch : auto_batch(ctx, pixels, spp_end - spp_begin);
+    }
+    const bool polled = rtw_polled(opts);
+    const uint64_t total = pixels * (uint64_t)(spp_end - spp_begin);
+    int rc = RTW_OK;
+    for (uint32_t s = spp_begin; s < spp_end && rc == RTW_OK; s += batch) {
+        if (rtw_stop_requested(opts)) {
+            rc = fail(RTW_E_CANCELLED, "cancelled");
+            break;
+        }
+        const uint32_t s_end = (spp_end - s < batch) ? spp_end : s + batch;
+        {
+            std::lock_guard<std::mutex> lock(ctx->mu);
+            if (hipSetDevice(ctx->device) != hipSuccess || stream_enter(ctx, ctx->stream)) {
+                rc = fail(RTW_E_HIP, "rtw_render_ex: device");
+                break;
+            }
+            rtw_launch L = make_launch(ctx, cam, seed);
+            L.accum = reinterpret_cast<float4*>(ctx->d_scratch);
+            L.pix_begin = pix_begin;
+            L.pix_end = pix_end;
+            L.row0 = pix_begin / cam->image_width;
+            L.n_rows = (pix_end - 1) / cam->image_width - L.row0 + 1;
+            L.n_shards = 0;
+            L.counters = nullptr;
+            set_tiles(L);
+            rc = run_batches(ctx, L, s, s_end, s_end - s, ctx->stream, nullptr, pixels);
+            if (rc == RTW_OK) rc = stream_leave(ctx, ctx->stream);
+            if (rc == RTW_OK && hipEventRecord(done, ctx->stream) != hipSuccess) rc = fail(RTW_E_HIP, "event");
+        }
+        if (rc == RTW_OK && polled) {  // wait for this batch without the lock, then report it
+            if (hipEventSynchronize(done) != hipSuccess) rc = fail(RTW_E_HIP, "rtw_render_ex: batch");
+            else if (opts->progress && opts->progress(pixels * (uint64_t)(s_end - spp_begin), total, opts->user))
+                rc = fail(RTW_E_CANCELLED, "cancelled by progress callback");
+        }
+    }
     // copy back whatever was rendered (also on cancel: completed batches are valid)
-    hipError_t e = hipMemcpyAsync((char*)accum + o, (char*)ctx->d_scratch + o, nb, hipMemcpyDeviceToHost, ctx->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    hipError_t e;
+    {
+        std::lock_guard<std::mutex> lock(ctx->mu);
+        e = hipSetDevice(ctx->device);
+        if (e == hipSuccess && ctx->last_stream && ctx->last_stream != ctx->stream)
+            e = hipStreamWaitEvent(ctx->stream, ctx->last_done, 0);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync((char*)accum + o, (char*)ctx->d_scratch + o, nb, hipMemcpyDeviceToHost, ctx->stream);
+        if (e == hipSuccess) e = hipEventRecord(done, ctx->stream);
+        if (e == hipSuccess) (void)stream_leave(ctx, ctx->stream);
+    }
+    if (e == hipSuccess) e = hipEventSynchronize(done);
+    (void)hipEventDestroy(done);
+    {
+        std::lock_guard<std::mutex> lock(ctx->mu);
+        ctx->host_calls--;
+    }
+    ctx->host_cv.notify_all();
     if (e != hipSuccess) return hip_fail(e, "rtw_render copy back");
-    ctx->last_stream = nullptr;  // synchronised: nothing of this context is in flight
     return rc;
 }
 

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <condition_variable>
 #include <mutex>
 #include <vector>
 
@@ -227,9 +228,13 @@ struct rtw_ctx {
     float box_pad = 0;             // absolute pad baked into the inner boxes (SAH trees), 0 = none
     float extent = 0;              // max |coordinate| over the scene's boxes
     // Concurrent callers (the reference's 8 RenderThreads call Camera.render at once, main.zig:314-326):
-    // one render call at a time per context -- the wavefront state and staging buffers are per context --
-    // and a call on another stream than the previous one waits for that call's work on the device.
+    // one caller at a time enqueues work on a context -- the wavefront state and staging buffers are per
+    // context -- and work on another stream than the previous enqueue's waits for that work on the
+    // device.  The host-buffer API (rtw_render_ex) holds the lock only while it enqueues one spp batch,
+    // so the 8 Tasks' batches interleave; host_calls counts its calls with a chunk staged in d_scratch.
     std::mutex mu;
+    std::condition_variable host_cv;
+    int host_calls = 0;
     hipEvent_t last_done = nullptr;
     hipStream_t last_stream = nullptr;
 };

@@ -1293,6 +1293,14 @@ __device__ __forceinline__ void wf_step_zero_next(const rtw_wf& W, uint32_t it) 
 template <uint32_t FEAT>
 __global__ __launch_bounds__(1024) void wf_step_clds(rtw_launch L, rtw_wf W, uint32_t it) {
     static_assert((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING)) == 0, "static sphere scenes");
+#if defined(RTW_SETPRIO)
+    {   // A/B variant: the 4 waves a SIMD holds get priorities 0..3 (waves of one block go to SIMDs cyclically)
+        const uint32_t pr = __builtin_amdgcn_readfirstlane(threadIdx.x >> 8) & 3u;
+        if (pr == 1u) __builtin_amdgcn_s_setprio(1);
+        else if (pr == 2u) __builtin_amdgcn_s_setprio(2);
+        else if (pr == 3u) __builtin_amdgcn_s_setprio(3);
+    }
+#endif
     wf_step_zero_next(W, it);
     extern __shared__ uint4 wf_clds[];
     stage_clds(L, wf_clds);

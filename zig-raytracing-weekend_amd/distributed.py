@@ -87,9 +87,14 @@ class ShardedRender:
                counters: Optional[int] = None, sync: bool = False, timing=None) -> None:
         """Enqueue this rank's rows x samples [spp_begin, spp_end) on `stream`.
         timing: optional _abi.RtwKernelTiming filled with per-kernel device time
-        (the call then synchronises the stream)."""
+        (the call then synchronises the stream).  A CPU tile (a host context, RTW_DEVICE_CPU: bench.py
+        --host-backend) renders through rtw_render_rows, blocking."""
         import torch
         self.tile.zero_()
+        if self.tile.device.type == "cpu":
+            render_rows_host(self.world, self.cam, self.rpb, self.world_size, self.rank, spp_begin, spp_end,
+                             self.tile.numpy(), seed=seed, spp_batch=spp_batch)
+            return
         if stream is not None and stream != torch.cuda.current_stream(self.tile.device):
             stream.wait_stream(torch.cuda.current_stream(self.tile.device))  # the zeroing precedes the render
         flags = 0 if sync else _abi.RTW_RENDER_NO_SYNC
