@@ -61,6 +61,113 @@ __global__ void valu_chains(float* out, int iters, float b, float c) {
     out[blockIdx.x * blockDim.x + threadIdx.x] = s;
 }
 
+// one instruction class per kernel (16 independent chains x UNR per loop branch): its issue cost and
+// whether two waves' instances dual-issue (SQ_ACTIVE_INST_VALU2).  Operands are garbage; only timing counts.
+enum Cls { C_CNDMASK = 0, C_MAX3, C_FMA_MIX, C_SQRT, C_RCP, C_ADD_U32, C_MUL_LO_U32, C_MOV, C_CMP_SGPR,
+           C_FMA_SGPR, C_MUL_F32, C_CNDMASK_VCC, C_LSHL_ADD, C_BFE, C_XOR,
+           C_MIN_F32, C_MAX_F32, C_MIN3, C_MED3, C_SUB_F32, C_ADD_ABS, C_SUB_NEG, C_CMP_VCC, C_CMP_VCC_CND,
+           C_AND, C_OR, C_LSHL, C_LSHR, C_CVT_F16, C_PK_ADD, C_PK_MUL, C_PERM, C_MUL_HI, C_FMA_INLINE,
+           C_ADD_LITERAL, C_FMAC, C_MUL_U24, C_CMP_SGPR_OPND, C_LDEXP,
+           C_MAX_I32, C_MIN_U32, C_MAX3_I32, C_SUB_U32, C_ASHR_I32, C_ADD3_U32, C_LSHL_OR, C_BFI, C_CNDMASK_VGPR3,
+           C_PK_MAX_F16, C_MUL_F32_SGPR, C_ADD_F32_SGPR, C_COUNT };
+template <int K>
+__device__ __forceinline__ void cls_step(float& a, float b, float c, uint64_t m, uint64_t& sm, float sc) {
+    if constexpr (K == C_CNDMASK) asm volatile("v_cndmask_b32_e64 %0, %0, %1, %2" : "+v"(a) : "v"(b), "s"(m));
+    if constexpr (K == C_MAX3) asm volatile("v_max3_f32 %0, %0, %1, %2" : "+v"(a) : "v"(b), "v"(c));
+    if constexpr (K == C_FMA_MIX) asm volatile("v_fma_mix_f32 %0, %1, %2, %0 op_sel_hi:[1,0,0]" : "+v"(a) : "v"(b), "v"(c));
+    if constexpr (K == C_SQRT) asm volatile("v_sqrt_f32 %0, %0" : "+v"(a));
+    if constexpr (K == C_RCP) asm volatile("v_rcp_f32 %0, %0" : "+v"(a));
+    if constexpr (K == C_ADD_U32) asm volatile("v_add_u32 %0, %0, %1" : "+v"(a) : "v"(b));
+    if constexpr (K == C_MUL_LO_U32) asm volatile("v_mul_lo_u32 %0, %0, %1" : "+v"(a) : "v"(b));
+    if constexpr (K == C_MOV) asm volatile("v_mov_b32 %0, %1" : "=v"(a) : "v"(b));
+    if constexpr (K == C_CMP_SGPR) asm volatile("v_cmp_gt_f32_e64 %0, %1, %2" : "=s"(sm) : "v"(a), "v"(b));
+    if constexpr (K == C_FMA_SGPR) asm volatile("v_fma_f32 %0, %1, %2, %0" : "+v"(a) : "v"(b), "s"(sc));
+    if constexpr (K == C_MUL_F32) asm volatile("v_mul_f32 %0, %0, %1" : "+v"(a) : "v"(b));
+    if constexpr (K == C_CNDMASK_VCC) asm volatile("v_cndmask_b32 %0, %0, %1, vcc" : "+v"(a) : "v"(b));
+    if constexpr (K == C_LSHL_ADD) asm volatile("v_lshl_add_u32 %0, %0, 4, %1" : "+v"(a) : "v"(b));
+    if constexpr (K == C_BFE) asm volatile("v_bfe_u32 %0, %0, 8, 8" : "+v"(a));
+    if constexpr (K == C_XOR) asm volatile("v_xor_b32 %0, %0, %1" : "+v"(a) : "v"(b));
+    if constexpr (K == C_MIN_F32) asm volatile("v_min_f32 %0, %0, %1" : "+v"(a) : "v"(b));
+    if constexpr (K == C_MAX_F32) asm volatile("v_max_f32 %0, %0, %1" : "+v"(a) : "v"(b));
+    if constexpr (K == C_MIN3) asm volatile("v_min3_f32 %0, %0, %1, %2" : "+v"(a) : "v"(b), "v"(c));
+    if constexpr (K == C_MED3) asm volatile("v_med3_f32 %0, %0, %1, %2" : "+v"(a) : "v"(b), "v"(c));
+    if constexpr (K == C_SUB_F32) asm volatile("v_sub_f32 %0, %0, %1" : "+v"(a) : "v"(b));
+    if constexpr (K == C_ADD_ABS) asm volatile("v_add_f32_e64 %0, %0, |%1|" : "+v"(a) : "v"(b));
+    if constexpr (K == C_SUB_NEG) asm volatile("v_sub_f32_e64 %0, -%0, %1" : "+v"(a) : "v"(b));
+    if constexpr (K == C_CMP_VCC) asm volatile("v_cmp_gt_f32 vcc, %0, %1" : : "v"(a), "v"(b) : "vcc");
+    if constexpr (K == C_CMP_VCC_CND)
+        asm volatile("v_cmp_gt_f32 vcc, %0, %1\n\ts_nop 0\n\tv_cndmask_b32 %0, %0, %1, vcc" : "+v"(a) : "v"(b) : "vcc");
+    if constexpr (K == C_AND) asm volatile("v_and_b32 %0, %0, %1" : "+v"(a) : "v"(b));
+    if constexpr (K == C_OR) asm volatile("v_or_b32 %0, %0, %1" : "+v"(a) : "v"(b));
+    if constexpr (K == C_LSHL) asm volatile("v_lshlrev_b32 %0, 3, %0" : "+v"(a));
+    if constexpr (K == C_LSHR) asm volatile("v_lshrrev_b32 %0, 3, %0" : "+v"(a));
+    if constexpr (K == C_CVT_F16) asm volatile("v_cvt_f32_f16 %0, %1" : "=v"(a) : "v"(b));
+    if constexpr (K == C_PERM) asm volatile("v_perm_b32 %0, %0, %1, %2" : "+v"(a) : "v"(b), "v"(c));
+    if constexpr (K == C_MUL_HI) asm volatile("v_mul_hi_u32 %0, %0, %1" : "+v"(a) : "v"(b));
+    if constexpr (K == C_FMA_INLINE) asm volatile("v_fma_f32 %0, %0, %1, 1.0" : "+v"(a) : "v"(b));
+    if constexpr (K == C_ADD_LITERAL) asm volatile("v_add_f32 %0, 0x35800000, %0" : "+v"(a));
+    if constexpr (K == C_FMAC) asm volatile("v_fmac_f32 %0, %1, %2" : "+v"(a) : "v"(b), "v"(c));
+    if constexpr (K == C_MUL_U24) asm volatile("v_mul_u32_u24 %0, %0, %1" : "+v"(a) : "v"(b));
+    if constexpr (K == C_CMP_SGPR_OPND) asm volatile("v_cmp_gt_f32 vcc, %0, %1" : : "s"(sc), "v"(a) : "vcc");
+    if constexpr (K == C_LDEXP) asm volatile("v_ldexp_f32 %0, %0, %1" : "+v"(a) : "v"(b));
+    if constexpr (K == C_MAX_I32) asm volatile("v_max_i32 %0, %0, %1" : "+v"(a) : "v"(b));
+    if constexpr (K == C_MIN_U32) asm volatile("v_min_u32 %0, %0, %1" : "+v"(a) : "v"(b));
+    if constexpr (K == C_MAX3_I32) asm volatile("v_max3_i32 %0, %0, %1, %2" : "+v"(a) : "v"(b), "v"(c));
+    if constexpr (K == C_SUB_U32) asm volatile("v_sub_u32 %0, %0, %1" : "+v"(a) : "v"(b));
+    if constexpr (K == C_ASHR_I32) asm volatile("v_ashrrev_i32 %0, 3, %0" : "+v"(a));
+    if constexpr (K == C_ADD3_U32) asm volatile("v_add3_u32 %0, %0, %1, %2" : "+v"(a) : "v"(b), "v"(c));
+    if constexpr (K == C_LSHL_OR) asm volatile("v_lshl_or_b32 %0, %0, 3, %1" : "+v"(a) : "v"(b));
+    if constexpr (K == C_BFI) asm volatile("v_bfi_b32 %0, %0, %1, %2" : "+v"(a) : "v"(b), "v"(c));
+    if constexpr (K == C_CNDMASK_VGPR3) asm volatile("v_cndmask_b32_e64 %0, %0, %1, %2" : "+v"(a) : "v"(b), "s"(m));
+    if constexpr (K == C_PK_MAX_F16) asm volatile("v_pk_max_f16 %0, %0, %1" : "+v"(a) : "v"(b));
+    if constexpr (K == C_MUL_F32_SGPR) asm volatile("v_mul_f32 %0, %1, %0" : "+v"(a) : "s"(sc));
+    if constexpr (K == C_ADD_F32_SGPR) asm volatile("v_add_f32 %0, %1, %0" : "+v"(a) : "s"(sc));
+}
+// packed pairs (64-bit registers)
+template <int K>
+__global__ void cls_pk_chains(float* out, int iters, float b, float c) {
+    extern __shared__ float lds_pad[];
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    f2 a[16];
+    const f2 bb = {b, c};
+#pragma unroll
+    for (int i = 0; i < 16; ++i) a[i] = f2{(float)threadIdx.x, (float)i};
+    for (int it = 0; it < iters; it += 16) {
+#pragma unroll
+        for (int u = 0; u < 16; ++u)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                if constexpr (K == C_PK_ADD) asm volatile("v_pk_add_f32 %0, %0, %1" : "+v"(a[i]) : "v"(bb));
+                else asm volatile("v_pk_mul_f32 %0, %0, %1" : "+v"(a[i]) : "v"(bb));
+            }
+    }
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) s += a[i].x + a[i].y;
+    if (threadIdx.x == 0) lds_pad[0] = s;
+    out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+template <int K>
+__global__ void cls_chains(float* out, int iters, float b, float c) {
+    extern __shared__ float lds_pad[];
+    float a[16];
+    uint64_t sm[16];
+    const uint64_t m = __ballot(threadIdx.x & 1);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) { a[i] = (float)(threadIdx.x + i); sm[i] = 0; }
+    for (int it = 0; it < iters; it += 16) {
+#pragma unroll
+        for (int u = 0; u < 16; ++u)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) cls_step<K>(a[i], b, c, m, sm[i], c);
+    }
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) s += a[i] + (float)(sm[i] & 1);
+    if (threadIdx.x == 0) lds_pad[0] = s;
+    out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+
 // packed form: one v_pk_fma_f32 = 2 lane-ops per lane
 template <int NCH>
 __global__ void valu_pk_chains(float* out, int iters, float b, float c) {
@@ -144,7 +251,7 @@ int main(int argc, char** argv) {
     fprintf(stderr, "device %s, %d CUs, clock %d kHz, LDS/block max %zu\n", p.gcnArchName, cus, p.clockRate,
             p.sharedMemPerBlock);
 
-    Case cases[64];
+    Case cases[192];
     int n = 0;
     const int waves[] = {1, 2, 4, 8};
     for (int w : waves) {
@@ -175,6 +282,36 @@ int main(int argc, char** argv) {
     cases[n++] = {"fma_ch16_unr16_wfstep_shape", (const void*)valu_chains<OP_FMA, 16, 16>, 1, 16, 1024, 4, 124 * 1024};
     cases[n++] = {"fma_ch4_unr64_wfstep_shape", (const void*)valu_chains<OP_FMA, 4, 64>, 1, 4, 1024, 4, 124 * 1024};
     cases[n++] = {"fma_ch1_unr256_wfstep_shape", (const void*)valu_chains<OP_FMA, 1, 256>, 1, 1, 1024, 4, 124 * 1024};
+    {
+        static const char* cls_names[C_COUNT] = {"cndmask_sgpr", "max3", "fma_mix", "sqrt", "rcp", "add_u32",
+                                                 "mul_lo_u32", "mov", "cmp_to_sgpr", "fma_sgpr_operand", "mul_f32",
+                                                 "cndmask_vcc", "lshl_add_u32", "bfe_u32", "xor_b32",
+                                                 "min_f32", "max_f32", "min3_f32", "med3_f32", "sub_f32", "add_abs_e64",
+                                                 "sub_neg_e64", "cmp_to_vcc", "cmp_vcc_nop_cndmask_pair", "and_b32",
+                                                 "or_b32", "lshlrev_b32", "lshrrev_b32", "cvt_f32_f16", "pk_add_f32",
+                                                 "pk_mul_f32", "perm_b32", "mul_hi_u32", "fma_inline_const",
+                                                 "add_literal", "fmac_f32", "mul_u32_u24", "cmp_sgpr_operand", "ldexp_f32",
+                                                 "max_i32", "min_u32", "max3_i32", "sub_u32", "ashrrev_i32", "add3_u32",
+                                                 "lshl_or_b32", "bfi_b32", "cndmask_sgpr_b", "pk_max_f16",
+                                                 "mul_f32_sgpr_operand", "add_f32_sgpr_operand"};
+#define CLS(k) (const void*)cls_chains<k>
+        const void* fns[C_COUNT] = {CLS(0), CLS(1), CLS(2), CLS(3), CLS(4), CLS(5), CLS(6), CLS(7), CLS(8), CLS(9),
+                                    CLS(10), CLS(11), CLS(12), CLS(13), CLS(14), CLS(15), CLS(16), CLS(17), CLS(18),
+                                    CLS(19), CLS(20), CLS(21), CLS(22), CLS(23), CLS(24), CLS(25), CLS(26), CLS(27),
+                                    CLS(28), (const void*)cls_pk_chains<C_PK_ADD>, (const void*)cls_pk_chains<C_PK_MUL>,
+                                    CLS(31), CLS(32), CLS(33), CLS(34), CLS(35), CLS(36), CLS(37), CLS(38), CLS(39),
+                                    CLS(40), CLS(41), CLS(42), CLS(43), CLS(44), CLS(45), CLS(46), CLS(47), CLS(48),
+                                    CLS(49), CLS(50)};
+#undef CLS
+        static char names[C_COUNT][2][48];
+        for (int kk = 0; kk < C_COUNT; ++kk) {
+            const int wsel[2] = {4, 8};
+            for (int j = 0; j < 2; ++j) {
+                snprintf(names[kk][j], sizeof names[kk][j], "cls_%s", cls_names[kk]);
+                cases[n++] = {names[kk][j], fns[kk], 1, 16, 256, wsel[j], lds_for(wsel[j])};
+            }
+        }
+    }
     const int n_valu = n;
     // LDS dependent-read latency (lane-ops = reads): 16 KiB table, 1 chain per lane
     for (int w : waves) cases[n++] = {"lds_chase_b32", (const void*)lds_chase, 1, 1, 256, w, lds_for(w)};

@@ -499,6 +499,12 @@ int rtw_scene_nodes(rtw_ctx* ctx, void* out, uint32_t cap, uint32_t* n_out);
 int rtw_debug_rng(rtw_ctx* ctx, uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t n, float* out);
 int rtw_debug_sample(rtw_ctx* ctx, const rtw_camera* cam, uint64_t seed, uint32_t pixel, uint32_t sample,
                      float out[3]);
+/* ABI 6, host-only: the walk's sphere fast-reject (sphere_may_hit, the same fp32 operations as the
+ * device) and Sphere.hit's exact accept (objects.zig:127-136, tmin = 0.001) for n sphere tests given
+ * a = lengthSquared(d), half_b = dot(oc, d), c = lengthSquared(oc) - r*r and closest: the test suite
+ * checks that the filter never rejects a test the exact arithmetic accepts. */
+int rtw_debug_sphere_filter(uint32_t n, const float* a, const float* half_b, const float* c, const float* closest,
+                            uint8_t* may_hit, uint8_t* accept);
 
 #ifdef __cplusplus
 }

@@ -175,8 +175,10 @@ int main(int argc, char** argv) {
             all_running &= rt.threads[k].running;
         }
         /* while every task is still rendering, their samples done differ by whole batches */
-        /* (a snapshot taken while some Task reported is retried: the 8 reads must describe one instant) */
-        if (stable && all_running && !stopped && (mx - mn) / rt.spp_batch > max_spread)
+        /* while every Task is running and each has finished its first batch (thread start-up is host
+         * jitter, not the library's scheduling); a snapshot taken while some Task reported is retried:
+         * the 8 reads must describe one instant */
+        if (stable && all_running && !stopped && mn >= rt.spp_batch && (mx - mn) / rt.spp_batch > max_spread)
             max_spread = (mx - mn) / rt.spp_batch;
         last_count = rtw_count_samples(rt.buffer, size);  /* main.zig:470-477 */
         polls++;

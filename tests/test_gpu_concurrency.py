@@ -1,9 +1,9 @@
 """Concurrent callers of one context.  The reference renders with 8 RenderThreads that
 call Camera.render at the same time on disjoint chunks (startRender, src/main.zig:314-326;
 Camera.render, src/camera.zig:93-116); the Zig binding in INTEGRATION.md keeps those
-Tasks.  rtw_render serialises the calls on a context (its wavefront state is per context),
-and device-API calls on different streams are ordered on the device: both give the
-images of back-to-back calls, bit for bit."""
+Tasks.  rtw_render interleaves the calls' spp batches on the context's stream (its lock is held
+only while a call enqueues a batch: the wavefront state is per context), and device-API calls on
+different streams are ordered on the device: both give the images of back-to-back calls, bit for bit."""
 import ctypes as C
 import threading
 

@@ -159,6 +159,8 @@ class RtwSceneStats(C.Structure):
 SIGNATURES = {
     "rtw_version": (C.c_int, []),
     "rtw_build_id": (C.c_char_p, []),
+    "rtw_debug_sphere_filter": (C.c_int, [C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                          C.c_void_p]),
     "rtw_last_error": (C.c_char_p, []),
     "rtw_device_count": (C.c_int, [C.POINTER(C.c_int)]),
     "rtw_camera_init": (C.c_int, [C.POINTER(RtwCameraParams), C.POINTER(RtwCamera)]),
@@ -232,7 +234,13 @@ def lib() -> C.CDLL:
         except Exception:
             pass
         L = C.CDLL(LIB_PATH)
+        # an A/B build of an earlier ABI (RTW_LIB=...) may lack the newest entry points: those stay
+        # unbound there (AttributeError on use); the in-tree library must export every one
+        # (tests/test_abi.py)
+        optional = os.environ.get("RTW_LIB") is not None
         for name, (res, args) in SIGNATURES.items():
+            if optional and not hasattr(L, name):
+                continue
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args

@@ -132,7 +132,10 @@ class Camera:
         """Samples [spp_begin, spp_end) of pixels [pix_begin, pix_end) through rtw_render_ex, polling the
         state's RenderThread.running flag (camera.zig:107) between sample batches (spp_batch, 0 = auto);
         progress(done, total) -> True stops.  A stop raises RtwError(RTW_E_CANCELLED) with the finished
-        batches in the buffer (and the texture updated from them)."""
+        batches in the buffer (and the texture updated from them): every pixel's .w is the end of the last
+        finished batch, so a resume from it adds no sample twice.  Exception: a host context (RTW_DEVICE_CPU)
+        given spp_batch = 0 polls per pixel as camera.zig:107 does, so a stop there leaves each pixel at its
+        own .w -- resume each pixel from its own .w, or pass a spp_batch."""
         w = state.writer
         buf = w.buffer
         assert buf.flags["C_CONTIGUOUS"] and buf.dtype == np.float32 and buf.shape == (self.size, 4)

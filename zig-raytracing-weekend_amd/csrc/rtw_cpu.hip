@@ -62,3 +62,31 @@ int rtw_cpu_render(const rtw_launch& L, uint32_t begin, uint32_t end, float* out
     for (std::thread& th : pool) th.join();
     return stopped ? RTW_E_CANCELLED : RTW_OK;
 }
+
+// ABI 6 test hook (include/rtw_gpu.h): the walk's sphere fast-reject against Sphere.hit's exact accept, on
+// the host -- sphere_may_hit is the device's code (rtw_device.h), the same fp32 operations
+extern "C" int rtw_debug_sphere_filter(uint32_t n, const float* a, const float* half_b, const float* c, const float* closest,
+                            uint8_t* may_hit, uint8_t* accept) {
+    if (n && (!a || !half_b || !c || !closest || !may_hit || !accept)) return RTW_E_INVALID;
+    for (uint32_t i = 0; i < n; i++) {
+        // the ray constants as ray_trav derives them from a (fast_reject on)
+        const float aa = a[i], hb = half_b[i];
+        const bool in_range = aa >= 0x1p-40f && aa <= 0x1p40f;
+        const float tk = aa * 0.001f, ktk = tk * 9.5367432e-07f, gk = in_range ? 0.99999905f : 0.0f;
+        const float disc = hb * hb - aa * c[i];
+        may_hit[i] = sphere_may_hit(hb, disc, aa, closest[i], tk, ktk, gk) ? 1 : 0;
+        // Sphere.hit (objects.zig:127-136): nearest root in the open interval (0.001, closest)
+        bool ok = false;
+        if (disc >= 0) {
+            const float sq = std::sqrt(disc);
+            float root = (-hb - sq) / aa;
+            ok = 0.001f < root && root < closest[i];
+            if (!ok) {
+                root = (-hb + sq) / aa;
+                ok = 0.001f < root && root < closest[i];
+            }
+        }
+        accept[i] = ok ? 1 : 0;
+    }
+    return RTW_OK;
+}

@@ -377,6 +377,11 @@ struct RayTrav {
     float a;     // lengthSquared(d) (objects.zig:124)
     float rcp_a; // hardware 1/a estimate for the sphere fast-reject (0 disables it)
     float ya;    // rcp_refined(a) for div_shared (0: a outside [2^-40, 2^40], IEEE division)
+    float tk;    // a * tmin (sphere_may_hit)
+    float ktk;   // 2^-20 * tk
+    float gk;    // 1 - 2^-20 where the sphere filter applies (a in [2^-40, 2^40]), else 0
+    float nk;    // -2^-20 in a VGPR: as an SGPR operand (gfx9 VOP3 has no literal) its FMAs would take 4
+                 // clocks instead of dual-issuing at 2 (profiles/r4_valu_peak/)
 };
 RTW_DHD RayTrav ray_trav(const Ray& r, bool fast_box) {
     RayTrav t;
@@ -397,10 +402,32 @@ RTW_DHD RayTrav ray_trav(const Ray& r, bool fast_box) {
     // fast-reject only where every intermediate below stays normal and finite
     t.rcp_a = (t.a > 1e-30f && t.a < 1e30f) ? RTW_RCP_EST(t.a) : 0.0f;
     t.ya = (t.a >= 0x1p-40f && t.a <= 0x1p40f) ? rcp_refined(t.a, t.rcp_a) : 0.0f;
+    t.tk = t.a * 0.001f;  // kTmin (camera.zig:187)
+    t.ktk = t.tk * 9.5367432e-07f;
+    t.gk = (t.a >= 0x1p-40f && t.a <= 0x1p40f) ? 0.99999905f : 0.0f;  // 1 - 2^-20
+    t.nk = -9.5367432e-07f;
+#if defined(__HIP_DEVICE_COMPILE__)
+    asm volatile("" : "+v"(t.nk));  // keep it a per-lane register
+#endif
     return t;
 }
 
 constexpr float kTmin = 0.001f;  // camera.zig:187
+
+// The sphere fast-reject of sphere_leaf (derivation there and in DESIGN.md §4): false only if no root of
+// Sphere.hit's exact IEEE arithmetic (objects.zig:127-136) can lie in (tmin, closest).  tk = fl(a * tmin),
+// ktk = 2^-20 * tk, gk = 1 - 2^-20 (0: no filtering, every disc >= 0 passes).  Host and device run the same
+// fp32 operations (FMAs are correctly rounded on both), so tests/test_filter.py checks it on the host.
+// nk = -2^-20 (RayTrav::nk: a VGPR on the device).
+RTW_DHD bool sphere_may_hit(float hb, float disc, float a, float closest, float tk, float ktk, float gk,
+                            float nk = -9.5367432e-07f) {
+    const float xb = hb + tk;                                // X = hb + a tmin
+    const float yb = __builtin_fmaf(-a, closest, -hb);       // Y = -hb - a closest (one rounding; -inf for inf)
+    const float lx = __builtin_fmaf(nk, __builtin_fabsf(xb), xb - ktk);
+    const float ly = __builtin_fmaf(nk, __builtin_fabsf(yb), __builtin_fmaf(nk, __builtin_fabsf(hb), yb));
+    const float b = __builtin_fmaxf(__builtin_fmaxf(lx, ly) * gk, 0.0f);  // maxNum: a NaN bound becomes 0
+    return disc >= b * b;
+}
 
 // ---------------------------------------------------------------------------
 // Non-sphere world objects (scenes with RTW_F_GEOM / RTW_F_MEDIUM): quads,
@@ -660,47 +687,22 @@ RTW_DHD void sphere_leaf(const rtw_launch& L, const Ray& r, const RayTrav& rt, f
 #endif
     const float disc = half_b * half_b - rt.a * c;
     bool exact = disc >= 0;
-    bool quick = false;  // the exact roots by sqrt_refined / div_shared (operands in range)
-    float sa = 0.0f;
 #if !defined(RTW_ABLATE_MATH)
-    // Exact fast-reject: with hardware sqrt/rcp estimates (<= 1 ulp each) the
-    // candidate roots q1, q2 are within (|hb| + sq) / a * 6e-7 of the correctly
-    // rounded roots of objects.zig:130-136.  If neither can lie in
-    // (tmin, closest) even with a 2^-18 relative margin, the exact test
-    // would reject both: skip the IEEE sqrt and divisions.  Guards keep every
-    // intermediate finite and normal; otherwise the exact path runs.
-    // Written as ONE predicate (no nested branch): a nested-branch form was
-    // miscompiled by hipcc 7.2 (numerator left undefined on the guard-false edge).
-    {
-        // The exact roots satisfy r1 <= r2 (a > 0), so one of them lies in (tmin, closest)
-        // only if r2 > tmin and r1 < closest: with |r - q| <= e, only if q2 + e2 > tmin and
-        // q1 - e1 < closest (a necessary condition; non-short-circuit & and |, no branches).
-        // Error of an estimated root, u = 2^-24: the reference's r = fl(fl(-hb -+ sq) / a) with sq
-        // the correctly rounded sqrt; the estimate q = fl(fl(-hb -+ sa) * rcp_a) with sa and rcp_a
-        // within 1 ulp (<= 2u relative) of sqrt(disc) and 1/a.  |sa - sq| <= 3.01u sa, so the
-        // numerators m, n differ by <= 3.02u sa + 2.01u |m|, and with the roundings of the
-        // division, the product and rcp_a: |q - r| <= (3.04u sa + 6.03u |m|) rcp_a
-        // < 6.1u (sa + |m|) rcp_a.  e = 2^-20 (sa + |m|) rcp_a is 2.6x that, which also covers
-        // the roundings of e itself; under the guard the quantities are normal (an underflowed
-        // e or q errs by <= 2^-149 absolute, far below the float gaps at kTmin and at closest
-        // >= kTmin).  r2 > kTmin means r2 >= nextafter(kTmin), so fl(q2 + e2) > kTmin, and
-        // likewise for r1 < closest.  Bounding each root by its own numerator keeps e2 tight
-        // where -hb + sa cancels -- the near-zero root of a ray leaving a large sphere's surface
-        // (the ground): a shared bound (|hb| + sa) * 2^-18 left those undecided (exact path).
-        sa = RTW_SQRT_EST(disc);
-        const float m1 = -half_b - sa, m2 = -half_b + sa;
-        const float q1 = m1 * rt.rcp_a, q2 = m2 * rt.rcp_a;
-        const float re = rt.rcp_a * 9.5367432e-07f;  // 2^-20 (a power of two: exact)
-        const float e1 = (sa + __builtin_fabsf(m1)) * re, e2 = (sa + __builtin_fabsf(m2)) * re;
-        const bool guard = L.fast_reject & (rt.rcp_a != 0.0f) & (disc > 1e-30f) & (disc < 1e30f) &
-                           (__builtin_fabsf(half_b) < 1e15f);
-        const bool plausible = (q2 + e2 > kTmin) & (q1 - e1 < closest);
-        exact = exact & (plausible | !guard);
-        // under the guard |-hb -+ sq| < 2^51 and disc >= 2^-96; with a in [2^-40, 2^40] the
-        // divisions are unscaled except for quotients below 2^-80, which kTmin rejects
-        // either way
-        quick = guard & (rt.ya != 0.0f) & (disc >= 0x1p-96f);
-    }
+    // Exact fast-reject (round 4): no square root, no division.  A root of objects.zig:130-136 lies in
+    // (tmin, closest) only if root2 > tmin and root1 < closest (root1 <= root2: a > 0 and the rounded
+    // operations are monotone), and with s = sqrt(disc) those hold only if s > max(Lx, Ly) for
+    //   Lx = X - 2.03u|X| - 2.04u T,   X = hb + T, T = a * tmin          (root2 > tmin)
+    //   Ly = Y - 3.06u|Y| - 1.02u|hb|, Y = -hb - a * closest             (root1 < closest; -inf for inf)
+    // (u = 2^-24; the slack covers the reference's roundings of sqrt, the numerators and the divisions,
+    // and the roundings of X and Y here).  sphere_may_hit computes lower bounds of both with k = 2^-20 =
+    // 16u margins, b = max(them) * (1 - 2^-20) clamped at 0, and accepts iff disc >= fl(b * b): s > b >= 0
+    // gives disc = s^2 > fl(b^2), so a ray the exact test would accept is never rejected (derivation in
+    // DESIGN.md §4; tests/test_filter.py checks it against the exact test on adversarial inputs).  The
+    // bound needs T normal: the ray's guard factor rt.gk is 0 (every disc >= 0 goes exact) unless
+    // fast_reject and a in [2^-40, 2^40].  Overflowing squares only reject rays the reference rejects.
+    // Measured on gfx950 (profiles/r4_valu_peak/): the old filter's v_sqrt_f32 took 8 clocks per wave and
+    // its SGPR compares 4; these adds, FMAs and maxes dual-issue at 2.
+    exact = sphere_may_hit(half_b, disc, rt.a, closest, rt.tk, rt.ktk, L.fast_reject ? rt.gk : 0.0f, rt.nk);
 #endif
 #if defined(RTW_DIAG_WALK) && defined(__HIP_DEVICE_COMPILE__)
     const float closest_in = closest;
@@ -714,8 +716,15 @@ RTW_DHD void sphere_leaf(const rtw_launch& L, const Ray& r, const RayTrav& rt, f
 #endif
     if (exact) {
         float sq, root, root2;
+        bool quick = false;  // the exact roots by sqrt_refined / div_shared (operands in range)
+#if !defined(RTW_ABLATE_MATH)
+        // |-hb -+ sq| < 2^51 and disc >= 2^-96; with a in [2^-40, 2^40] (ya != 0) the divisions are
+        // unscaled except for quotients below 2^-80, which kTmin rejects either way
+        quick = L.fast_reject & (rt.ya != 0.0f) & (disc >= 0x1p-96f) & (disc < 1e30f) &
+                (__builtin_fabsf(half_b) < 1e15f);
+#endif
         if (quick) {
-            sq = sqrt_refined(disc, sa);
+            sq = sqrt_refined(disc, RTW_SQRT_EST(disc));
             root = div_shared(-half_b - sq, rt.a, rt.ya);
             root2 = div_shared(-half_b + sq, rt.a, rt.ya);
         } else {
