@@ -98,7 +98,8 @@ def main():
 
     pkg = importlib.import_module("zig-raytracing-weekend_amd")
     L = pkg.lib()
-    build_id = L.rtw_build_id().decode()
+    # (an A/B build of an ABI before 6, RTW_LIB=..., has no build id: its rooflines are not derived anyway)
+    build_id = L.rtw_build_id().decode() if hasattr(L, "rtw_build_id") else "pre-abi6"
     cfg = pkg.configs.CONFIGS[args.config]
     objs = cfg.objects()
     bvh_mode = {"sah": pkg._abi.RTW_BVH_SAH, "reference": pkg._abi.RTW_BVH_REFERENCE}[args.bvh]
