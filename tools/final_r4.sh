@@ -20,6 +20,7 @@ if [ "${SKIP_PMC:-0}" != 1 ]; then
     echo "pmc $c: $(grep '^build' "$OUT/pmc_$c/valu/summary.txt") / $(grep '^build' "$OUT/pmc_$c/traffic/summary.txt")"
   done
 fi
+[ "${SKIP_BENCH:-0}" = 1 ] && exit 0
 timeout -k 10 300 python bench.py > "$OUT/c2_bench.json" 2> "$OUT/c2.err" || exit $?
 timeout -k 10 300 python bench.py --config c3 --no-cpu-baseline --steps 1 > "$OUT/c3_bench.json" 2> "$OUT/c3.err" || exit $?
 for c in c4 c5 cornell cornell_smoke simple_light; do
