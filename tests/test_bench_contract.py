@@ -71,3 +71,45 @@ def test_rocprof_summary_agrees_with_bench_events():
             assert abs(mean_us / 1e3 - d["roofline"]["avg_launch_ms"]) <= 0.05 * d["roofline"]["avg_launch_ms"]
             return
     raise AssertionError(f"{kernel} not in the rocprof summary")
+
+
+PMC_CONFIGS = ["c2", "c3", "c4", "c5", "cornell", "cornell_smoke", "simple_light"]
+
+
+@pytest.mark.parametrize("config", PMC_CONFIGS)
+def test_pmc_passes_are_from_this_build(rtw, config):
+    """Every committed PMC pass bench.py derives a roofline from (profiles/pmc_{valu,traffic}_<config>_sah.json)
+    was taken on the library these sources build: its _build.build_id is rtw_build_id() (test_abi.py checks
+    that the loaded library IS these sources).  bench.py uses no pass of another build (roofline.frac null)."""
+    want = rtw.lib().rtw_build_id().decode()
+    for kind in ("valu", "traffic"):
+        with open(os.path.join(REPO, "profiles", f"pmc_{kind}_{config}_sah.json")) as f:
+            d = json.load(f)
+        assert d.get("_build", {}).get("build_id") == want, (kind, config, d.get("_build"), want)
+        assert d["_build"].get("config") == config
+
+
+def test_bench_refuses_a_stale_pmc_pass(tmp_path, monkeypatch):
+    """bench.py's PMC readers return nothing (so roofline.frac is null) for a pass of another build."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(REPO, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    prof = tmp_path / "profiles"
+    prof.mkdir()
+    entry = {"lane_ops": 1e11, "insts_valu": 3e9, "active_inst_valu": 3e9, "thread_cycles_valu": 1e11,
+             "kernels": ["wf_step_clds<0u>"], "lane_util": 0.5}
+    json.dump({"wf_step": entry, "_build": {"build_id": "aaaa", "config": "c2"}}, open(prof / "pmc_valu_c2_sah.json", "w"))
+    json.dump({"wf_step": {"traffic_bytes": 1e10}, "_build": {"build_id": "aaaa", "config": "c2"}},
+              open(prof / "pmc_traffic_c2_sah.json", "w"))
+    monkeypatch.setattr(bench, "REPO", str(tmp_path))
+    monkeypatch.delenv("RTW_LIB", raising=False)
+
+    class A:
+        config, bvh, spp, tuning = "c2", "sah", 0, ""
+    assert bench.pmc_valu(A, "wf_step", "aaaa")[0] == entry
+    assert bench.pmc_traffic(A, "wf_step", "aaaa")[0] == 10_000_000_000
+    e, src = bench.pmc_valu(A, "wf_step", "bbbb")
+    assert e is None and "stale" in src
+    t, src = bench.pmc_traffic(A, "wf_step", "bbbb")
+    assert t is None and "stale" in src

@@ -293,7 +293,13 @@ __device__ __forceinline__ uint32_t wf_push_bucketed(const rtw_wf& W, uint32_t i
     return rank < room ? base + fill + rank : fresh + (rank - room);
 }
 
-// the unused slots of the wave's partly filled blocks: dead (depth 0), so the next iteration skips them
+// packed path state (see wf_load_ray_it)
+template <uint32_t FEAT>
+constexpr bool wf_packed() { return (FEAT & (RTW_F_MOVING | RTW_F_LIGHT | RTW_F_GEOM | RTW_F_MEDIUM)) == 0; }
+
+// the unused slots of the wave's partly filled blocks: dead (depth 0; packed state: d = 0), so the next
+// iteration skips them
+template <uint32_t FEAT>
 __device__ __forceinline__ void wf_close_blocks(const rtw_wf& W, uint32_t it, uint32_t bb, uint32_t bf) {
     const rtw_wf_set& O = W.set[(it + 1u) & 1u];
     uint64_t open = __ballot(__lane_id() < RTW_WF_BUCKETS && bf > 0u && bf < 64u);
@@ -301,7 +307,10 @@ __device__ __forceinline__ void wf_close_blocks(const rtw_wf& W, uint32_t it, ui
         const uint32_t h = (uint32_t)__builtin_ctzll(open);
         open &= open - 1ull;
         const uint32_t base = __shfl(bb, (int)h), fill = __shfl(bf, (int)h);
-        if (__lane_id() >= fill) O.ray_d[base + __lane_id()] = make_float4(0, 0, 0, 0);
+        if (__lane_id() >= fill) {
+            O.ray_d[base + __lane_id()] = make_float4(0, 0, 0, 0);
+            if constexpr (wf_packed<FEAT>()) O.ray_o[base + __lane_id()] = make_float4(0, 0, 0, 0);
+        }
     }
 }
 
@@ -344,6 +353,71 @@ __device__ __forceinline__ void wf_load_state(const rtw_launch& L, const rtw_wf_
     }
 }
 
+// Packed path state (round 4) of static sphere scenes without emitters (BASELINE configs 2-5): no ray time
+// is ever read (no moving sphere), no radiance is carried (no emitter), and the remaining depth of every
+// path in iteration it's input set is max_depth - it, so a path is three 16-B streams instead of five
+// (60 B): ray_o = (o.xyz, d.x), ray_d = (d.y, d.z, thr.x, thr.y), thr = (thr.z, pid, rng lo, rng hi).  A dead
+// slot (a closed block's tail) has d = 0: no queued ray has a zero direction (Lambertian replaces a
+// near-zero one by the normal, material.zig:47-50; Metal absorbs dot(d, n) <= 0, :68; Dielectric's is a
+// unit-length reflection or refraction, :80-98).  The same values in the same registers: bit-identical.
+// The split shade of C4 moves 104 instead of 128 B per surviving ray (-19 %).
+// the ray of slot `slot` of iteration it's input set; depth 0 = no path.  txy: packed only, thr.xy
+template <uint32_t FEAT>
+__device__ __forceinline__ Ray wf_load_ray_it(const rtw_launch& L, const rtw_wf_set& S, uint32_t slot, uint32_t it,
+                                              uint32_t& depth, float2& txy) {
+    if constexpr (wf_packed<FEAT>()) {
+        const float4 o = S.ray_o[slot], d = S.ray_d[slot];
+        Ray r;
+        r.o = mk(o.x, o.y, o.z);
+        r.d = mk(o.w, d.x, d.y);
+        r.time = 0.0f;
+        depth = ((fbits(o.w) | fbits(d.x) | fbits(d.y)) << 1) ? L.max_depth - it : 0u;  // +-0 components: d = 0
+        txy = make_float2(d.z, d.w);
+        return r;
+    } else {
+        txy = make_float2(0.0f, 0.0f);
+        return wf_load_ray(S, slot, depth);
+    }
+}
+
+// throughput / radiance / RNG state / path id of a live path of iteration it >= 1 (the first bounce's are
+// implicit: thr 1, radiance 0, and the camera code makes the RNG state and pid = slot)
+template <uint32_t FEAT>
+__device__ __forceinline__ void wf_load_rest(const rtw_launch& L, const rtw_wf_set& S, uint32_t slot, uint32_t depth,
+                                             float2 txy, f3& thr, f3& acc, uint64_t& rng, uint32_t& pid) {
+    if constexpr (wf_packed<FEAT>()) {
+        const float4 c = S.thr[slot];
+        thr = mk(txy.x, txy.y, c.x);
+        acc = mk(0, 0, 0);
+        pid = fbits(c.y);
+        rng = (uint64_t)fbits(c.z) | ((uint64_t)fbits(c.w) << 32);
+    } else {
+        pid = S.pid[slot];
+        rng = S.rng[slot];
+        wf_load_state<FEAT>(L, S, slot, depth, thr, acc);
+    }
+}
+
+// a surviving path into slot `out` of the output set (depth: its remaining depth after this bounce)
+template <uint32_t FEAT>
+__device__ __forceinline__ void wf_store_path(const rtw_wf_set& O, uint32_t out, const Ray& r, uint32_t depth, f3 thr,
+                                              uint64_t rng, uint32_t pid, f3 acc) {
+    if constexpr (wf_packed<FEAT>()) {
+        O.ray_o[out] = make_float4(r.o.x, r.o.y, r.o.z, r.d.x);
+        O.ray_d[out] = make_float4(r.d.y, r.d.z, thr.x, thr.y);
+        O.thr[out] = make_float4(thr.z, __uint_as_float(pid), __uint_as_float((uint32_t)rng),
+                                 __uint_as_float((uint32_t)(rng >> 32)));
+        (void)depth;
+        (void)acc;
+    } else {
+        wf_store_ray(O, out, r, depth);
+        O.thr[out] = make_float4(thr.x, thr.y, thr.z, 0);
+        O.rng[out] = rng;
+        O.pid[out] = pid;
+        if constexpr ((FEAT & RTW_F_LIGHT) != 0) O.acc[out] = make_float4(acc.x, acc.y, acc.z, 0);
+    }
+}
+
 // Iteration 0: path `slot`'s camera ray and RNG state (camera.zig:169-180 with the +1 pixel offset,
 // camera.zig:100-101), generated in registers by the kernel that needs them -- the fused step, and both
 // the split trace and the split shade (each recomputes it: no ray or RNG state goes through HBM before
@@ -374,14 +448,15 @@ __device__ __forceinline__ bool wf_camera(const rtw_launch& L, const rtw_wf& W, 
 // depth 0 = no path.  rng: the camera ray's RNG state (CAM).
 template <uint32_t FEAT, bool CAM>
 __device__ __forceinline__ Ray wf_input_ray(const rtw_launch& L, const rtw_wf& W, const rtw_wf_set& S,
-                                            uint32_t slot, uint32_t& depth, rtw_rng& rng) {
+                                            uint32_t slot, uint32_t it, uint32_t& depth, rtw_rng& rng, float2& txy) {
     if constexpr (CAM) {
         Ray r;
         depth = wf_camera<FEAT>(L, W, true, slot, r, rng) ? L.max_depth : 0u;
+        txy = make_float2(0.0f, 0.0f);
         return r;
     }
     rng.s = 0;
-    return wf_load_ray(S, slot, depth);
+    return wf_load_ray_it<FEAT>(L, S, slot, it, depth, txy);
 }
 
 // L.geom_lds: copy the scene's quads | members | instances (one contiguous range of the scene
@@ -775,7 +850,8 @@ __global__ __launch_bounds__(256) void wf_trace(rtw_launch L, rtw_wf W, uint32_t
                 if (e.get(W, slot)) {
                     uint32_t depth;
                     rtw_rng rng;
-                    const Ray r = wf_input_ray<FEAT, CAM>(G, W, S, slot, depth, rng);
+                    float2 txy;
+                    const Ray r = wf_input_ray<FEAT, CAM>(G, W, S, slot, it, depth, rng, txy);
                     if (depth) {
                         float t;
                         const int h = traverse<FEAT>(wf_lds_nodes, G, r, t, cnt, CAM ? rng.s : wf_mkey<FEAT>(S, slot));
@@ -804,7 +880,8 @@ __global__ __launch_bounds__(256) void wf_trace(rtw_launch L, rtw_wf W, uint32_t
         if (e.get(W, slot)) {
             uint32_t depth;
             rtw_rng rng;
-            const Ray r = wf_input_ray<FEAT, CAM>(L, W, S, slot, depth, rng);
+            float2 txy;
+            const Ray r = wf_input_ray<FEAT, CAM>(L, W, S, slot, it, depth, rng, txy);
             if (depth) {
                 float t = kInf;
                 int h = -1;
@@ -841,7 +918,8 @@ __global__ __launch_bounds__(1024) void wf_trace_clds(rtw_launch L, rtw_wf W, ui
         if (e.get(W, slot)) {
             uint32_t depth;
             rtw_rng rng;
-            const Ray r = wf_input_ray<FEAT, CAM>(L, W, S, slot, depth, rng);
+            float2 txy;
+            const Ray r = wf_input_ray<FEAT, CAM>(L, W, S, slot, it, depth, rng, txy);
             if (depth) {
                 float t;
                 const int h = L.counters ? traverse_compact<true, true>(L, wf_clds, r, t, cnt)
@@ -889,16 +967,23 @@ __device__ __forceinline__ void wf_shade_body(const rtw_launch& L, const rtw_wf&
         HitPrep hp;
         bool hitp = false, need_uv = false;
         if (e.get(W, slot)) {
-            const Ray r = wf_input_ray<FEAT, CAM>(L, W, S, slot, depth, rng);
+            float2 txy;
+            const Ray r = wf_input_ray<FEAT, CAM>(L, W, S, slot, it, depth, rng, txy);
             if (depth) {
-                pid = CAM ? slot : S.pid[slot];
                 const float2 h = W.hit[slot];
                 const int hit = __float_as_int(h.y);
-                wf_load_state<FEAT>(L, S, slot, depth, thr, acc);
+                if (CAM) {
+                    pid = slot;
+                    thr = mk(1, 1, 1);
+                    acc = mk(0, 0, 0);
+                } else {
+                    uint64_t rs;
+                    wf_load_rest<FEAT>(L, S, slot, depth, txy, thr, acc, rs, pid);
+                    rng.s = rs;
+                }
                 if (hit < 0) {
                     acc = acc + thr * background(L, r);
                 } else {
-                    if (!CAM) rng.s = S.rng[slot];
                     if constexpr ((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM)) == 0) {
                         // sphere scenes: the split form of the fused step (hit record, then one
                         // randomUnitVector rejection loop for the wave, then the material)
@@ -932,15 +1017,9 @@ __device__ __forceinline__ void wf_shade_body(const rtw_launch& L, const rtw_wf&
         if (CAM && !depth) W.ls[slot] = make_float4(0, 0, 0, 0);  // padding, rayColor(r, 0) = 0
         const uint32_t out = bucketed ? wf_push_bucketed(W, it, push, push ? wf_bucket(sc.d) & W.sort_mask : 0u, bb, bf)
                                       : wf_push(W, it, push);
-        if (push) {
-            wf_store_ray(O, out, sc, depth - 1);
-            O.thr[out] = make_float4(thr.x, thr.y, thr.z, 0);
-            O.rng[out] = rng.s;
-            O.pid[out] = pid;
-            if constexpr ((FEAT & RTW_F_LIGHT) != 0) O.acc[out] = make_float4(acc.x, acc.y, acc.z, 0);
-        }
+        if (push) wf_store_path<FEAT>(O, out, sc, depth - 1, thr, rng.s, pid, acc);
     }
-    if (bucketed) wf_close_blocks(W, it, bb, bf);
+    if (bucketed) wf_close_blocks<FEAT>(W, it, bb, bf);
 }
 
 // tail: the paths still queued after the last wavefront iteration, each to
@@ -968,11 +1047,12 @@ __device__ __forceinline__ void wf_tail_body(const rtw_launch& L, const rtw_wf& 
             uint32_t slot = 0;
             const bool ok = wf_nth(W, it, m, slot, end);
             exhausted = __ballot(end && !active) == need;
-            if (!active && ok) {
-                r = wf_load_ray(S, slot, depth);
-                wf_load_state<FEAT>(L, S, slot, depth, thr, acc);
-                rng.s = S.rng[slot];
-                pid = it == 0 ? slot : S.pid[slot];
+            if (!active && ok) {  // (the tail's input is iteration it >= 1's: wf_iters >= 1)
+                float2 txy;
+                r = wf_load_ray_it<FEAT>(L, S, slot, it, depth, txy);
+                uint64_t rs = 0;
+                if (depth) wf_load_rest<FEAT>(L, S, slot, depth, txy, thr, acc, rs, pid);
+                rng.s = rs;
                 active = depth != 0;
             }
         }
@@ -1177,12 +1257,13 @@ __device__ __forceinline__ void wf_step_body(const rtw_launch& L, const rtw_wf& 
             if (got && !live) W.ls[slot] = make_float4(0, 0, 0, 0);  // rayColor(r, 0) = 0
             depth = live ? L.max_depth : 0;
         } else if (got) {
-            r = wf_load_ray(S, slot, depth);
+            float2 txy;
+            r = wf_load_ray_it<FEAT>(L, S, slot, it, depth, txy);
             live = depth != 0;
             if (live) {  // issued before the walk: the loads land while it runs
-                pid = S.pid[slot];
-                rng.s = S.rng[slot];
-                wf_load_state<FEAT>(L, S, slot, depth, thr, acc);
+                uint64_t rs;
+                wf_load_rest<FEAT>(L, S, slot, depth, txy, thr, acc, rs, pid);
+                rng.s = rs;
             }
         }
         Ray sc;
@@ -1273,15 +1354,9 @@ __device__ __forceinline__ void wf_step_body(const rtw_launch& L, const rtw_wf& 
         if (live && !push) W.ls[pid] = make_float4(acc.x, acc.y, acc.z, 0);
         const uint32_t out = bucketed ? wf_push_bucketed(W, it, push, push ? wf_bucket(sc.d) & W.sort_mask : 0u, bb, bf)
                                       : wf_push(W, it, push);
-        if (push) {
-            wf_store_ray(O, out, sc, depth - 1);
-            O.thr[out] = make_float4(thr.x, thr.y, thr.z, 0);
-            O.rng[out] = rng.s;
-            O.pid[out] = pid;
-            if constexpr ((FEAT & RTW_F_LIGHT) != 0) O.acc[out] = make_float4(acc.x, acc.y, acc.z, 0);
-        }
+        if (push) wf_store_path<FEAT>(O, out, sc, depth - 1, thr, rng.s, pid, acc);
     }
-    if (bucketed) wf_close_blocks(W, it, bb, bf);
+    if (bucketed) wf_close_blocks<FEAT>(W, it, bb, bf);
     flush_counters(L, cnt, 0);
 }
 
