@@ -318,7 +318,8 @@ def test_v1_knobs_invariant(rtw, book1, knob):
                                   {"lds": 127 & ~2, "wide_walk": 0}, {"fuse": 5}, {"lds": 127 & ~2, "fuse": 5},
                                   {"lds": 127 & ~2, "fuse": 5, "wide_walk": 0}, {"hoist": 0}, {"hoist": 0, "fuse": 0},
                                   {"sort_iters": 0}, {"sort_iters": 50}, {"sort_iters_split": 50, "fuse": 0}, {"sort_iters_split": 0, "fuse": 0},
-                                  {"sort_iters": 2, "wf_iters": 1}, {"sort_bits": 0}, {"sort_bits": 2, "fuse": 0}])
+                                  {"sort_iters": 2, "wf_iters": 1}, {"sort_bits": 0}, {"sort_bits": 2, "fuse": 0},
+                                  {"fuse": 8}, {"fuse": 8, "sort_iters_split": 50}, {"fuse": 10, "lds": 127 & ~2}])
 def test_wavefront_knobs_invariant(rtw, book1, knob):
     """Wavefront tuning (rtw_tuning: bounces before the tail kernel, batch size ->
     many batches, FMA vs reference slab test, LDS-staged nodes, SAH leaf runs of up
@@ -327,7 +328,8 @@ def test_wavefront_knobs_invariant(rtw, book1, knob):
     one node ordering instead of 8, camera rays against per-tile candidate lists vs
     the walk, the two-wide stack walk through L1/L2 vs the
     octant-ordered compact walk, the fused step through L1/L2, dominant spheres hoisted ahead of the
-    tree or not, survivors filed into direction-bucketed blocks or appended) never changes a pixel."""
+    tree or not, survivors filed into direction-bucketed blocks or appended, the split kernels' queues in the
+    packed 48-B or the 60-B path state) never changes a pixel."""
     arr, world = book1
     cam = rtw.book1_camera(image_width=300, aspect_ratio=1.5, spp=5).init()
     ref = render_rows(rtw, world, cam, 0, 200, 0, 5, 4)
@@ -357,6 +359,27 @@ def test_compact_nodes_are_exact(rtw, n, seed):
     assert np.array_equal(outs[0], outs[2])  # the two-wide stack walk (rtw_wide2_nodes): same hits
     assert np.array_equal(outs[0], outs[3])  # the ground sphere inside the tree (no hoisting)
     # (the defaults also give camera rays the frustum-walked tile lists of large trees: same hits)
+
+
+@pytest.mark.parametrize("scene", ["ref_head", "book1"])
+def test_hoisted_ground_to_the_horizon(rtw, scene):
+    """The FMA slab test's pad covers secondary-ray origins on the hoisted r = 1000 ground, hundreds of units
+    out at the horizon (rtw_bvh.hip: the pad's extent spans every object box, hoisted ones included): the
+    ground hoisted ahead of the tree or inside it, and the exact slab test, give the same image.  ref_head has
+    moving spheres (the padded 32-B fp32 walk); the camera looks up so the horizon crosses the frame."""
+    arr = rtw.flatten(rtw.worlds.generate_world(0, scene))
+    cam = rtw.Camera(aspect_ratio=1.5, image_width=360, samples_per_pixel=4, max_depth=50,
+                     background_mode=rtw._abi.RTW_BG_GRADIENT, vfov=40.0, lookfrom=(13.0, 2.0, 3.0),
+                     lookat=(0.0, 2.0, 0.0), defocus_angle=0.0, focus_dist=10.0).init()
+    outs = []
+    for tu in ({"hoist": 1}, {"hoist": 0}, {"hoist": 1, "fast_box": 0}, {"hoist": 0, "fast_box": 0}):
+        w = rtw.World(arr, tuning=tu)
+        assert w.stats()["n_hoisted"] == tu["hoist"]
+        outs.append(render_rows(rtw, w, cam, 0, cam.derived.image_height, 0, 4, 11))
+        w.close()
+    assert np.isfinite(outs[0]).all()
+    for o in outs[1:]:
+        assert np.array_equal(outs[0], o)
 
 
 @pytest.mark.parametrize("scene", ["book1", "stress"])

@@ -632,7 +632,7 @@ int run_wavefront(rtw_ctx* ctx, rtw_launch L, hipStream_t stream, rtw_timer* T) 
         S.pid = reinterpret_cast<uint32_t*>(take(Q * 4));
     }
     W.hit = reinterpret_cast<float2*>(take(Q * 8));
-    W.ls = reinterpret_cast<float4*>(take(P * 16));
+    W.ls = reinterpret_cast<rtw_rgb*>(take(P * sizeof(rtw_rgb)));
     for (int k = 0; k < 3; k++) W.len[k] = reinterpret_cast<uint32_t*>(take(RTW_WF_STRIPES * RTW_WF_LEN_STRIDE * 4));
     W.n_pix = (uint32_t)n_pix;
     W.iters = ctx->wf_iters;

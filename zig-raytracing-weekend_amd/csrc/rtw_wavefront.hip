@@ -69,7 +69,7 @@ __device__ __forceinline__ bool wf_chunk0(const rtw_wf& W, uint32_t w, uint32_t 
 // Path ids are tile-major: path p is sample s_local of pixel q (in tile order) with
 // p = ((q / 64) * n_s + s_local) * 64 + q % 64, so chunk c = p / 64 is sample c % n_s of tile c / n_s and
 // the paths of one tile-run (wf_chunk0) are RUN consecutive chunks: the radiance stores of a block's rays
-// (W.ls[pid], pids of one run) stay within 16 KB, and the reduce reads 64 consecutive pixels per sample.
+// (W.ls[pid], pids of one run) stay within 12 KB, and the reduce reads 64 consecutive pixels per sample.
 __device__ __forceinline__ void wf_path(const rtw_wf& W, uint32_t p, uint32_t& s_local, uint32_t& q) {
     const uint32_t c = p >> 6, t = c / W.n_s;
     s_local = c - t * W.n_s;
@@ -294,13 +294,18 @@ __device__ __forceinline__ uint32_t wf_push_bucketed(const rtw_wf& W, uint32_t i
 }
 
 // packed path state (see wf_load_ray_it)
+#if defined(RTW_NO_PACK_SPLIT)
+#define wf_pk(W) false  // A/B variant: the kernels outside the fused step never read the packed state
+#else
+#define wf_pk(W) ((W).packed != 0u)
+#endif
 template <uint32_t FEAT>
 constexpr bool wf_packed() { return (FEAT & (RTW_F_MOVING | RTW_F_LIGHT | RTW_F_GEOM | RTW_F_MEDIUM)) == 0; }
 
 // the unused slots of the wave's partly filled blocks: dead (depth 0; packed state: d = 0), so the next
 // iteration skips them
 template <uint32_t FEAT>
-__device__ __forceinline__ void wf_close_blocks(const rtw_wf& W, uint32_t it, uint32_t bb, uint32_t bf) {
+__device__ __forceinline__ void wf_close_blocks(const rtw_wf& W, uint32_t it, uint32_t bb, uint32_t bf, bool pk) {
     const rtw_wf_set& O = W.set[(it + 1u) & 1u];
     uint64_t open = __ballot(__lane_id() < RTW_WF_BUCKETS && bf > 0u && bf < 64u);
     while (open) {
@@ -309,7 +314,7 @@ __device__ __forceinline__ void wf_close_blocks(const rtw_wf& W, uint32_t it, ui
         const uint32_t base = __shfl(bb, (int)h), fill = __shfl(bf, (int)h);
         if (__lane_id() >= fill) {
             O.ray_d[base + __lane_id()] = make_float4(0, 0, 0, 0);
-            if constexpr (wf_packed<FEAT>()) O.ray_o[base + __lane_id()] = make_float4(0, 0, 0, 0);
+            if (wf_packed<FEAT>() && pk) O.ray_o[base + __lane_id()] = make_float4(0, 0, 0, 0);
         }
     }
 }
@@ -364,8 +369,9 @@ __device__ __forceinline__ void wf_load_state(const rtw_launch& L, const rtw_wf_
 // the ray of slot `slot` of iteration it's input set; depth 0 = no path.  txy: packed only, thr.xy
 template <uint32_t FEAT>
 __device__ __forceinline__ Ray wf_load_ray_it(const rtw_launch& L, const rtw_wf_set& S, uint32_t slot, uint32_t it,
-                                              uint32_t& depth, float2& txy) {
-    if constexpr (wf_packed<FEAT>()) {
+                                              uint32_t& depth, float2& txy,
+                                              bool pk) {
+    if (wf_packed<FEAT>() && pk) {
         const float4 o = S.ray_o[slot], d = S.ray_d[slot];
         Ray r;
         r.o = mk(o.x, o.y, o.z);
@@ -384,8 +390,8 @@ __device__ __forceinline__ Ray wf_load_ray_it(const rtw_launch& L, const rtw_wf_
 // implicit: thr 1, radiance 0, and the camera code makes the RNG state and pid = slot)
 template <uint32_t FEAT>
 __device__ __forceinline__ void wf_load_rest(const rtw_launch& L, const rtw_wf_set& S, uint32_t slot, uint32_t depth,
-                                             float2 txy, f3& thr, f3& acc, uint64_t& rng, uint32_t& pid) {
-    if constexpr (wf_packed<FEAT>()) {
+                                             float2 txy, f3& thr, f3& acc, uint64_t& rng, uint32_t& pid, bool pk) {
+    if (wf_packed<FEAT>() && pk) {
         const float4 c = S.thr[slot];
         thr = mk(txy.x, txy.y, c.x);
         acc = mk(0, 0, 0);
@@ -401,8 +407,8 @@ __device__ __forceinline__ void wf_load_rest(const rtw_launch& L, const rtw_wf_s
 // a surviving path into slot `out` of the output set (depth: its remaining depth after this bounce)
 template <uint32_t FEAT>
 __device__ __forceinline__ void wf_store_path(const rtw_wf_set& O, uint32_t out, const Ray& r, uint32_t depth, f3 thr,
-                                              uint64_t rng, uint32_t pid, f3 acc) {
-    if constexpr (wf_packed<FEAT>()) {
+                                              uint64_t rng, uint32_t pid, f3 acc, bool pk) {
+    if (wf_packed<FEAT>() && pk) {
         O.ray_o[out] = make_float4(r.o.x, r.o.y, r.o.z, r.d.x);
         O.ray_d[out] = make_float4(r.d.y, r.d.z, thr.x, thr.y);
         O.thr[out] = make_float4(thr.z, __uint_as_float(pid), __uint_as_float((uint32_t)rng),
@@ -448,7 +454,8 @@ __device__ __forceinline__ bool wf_camera(const rtw_launch& L, const rtw_wf& W, 
 // depth 0 = no path.  rng: the camera ray's RNG state (CAM).
 template <uint32_t FEAT, bool CAM>
 __device__ __forceinline__ Ray wf_input_ray(const rtw_launch& L, const rtw_wf& W, const rtw_wf_set& S,
-                                            uint32_t slot, uint32_t it, uint32_t& depth, rtw_rng& rng, float2& txy) {
+                                            uint32_t slot, uint32_t it, uint32_t& depth, rtw_rng& rng, float2& txy,
+                                            bool pk) {
     if constexpr (CAM) {
         Ray r;
         depth = wf_camera<FEAT>(L, W, true, slot, r, rng) ? L.max_depth : 0u;
@@ -456,7 +463,7 @@ __device__ __forceinline__ Ray wf_input_ray(const rtw_launch& L, const rtw_wf& W
         return r;
     }
     rng.s = 0;
-    return wf_load_ray_it<FEAT>(L, S, slot, it, depth, txy);
+    return wf_load_ray_it<FEAT>(L, S, slot, it, depth, txy, pk);
 }
 
 // L.geom_lds: copy the scene's quads | members | instances (one contiguous range of the scene
@@ -851,7 +858,7 @@ __global__ __launch_bounds__(256) void wf_trace(rtw_launch L, rtw_wf W, uint32_t
                     uint32_t depth;
                     rtw_rng rng;
                     float2 txy;
-                    const Ray r = wf_input_ray<FEAT, CAM>(G, W, S, slot, it, depth, rng, txy);
+                    const Ray r = wf_input_ray<FEAT, CAM>(G, W, S, slot, it, depth, rng, txy, wf_pk(W));
                     if (depth) {
                         float t;
                         const int h = traverse<FEAT>(wf_lds_nodes, G, r, t, cnt, CAM ? rng.s : wf_mkey<FEAT>(S, slot));
@@ -881,7 +888,7 @@ __global__ __launch_bounds__(256) void wf_trace(rtw_launch L, rtw_wf W, uint32_t
             uint32_t depth;
             rtw_rng rng;
             float2 txy;
-            const Ray r = wf_input_ray<FEAT, CAM>(L, W, S, slot, it, depth, rng, txy);
+            const Ray r = wf_input_ray<FEAT, CAM>(L, W, S, slot, it, depth, rng, txy, wf_pk(W));
             if (depth) {
                 float t = kInf;
                 int h = -1;
@@ -919,7 +926,7 @@ __global__ __launch_bounds__(1024) void wf_trace_clds(rtw_launch L, rtw_wf W, ui
             uint32_t depth;
             rtw_rng rng;
             float2 txy;
-            const Ray r = wf_input_ray<FEAT, CAM>(L, W, S, slot, it, depth, rng, txy);
+            const Ray r = wf_input_ray<FEAT, CAM>(L, W, S, slot, it, depth, rng, txy, wf_pk(W));
             if (depth) {
                 float t;
                 const int h = L.counters ? traverse_compact<true, true>(L, wf_clds, r, t, cnt)
@@ -968,7 +975,7 @@ __device__ __forceinline__ void wf_shade_body(const rtw_launch& L, const rtw_wf&
         bool hitp = false, need_uv = false;
         if (e.get(W, slot)) {
             float2 txy;
-            const Ray r = wf_input_ray<FEAT, CAM>(L, W, S, slot, it, depth, rng, txy);
+            const Ray r = wf_input_ray<FEAT, CAM>(L, W, S, slot, it, depth, rng, txy, wf_pk(W));
             if (depth) {
                 const float2 h = W.hit[slot];
                 const int hit = __float_as_int(h.y);
@@ -978,7 +985,7 @@ __device__ __forceinline__ void wf_shade_body(const rtw_launch& L, const rtw_wf&
                     acc = mk(0, 0, 0);
                 } else {
                     uint64_t rs;
-                    wf_load_rest<FEAT>(L, S, slot, depth, txy, thr, acc, rs, pid);
+                    wf_load_rest<FEAT>(L, S, slot, depth, txy, thr, acc, rs, pid, wf_pk(W));
                     rng.s = rs;
                 }
                 if (hit < 0) {
@@ -1013,13 +1020,13 @@ __device__ __forceinline__ void wf_shade_body(const rtw_launch& L, const rtw_wf&
                 }
             }
         }
-        if (depth && !push) W.ls[pid] = make_float4(acc.x, acc.y, acc.z, 0);
-        if (CAM && !depth) W.ls[slot] = make_float4(0, 0, 0, 0);  // padding, rayColor(r, 0) = 0
+        if (depth && !push) W.ls[pid] = rtw_rgb{acc.x, acc.y, acc.z};
+        if (CAM && !depth) W.ls[slot] = rtw_rgb{0.0f, 0.0f, 0.0f};  // padding, rayColor(r, 0) = 0
         const uint32_t out = bucketed ? wf_push_bucketed(W, it, push, push ? wf_bucket(sc.d) & W.sort_mask : 0u, bb, bf)
                                       : wf_push(W, it, push);
-        if (push) wf_store_path<FEAT>(O, out, sc, depth - 1, thr, rng.s, pid, acc);
+        if (push) wf_store_path<FEAT>(O, out, sc, depth - 1, thr, rng.s, pid, acc, wf_pk(W));
     }
-    if (bucketed) wf_close_blocks<FEAT>(W, it, bb, bf);
+    if (bucketed) wf_close_blocks<FEAT>(W, it, bb, bf, wf_pk(W));
 }
 
 // tail: the paths still queued after the last wavefront iteration, each to
@@ -1049,9 +1056,9 @@ __device__ __forceinline__ void wf_tail_body(const rtw_launch& L, const rtw_wf& 
             exhausted = __ballot(end && !active) == need;
             if (!active && ok) {  // (the tail's input is iteration it >= 1's: wf_iters >= 1)
                 float2 txy;
-                r = wf_load_ray_it<FEAT>(L, S, slot, it, depth, txy);
+                r = wf_load_ray_it<FEAT>(L, S, slot, it, depth, txy, wf_pk(W));
                 uint64_t rs = 0;
-                if (depth) wf_load_rest<FEAT>(L, S, slot, depth, txy, thr, acc, rs, pid);
+                if (depth) wf_load_rest<FEAT>(L, S, slot, depth, txy, thr, acc, rs, pid, wf_pk(W));
                 rng.s = rs;
                 active = depth != 0;
             }
@@ -1133,7 +1140,7 @@ __device__ __forceinline__ void wf_tail_body(const rtw_launch& L, const rtw_wf& 
             }
         }
         if (active && done) {
-            W.ls[pid] = make_float4(acc.x, acc.y, acc.z, 0);
+            W.ls[pid] = rtw_rgb{acc.x, acc.y, acc.z};
             active = false;
         }
     }
@@ -1254,15 +1261,15 @@ __device__ __forceinline__ void wf_step_body(const rtw_launch& L, const rtw_wf& 
         if (it == 0) {  // the camera ray in registers (wf_camera)
             pid = slot;
             live = wf_camera<FEAT>(L, W, got, slot, r, rng);
-            if (got && !live) W.ls[slot] = make_float4(0, 0, 0, 0);  // rayColor(r, 0) = 0
+            if (got && !live) W.ls[slot] = rtw_rgb{0.0f, 0.0f, 0.0f};  // rayColor(r, 0) = 0
             depth = live ? L.max_depth : 0;
         } else if (got) {
             float2 txy;
-            r = wf_load_ray_it<FEAT>(L, S, slot, it, depth, txy);
+            r = wf_load_ray_it<FEAT>(L, S, slot, it, depth, txy, true);
             live = depth != 0;
             if (live) {  // issued before the walk: the loads land while it runs
                 uint64_t rs;
-                wf_load_rest<FEAT>(L, S, slot, depth, txy, thr, acc, rs, pid);
+                wf_load_rest<FEAT>(L, S, slot, depth, txy, thr, acc, rs, pid, true);
                 rng.s = rs;
             }
         }
@@ -1351,12 +1358,12 @@ __device__ __forceinline__ void wf_step_body(const rtw_launch& L, const rtw_wf& 
                 }
             }
         }
-        if (live && !push) W.ls[pid] = make_float4(acc.x, acc.y, acc.z, 0);
+        if (live && !push) W.ls[pid] = rtw_rgb{acc.x, acc.y, acc.z};
         const uint32_t out = bucketed ? wf_push_bucketed(W, it, push, push ? wf_bucket(sc.d) & W.sort_mask : 0u, bb, bf)
                                       : wf_push(W, it, push);
-        if (push) wf_store_path<FEAT>(O, out, sc, depth - 1, thr, rng.s, pid, acc);
+        if (push) wf_store_path<FEAT>(O, out, sc, depth - 1, thr, rng.s, pid, acc, true);
     }
-    if (bucketed) wf_close_blocks<FEAT>(W, it, bb, bf);
+    if (bucketed) wf_close_blocks<FEAT>(W, it, bb, bf, true);
     flush_counters(L, cnt, 0);
 }
 
@@ -1456,7 +1463,7 @@ __global__ __launch_bounds__(256) void wf_reduce(rtw_launch L, rtw_wf W) {
         if (wf_pixel(L, W, q, pixel, out_idx, x, y)) {
             float4 a = L.accum[out_idx];
             for (uint32_t s = 0; s < W.n_s; s++) {
-                const float4 c = W.ls[((((size_t)(q >> 6) * W.n_s) + s) << 6) | (q & 63u)];  // wf_path
+                const rtw_rgb c = W.ls[((((size_t)(q >> 6) * W.n_s) + s) << 6) | (q & 63u)];  // wf_path
                 if (is_nan3(mk(c.x, c.y, c.z))) cnt.nans++;
                 a.x += c.x;
                 a.y += c.y;
@@ -1610,14 +1617,15 @@ void wf_run_fused(const rtw_launch& L, const rtw_wf& W0, hipStream_t st, int n_c
     // iteration 0 appends to len[1]; every later iteration's output counters are
     // zeroed by the kernel two iterations before (wf_step_zero_next)
     (void)hipMemsetAsync(W0.len[1], 0, RTW_WF_STRIPES * RTW_WF_LEN_STRIDE * 4, st);
-    const rtw_wf W = wf_coherence(W0, grid * (clds ? 16u : 4u), W0.sort_iters);
+    rtw_wf W = wf_coherence(W0, grid * (clds ? 16u : 4u), W0.sort_iters);
+    W.packed = wf_packed<FEAT>() ? 1u : 0u;  // the fused step and its tail: always the packed state
     const uint32_t iters = L.max_depth < W.iters ? L.max_depth : W.iters;
     rtw_wf Wt = W;  // the camera-ray lists serve the LDS-staged steps of static sphere scenes
     if ((clds || lds) && iters) Wt = wf_lists<FEAT>(L, W, st);
     else Wt.tl_count = nullptr;
     // rayColor(depth <= 0) = 0 (camera.zig:183-185): no iteration writes W.ls, which holds the
     // previous render's radiance, so the reduce must add zeros
-    if (iters == 0) (void)hipMemsetAsync(W.ls, 0, (size_t)W.n_paths * sizeof(float4), st);
+    if (iters == 0) (void)hipMemsetAsync(W.ls, 0, (size_t)W.n_paths * sizeof(rtw_rgb), st);
     for (uint32_t it = 0; it < iters; it++) {
         RTW_TIME_BEGIN(T, RTW_K_TRACE)
         if constexpr ((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING)) == 0) {
@@ -1682,11 +1690,13 @@ void wf_run(const rtw_launch& L, const rtw_wf& W0, hipStream_t st, int n_cu, rtw
             return;
         }
     }
-    const rtw_wf W = wf_coherence(W0, g.shade * 4u, W0.sort_iters_split);  // the split kernels' queues
+    rtw_wf W = wf_coherence(W0, g.shade * 4u, W0.sort_iters_split);  // the split kernels' queues
+    // the split path keeps the 60-B state unless asked (C4: the packed state's shade -10 %, its trace +12 %)
+    W.packed = (wf_packed<FEAT>() && (L.wf_fuse & RTW_FUSE_PACK_SPLIT)) ? 1u : 0u;
     const uint32_t iters = L.max_depth < W.iters ? L.max_depth : W.iters;
     // iteration 0's trace and shade generate the camera rays themselves (wf_camera); with no
     // iteration (max_depth 0) nothing writes W.ls and the reduce must add zeros
-    if (iters == 0) (void)hipMemsetAsync(W.ls, 0, (size_t)W.n_paths * sizeof(float4), st);
+    if (iters == 0) (void)hipMemsetAsync(W.ls, 0, (size_t)W.n_paths * sizeof(rtw_rgb), st);
     const rtw_wf Wt = iters ? wf_lists<FEAT>(L, W, st) : W;  // camera rays: iteration 0 of wf_trace (L1/L2)
     const size_t w2l = wf_w2_lds<FEAT>(L);  // the two-wide walk's stacks (trace / tail through L1/L2)
     thread_local uint32_t wtrace[2] = {0, 0}, wtrace0[2] = {0, 0}, wtail[2] = {0, 0};
