@@ -1010,7 +1010,11 @@ __device__ __forceinline__ void wf_shade_body(const rtw_launch& L, const rtw_wf&
         }
         if constexpr ((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM)) == 0) {
             float uv3[3] = {0.0f, 0.0f, 0.0f};
+#if defined(RTW_COOP_REJECT_SPHERES)
+            wf_reject3(need_uv, rng, uv3);  // A/B variant: the wave-cooperative form (same draws, same states)
+#else
             if (need_uv) seq_reject<3>(rng, uv3);
+#endif
             if (hitp) {
                 const f3 ruv = need_uv ? unit_vector(mk(uv3[0], uv3[1], uv3[2])) : mk(0, 0, 0);
                 f3 att;
@@ -1126,7 +1130,11 @@ __device__ __forceinline__ void wf_tail_body(const rtw_launch& L, const rtw_wf& 
         }
         if constexpr ((FEAT & ~RTW_F_CHECKER) == 0) {
             float uv3[3] = {0.0f, 0.0f, 0.0f};
+#if defined(RTW_COOP_REJECT_SPHERES)
+            wf_reject3(need_uv, rng, uv3);  // A/B variant: the wave-cooperative form (same draws, same states)
+#else
             if (need_uv) seq_reject<3>(rng, uv3);
+#endif
             if (hitp) {
                 const f3 ruv = need_uv ? unit_vector(mk(uv3[0], uv3[1], uv3[2])) : mk(0, 0, 0);
                 f3 att;
@@ -1316,7 +1324,11 @@ __device__ __forceinline__ void wf_step_body(const rtw_launch& L, const rtw_wf& 
                 }
             }
             float uv3[3] = {0.0f, 0.0f, 0.0f};
+#if defined(RTW_COOP_REJECT_SPHERES)
+            wf_reject3(need_uv, rng, uv3);  // A/B variant: the wave-cooperative form (same draws, same states)
+#else
             if (need_uv) seq_reject<3>(rng, uv3);
+#endif
             if (hitp) {
                 const f3 ruv = need_uv ? unit_vector(mk(uv3[0], uv3[1], uv3[2])) : mk(0, 0, 0);
                 f3 att;
