@@ -306,9 +306,7 @@ enum {  /* rtw_tuning.lds: what the kernels may stage in LDS when it fits */
 enum {  /* rtw_tuning.fuse */
     RTW_FUSE_STEP = 1u,        /* gen + trace + shade of an iteration in one kernel (trees staged in LDS) */
     RTW_FUSE_TAIL_LDS = 2u,    /* the tail kernel walks the LDS stage */
-    RTW_FUSE_GLOBAL = 4u,      /* the fused step also for trees read through L1/L2 */
-    RTW_FUSE_PACK_SPLIT = 8u   /* the split trace / shade kernels keep the packed 48-B path state of static unlit
-                                  sphere scenes too (the fused step always does; default off: C4 -3.8 %) */
+    RTW_FUSE_GLOBAL = 4u       /* the fused step also for trees read through L1/L2 */
 };
 #define RTW_OTREE_NO_CULL 0x100u  /* rtw_tuning.object_tree */
 typedef struct rtw_tuning {

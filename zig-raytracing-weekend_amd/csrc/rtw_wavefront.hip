@@ -294,11 +294,6 @@ __device__ __forceinline__ uint32_t wf_push_bucketed(const rtw_wf& W, uint32_t i
 }
 
 // packed path state (see wf_load_ray_it)
-#if defined(RTW_NO_PACK_SPLIT)
-#define wf_pk(W) false  // A/B variant: the kernels outside the fused step never read the packed state
-#else
-#define wf_pk(W) ((W).packed != 0u)
-#endif
 template <uint32_t FEAT>
 constexpr bool wf_packed() { return (FEAT & (RTW_F_MOVING | RTW_F_LIGHT | RTW_F_GEOM | RTW_F_MEDIUM)) == 0; }
 
@@ -858,7 +853,7 @@ __global__ __launch_bounds__(256) void wf_trace(rtw_launch L, rtw_wf W, uint32_t
                     uint32_t depth;
                     rtw_rng rng;
                     float2 txy;
-                    const Ray r = wf_input_ray<FEAT, CAM>(G, W, S, slot, it, depth, rng, txy, wf_pk(W));
+                    const Ray r = wf_input_ray<FEAT, CAM>(G, W, S, slot, it, depth, rng, txy, false);
                     if (depth) {
                         float t;
                         const int h = traverse<FEAT>(wf_lds_nodes, G, r, t, cnt, CAM ? rng.s : wf_mkey<FEAT>(S, slot));
@@ -888,7 +883,7 @@ __global__ __launch_bounds__(256) void wf_trace(rtw_launch L, rtw_wf W, uint32_t
             uint32_t depth;
             rtw_rng rng;
             float2 txy;
-            const Ray r = wf_input_ray<FEAT, CAM>(L, W, S, slot, it, depth, rng, txy, wf_pk(W));
+            const Ray r = wf_input_ray<FEAT, CAM>(L, W, S, slot, it, depth, rng, txy, false);
             if (depth) {
                 float t = kInf;
                 int h = -1;
@@ -926,7 +921,7 @@ __global__ __launch_bounds__(1024) void wf_trace_clds(rtw_launch L, rtw_wf W, ui
             uint32_t depth;
             rtw_rng rng;
             float2 txy;
-            const Ray r = wf_input_ray<FEAT, CAM>(L, W, S, slot, it, depth, rng, txy, wf_pk(W));
+            const Ray r = wf_input_ray<FEAT, CAM>(L, W, S, slot, it, depth, rng, txy, false);
             if (depth) {
                 float t;
                 const int h = L.counters ? traverse_compact<true, true>(L, wf_clds, r, t, cnt)
@@ -975,7 +970,7 @@ __device__ __forceinline__ void wf_shade_body(const rtw_launch& L, const rtw_wf&
         bool hitp = false, need_uv = false;
         if (e.get(W, slot)) {
             float2 txy;
-            const Ray r = wf_input_ray<FEAT, CAM>(L, W, S, slot, it, depth, rng, txy, wf_pk(W));
+            const Ray r = wf_input_ray<FEAT, CAM>(L, W, S, slot, it, depth, rng, txy, false);
             if (depth) {
                 const float2 h = W.hit[slot];
                 const int hit = __float_as_int(h.y);
@@ -985,7 +980,7 @@ __device__ __forceinline__ void wf_shade_body(const rtw_launch& L, const rtw_wf&
                     acc = mk(0, 0, 0);
                 } else {
                     uint64_t rs;
-                    wf_load_rest<FEAT>(L, S, slot, depth, txy, thr, acc, rs, pid, wf_pk(W));
+                    wf_load_rest<FEAT>(L, S, slot, depth, txy, thr, acc, rs, pid, false);
                     rng.s = rs;
                 }
                 if (hit < 0) {
@@ -1010,11 +1005,7 @@ __device__ __forceinline__ void wf_shade_body(const rtw_launch& L, const rtw_wf&
         }
         if constexpr ((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM)) == 0) {
             float uv3[3] = {0.0f, 0.0f, 0.0f};
-#if defined(RTW_COOP_REJECT_SPHERES)
-            wf_reject3(need_uv, rng, uv3);  // A/B variant: the wave-cooperative form (same draws, same states)
-#else
             if (need_uv) seq_reject<3>(rng, uv3);
-#endif
             if (hitp) {
                 const f3 ruv = need_uv ? unit_vector(mk(uv3[0], uv3[1], uv3[2])) : mk(0, 0, 0);
                 f3 att;
@@ -1028,9 +1019,9 @@ __device__ __forceinline__ void wf_shade_body(const rtw_launch& L, const rtw_wf&
         if (CAM && !depth) W.ls[slot] = rtw_rgb{0.0f, 0.0f, 0.0f};  // padding, rayColor(r, 0) = 0
         const uint32_t out = bucketed ? wf_push_bucketed(W, it, push, push ? wf_bucket(sc.d) & W.sort_mask : 0u, bb, bf)
                                       : wf_push(W, it, push);
-        if (push) wf_store_path<FEAT>(O, out, sc, depth - 1, thr, rng.s, pid, acc, wf_pk(W));
+        if (push) wf_store_path<FEAT>(O, out, sc, depth - 1, thr, rng.s, pid, acc, false);
     }
-    if (bucketed) wf_close_blocks<FEAT>(W, it, bb, bf, wf_pk(W));
+    if (bucketed) wf_close_blocks<FEAT>(W, it, bb, bf, false);
 }
 
 // tail: the paths still queued after the last wavefront iteration, each to
@@ -1060,9 +1051,9 @@ __device__ __forceinline__ void wf_tail_body(const rtw_launch& L, const rtw_wf& 
             exhausted = __ballot(end && !active) == need;
             if (!active && ok) {  // (the tail's input is iteration it >= 1's: wf_iters >= 1)
                 float2 txy;
-                r = wf_load_ray_it<FEAT>(L, S, slot, it, depth, txy, wf_pk(W));
+                r = wf_load_ray_it<FEAT>(L, S, slot, it, depth, txy, W.packed != 0u);
                 uint64_t rs = 0;
-                if (depth) wf_load_rest<FEAT>(L, S, slot, depth, txy, thr, acc, rs, pid, wf_pk(W));
+                if (depth) wf_load_rest<FEAT>(L, S, slot, depth, txy, thr, acc, rs, pid, W.packed != 0u);
                 rng.s = rs;
                 active = depth != 0;
             }
@@ -1130,11 +1121,9 @@ __device__ __forceinline__ void wf_tail_body(const rtw_launch& L, const rtw_wf& 
         }
         if constexpr ((FEAT & ~RTW_F_CHECKER) == 0) {
             float uv3[3] = {0.0f, 0.0f, 0.0f};
-#if defined(RTW_COOP_REJECT_SPHERES)
-            wf_reject3(need_uv, rng, uv3);  // A/B variant: the wave-cooperative form (same draws, same states)
-#else
-            if (need_uv) seq_reject<3>(rng, uv3);
-#endif
+            // the wave-cooperative loop (same candidates, same RNG states as seq_reject<3>): C2 +1.4 %
+            if constexpr (CLDS) wf_reject3(need_uv, rng, uv3);
+            else if (need_uv) seq_reject<3>(rng, uv3);
             if (hitp) {
                 const f3 ruv = need_uv ? unit_vector(mk(uv3[0], uv3[1], uv3[2])) : mk(0, 0, 0);
                 f3 att;
@@ -1324,11 +1313,10 @@ __device__ __forceinline__ void wf_step_body(const rtw_launch& L, const rtw_wf& 
                 }
             }
             float uv3[3] = {0.0f, 0.0f, 0.0f};
-#if defined(RTW_COOP_REJECT_SPHERES)
-            wf_reject3(need_uv, rng, uv3);  // A/B variant: the wave-cooperative form (same draws, same states)
-#else
-            if (need_uv) seq_reject<3>(rng, uv3);
-#endif
+            // the wave-cooperative loop (same candidates, same RNG states as seq_reject<3>): C2 +1.4 %; not with
+            // image / noise textures, whose step is at its 128-VGPR cap (C5 -2.3 %)
+            if constexpr ((FEAT & (RTW_F_IMAGE | RTW_F_NOISE)) == 0) wf_reject3(need_uv, rng, uv3);
+            else if (need_uv) seq_reject<3>(rng, uv3);
             if (hitp) {
                 const f3 ruv = need_uv ? unit_vector(mk(uv3[0], uv3[1], uv3[2])) : mk(0, 0, 0);
                 f3 att;
@@ -1703,8 +1691,9 @@ void wf_run(const rtw_launch& L, const rtw_wf& W0, hipStream_t st, int n_cu, rtw
         }
     }
     rtw_wf W = wf_coherence(W0, g.shade * 4u, W0.sort_iters_split);  // the split kernels' queues
-    // the split path keeps the 60-B state unless asked (C4: the packed state's shade -10 %, its trace +12 %)
-    W.packed = (wf_packed<FEAT>() && (L.wf_fuse & RTW_FUSE_PACK_SPLIT)) ? 1u : 0u;
+    // the split trace / shade kernels keep the 60-B state: their packed form measured C4 -3.8 % (shade -10 %,
+    // and even a runtime-selected packed branch in wf_trace slows its walk 12 %: profiles/r4_packed_state/)
+    W.packed = 0u;
     const uint32_t iters = L.max_depth < W.iters ? L.max_depth : W.iters;
     // iteration 0's trace and shade generate the camera rays themselves (wf_camera); with no
     // iteration (max_depth 0) nothing writes W.ls and the reduce must add zeros
