@@ -1,4 +1,4 @@
-"""The committed bench line (profiles/r3_c2_bench.json, written by bench.py on an
+"""The committed bench line (profiles/r4_c2_bench.json, written by bench.py on an
 MI355X) carries every field of the driver's contract: the headline metric of
 BASELINE.json on config 2, the dominant kernel's roofline and the CPU baseline.
 Its roofline fractions are physical (<= 1) and recomputable from profiles/
@@ -11,8 +11,8 @@ import sys
 import pytest
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-BENCH = "r3_c2_bench.json"
-SUMMARY = "r3_c2_timed_summary.txt"
+BENCH = "r4_c2_bench.json"
+SUMMARY = "r4_c2_timed_summary.txt"
 
 
 def load(name):
@@ -50,18 +50,23 @@ def test_c2_bench_line_contract():
 
 @pytest.mark.parametrize("config", ["c2", "c3", "c4", "c5", "cornell", "cornell_smoke", "simple_light"])
 def test_roofline_recomputes_from_profiles(config):
-    """Every committed round-3 bench line: VALU and HBM fractions <= 1 and recomputable from
-    the PMC passes in profiles/ and the line's HIP-event launch time."""
-    line = os.path.join(REPO, "profiles", f"r3_{config}_bench.json")
+    """Every committed round-4 bench line: VALU and HBM fractions <= 1 and recomputable from
+    the PMC passes in profiles/ (taken on the same build: the line's build_id) and its HIP-event launch time."""
+    line = os.path.join(REPO, "profiles", f"r4_{config}_bench.json")
     rc = subprocess.run([sys.executable, os.path.join(REPO, "tools", "roofline_check.py"), line],
                         capture_output=True, text=True)
     assert rc.returncode == 0, rc.stdout + rc.stderr
-    r = load(f"r3_{config}_bench.json")["roofline"]
+    d = load(f"r4_{config}_bench.json")
+    r = d["roofline"]
     assert r["bound"] == "valu" and 0 < r["frac"] <= 1 and 0 < r["hbm"]["frac"] <= 1
+    assert r["peak"] == 78.643 and "r4_valu_peak" in r["valu"]["peak_source"]
+    for kind in ("valu", "traffic"):
+        with open(os.path.join(REPO, "profiles", f"pmc_{kind}_{config}_sah.json")) as f:
+            assert json.load(f)["_build"]["build_id"] == d["build_id"]
 
 
 def test_rocprof_summary_agrees_with_bench_events():
-    """profiles/r3_c2_timed_summary.txt (rocprofv3 --kernel-trace --stats of the bench
+    """profiles/r4_c2_timed_summary.txt (rocprofv3 --kernel-trace --stats of the bench
     command) and the bench's HIP-event average of the dominant kernel agree."""
     d = load(BENCH)
     kernel = d["roofline"]["kernel"].split("<")[0]
