@@ -1263,9 +1263,9 @@ RTW_DHD bool shade(const float4* __restrict__ nodes, const rtw_launch& L, const 
 // ---------------------------------------------------------------------------
 // Rejection sampling of vec3.randomInUnitSphere (D = 3) / randomInUnitDisk
 // (D = 2) (vec3.zig:40-45, 59-64): the reference's per-lane loop, each lane
-// drawing from its own counter-based stream.  (A wave-cooperative form that
-// evaluated the unresolved lanes' candidates on idle lanes gave the same draws
-// but measured -3 % on C2: removed)
+// drawing from its own counter-based stream.  (The wavefront kernels of sphere
+// scenes share the randomUnitVector loop between the lanes of a wave, wf_reject3:
+// the same draws; the camera's disk loop measured no gain that way)
 // ---------------------------------------------------------------------------
 template <int D>
 RTW_DHD void seq_reject(rtw_rng& rng, float (&out)[D]) {

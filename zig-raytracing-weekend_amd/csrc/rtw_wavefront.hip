@@ -1692,7 +1692,7 @@ void wf_run(const rtw_launch& L, const rtw_wf& W0, hipStream_t st, int n_cu, rtw
     }
     rtw_wf W = wf_coherence(W0, g.shade * 4u, W0.sort_iters_split);  // the split kernels' queues
     // the split trace / shade kernels keep the 60-B state: their packed form measured C4 -3.8 % (shade -10 %,
-    // and even a runtime-selected packed branch in wf_trace slows its walk 12 %: profiles/r4_packed_state/)
+    // but wf_trace 12 % slower with the same walk instructions and node visits: profiles/r4_packed_state/)
     W.packed = 0u;
     const uint32_t iters = L.max_depth < W.iters ? L.max_depth : W.iters;
     // iteration 0's trace and shade generate the camera rays themselves (wf_camera); with no
