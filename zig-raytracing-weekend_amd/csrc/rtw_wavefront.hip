@@ -1797,11 +1797,18 @@ uint32_t wf_pick_feat(uint32_t f) {
 
 }  // namespace
 
+#if !defined(RTW_WF_SPHERES_TU)
+// untextured static sphere scenes (FEAT 0 / CHECKER: BASELINE C2, C3, C4) run from rtw_wavefront_spheres.hip,
+// this code compiled with 64-B loop alignment (csrc/Makefile): C2 +0.8 %, C3 +0.7 %, while the same flag
+// costs the other scene classes' kernels up to 4 % (simple_light's tail), DESIGN.md §4
+void rtw_wf_run_spheres(const rtw_launch& L, const rtw_wf& W, hipStream_t st, int n_cu, rtw_timer* T, uint32_t feat);
+uint32_t rtw_wf_spheres_max_waves(int n_cu);
+
 void rtw_wavefront_batch(const rtw_launch& L, const rtw_wf& W, void* stream, int n_cu, rtw_timer* T) {
     hipStream_t st = (hipStream_t)stream;
     switch (wf_pick_feat(L.feat)) {
-    case 0u: wf_run<0u>(L, W, st, n_cu, T); break;
-    case RTW_F_CHECKER: wf_run<RTW_F_CHECKER>(L, W, st, n_cu, T); break;
+    case 0u: rtw_wf_run_spheres(L, W, st, n_cu, T, 0u); break;
+    case RTW_F_CHECKER: rtw_wf_run_spheres(L, W, st, n_cu, T, RTW_F_CHECKER); break;
     case RTW_F_SPHERES: wf_run<RTW_F_SPHERES>(L, W, st, n_cu, T); break;
     case RTW_F_OBJECTS: wf_run<RTW_F_OBJECTS>(L, W, st, n_cu, T); break;
     case RTW_F_TEXTURED: wf_run<RTW_F_TEXTURED>(L, W, st, n_cu, T); break;
@@ -1811,10 +1818,8 @@ void rtw_wavefront_batch(const rtw_launch& L, const rtw_wf& W, void* stream, int
 }
 
 uint32_t rtw_wavefront_max_waves(int n_cu) {
-    uint32_t m = 0;
+    uint32_t m = rtw_wf_spheres_max_waves(n_cu);
     auto mx = [&m](uint32_t a, uint32_t b) { m = std::max({m, a, b}); };
-    mx(wf_grids<0u>(n_cu).shade, wf_grids<0u>(n_cu).shade0);
-    mx(wf_grids<RTW_F_CHECKER>(n_cu).shade, wf_grids<RTW_F_CHECKER>(n_cu).shade0);
     mx(wf_grids<RTW_F_SPHERES>(n_cu).shade, wf_grids<RTW_F_SPHERES>(n_cu).shade0);
     mx(wf_grids<RTW_F_OBJECTS>(n_cu).shade, wf_grids<RTW_F_OBJECTS>(n_cu).shade0);
     mx(wf_grids<RTW_F_TEXTURED>(n_cu).shade, wf_grids<RTW_F_TEXTURED>(n_cu).shade0);
@@ -1822,8 +1827,18 @@ uint32_t rtw_wavefront_max_waves(int n_cu) {
     mx(wf_grids<RTW_F_ALL>(n_cu).shade, wf_grids<RTW_F_ALL>(n_cu).shade0);
     return 4 * m;
 }
+#else
+void rtw_wf_run_spheres(const rtw_launch& L, const rtw_wf& W, hipStream_t st, int n_cu, rtw_timer* T, uint32_t feat) {
+    if (feat) wf_run<RTW_F_CHECKER>(L, W, st, n_cu, T);
+    else wf_run<0u>(L, W, st, n_cu, T);
+}
 
-#if defined(RTW_DIAG_WALK)
+uint32_t rtw_wf_spheres_max_waves(int n_cu) {
+    return std::max({wf_grids<0u>(n_cu).shade, wf_grids<0u>(n_cu).shade0, wf_grids<RTW_F_CHECKER>(n_cu).shade,
+                     wf_grids<RTW_F_CHECKER>(n_cu).shade0});
+}
+
+#if defined(RTW_DIAG_WALK)  // (the sphere-scene kernels' records and counters: this translation unit's)
 // diagnostic build only: where the per-slot walk records of iteration `it` go (null: off)
 extern "C" int rtw_debug_walk_records(void* d_rec, uint32_t cap_slots, uint32_t it) {
     uint4* p = static_cast<uint4*>(d_rec);
@@ -1842,3 +1857,4 @@ extern "C" int rtw_debug_walk_counters(uint64_t* out, int reset) {
     return RTW_OK;
 }
 #endif
+#endif  // RTW_WF_SPHERES_TU
