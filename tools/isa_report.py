@@ -6,7 +6,7 @@ compiler reports them (.num_vgpr, ScratchSize, Occupancy), the instruction histo
 every loop (a backward branch to an earlier label) with its static instruction counts -- the walk
 loop is the one that loads BVH nodes (ds_read_b128 from the LDS stage, or global_load_dwordx4).
 
-Usage: python tools/isa_report.py build/isa/rtw_wavefront.s wf_step_cldsILj0E wf_traceILj0ELb0E wf_tail_cldsILj0E
+Usage: python tools/isa_report.py build/isa/rtw_wavefront_all.s wf_step_cldsILj0E wf_traceILj0ELb0E wf_tail_cldsILj0E
        [--json out.json]
 """
 from __future__ import annotations

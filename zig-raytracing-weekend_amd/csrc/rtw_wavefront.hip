@@ -1799,8 +1799,8 @@ uint32_t wf_pick_feat(uint32_t f) {
 
 #if !defined(RTW_WF_SPHERES_TU)
 // untextured static sphere scenes (FEAT 0 / CHECKER: BASELINE C2, C3, C4) run from rtw_wavefront_spheres.hip,
-// this code compiled with 64-B loop alignment (csrc/Makefile): C2 +0.8 %, C3 +0.7 %, while the same flag
-// costs the other scene classes' kernels up to 4 % (simple_light's tail), DESIGN.md §4
+// this code compiled with 64-B loop alignment (csrc/Makefile): C2 +0.8 %, C3 +0.7 %; the other scene classes
+// gained nothing from the flag (C5 -0.3 %, Cornell -0.4 %), so they keep the default placement
 void rtw_wf_run_spheres(const rtw_launch& L, const rtw_wf& W, hipStream_t st, int n_cu, rtw_timer* T, uint32_t feat);
 uint32_t rtw_wf_spheres_max_waves(int n_cu);
 
