@@ -629,7 +629,6 @@ int run_wavefront(rtw_ctx* ctx, rtw_launch L, hipStream_t stream, rtw_timer* T) 
         S.thr = reinterpret_cast<float4*>(take(Q * 16));
         S.acc = reinterpret_cast<float4*>(take(Q * 16));
         S.rng = reinterpret_cast<uint64_t*>(take(Q * 8));
-        S.pid = reinterpret_cast<uint32_t*>(take(Q * 4));
     }
     W.hit = reinterpret_cast<float2*>(take(Q * 8));
     W.ls = reinterpret_cast<rtw_rgb*>(take(P * sizeof(rtw_rgb)));

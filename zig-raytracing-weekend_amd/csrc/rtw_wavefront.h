@@ -37,10 +37,10 @@
 struct rtw_wf_set {
     float4* ray_o;      // o.xyz, time
     float4* ray_d;      // d.xyz, bits(remaining depth); depth 0 = no path
-    float4* thr;        // throughput.xyz (implicit 1 on the first bounce)
+    float4* thr;        // throughput.xyz, bits(path id) (implicit 1 and slot on the first bounce; packed state:
+                        // thr.z, path id, RNG state -- rtw_wavefront.hip wf_packed)
     float4* acc;        // radiance so far (scenes with emitters only)
     uint64_t* rng;      // RNG state
-    uint32_t* pid;      // path id (implicit = slot in iteration 0)
 };
 
 // a finished sample's radiance (12 B: the reduce reads 5.8 GB instead of 7.7 GB for C2's 480 M samples)
@@ -68,7 +68,7 @@ struct rtw_wf {
 };
 
 // bytes of device state per path (two slot sets + hit + ls)
-#define RTW_WF_PATH_BYTES (2 * (4 * 16 + 8 + 4) + 8 + 12)
+#define RTW_WF_PATH_BYTES (2 * (4 * 16 + 8) + 8 + 12)
 
 void rtw_wavefront_batch(const rtw_launch& L, const rtw_wf& W, void* stream, int n_cu, rtw_timer* T);
 // waves of the largest wavefront grid (bounds the stripe capacity)

@@ -336,23 +336,6 @@ __device__ __forceinline__ uint64_t wf_mkey(const rtw_wf_set& S, uint32_t slot) 
     return 0;
 }
 
-// throughput and radiance: implicit (1, 0) on the first bounce; the radiance is
-// only non-zero before the path ends in scenes with emitters
-template <uint32_t FEAT>
-__device__ __forceinline__ void wf_load_state(const rtw_launch& L, const rtw_wf_set& S, uint32_t slot, uint32_t depth,
-                                              f3& thr, f3& acc) {
-    thr = mk(1, 1, 1);
-    acc = mk(0, 0, 0);
-    if (depth != L.max_depth) {
-        const float4 t4 = S.thr[slot];
-        thr = mk(t4.x, t4.y, t4.z);
-        if constexpr ((FEAT & RTW_F_LIGHT) != 0) {
-            const float4 l4 = S.acc[slot];
-            acc = mk(l4.x, l4.y, l4.z);
-        }
-    }
-}
-
 // Packed path state (round 4) of static sphere scenes without emitters (BASELINE configs 2-5): no ray time
 // is ever read (no moving sphere), no radiance is carried (no emitter), and the remaining depth of every
 // path in iteration it's input set is max_depth - it, so a path is three 16-B streams instead of five
@@ -360,7 +343,8 @@ __device__ __forceinline__ void wf_load_state(const rtw_launch& L, const rtw_wf_
 // slot (a closed block's tail) has d = 0: no queued ray has a zero direction (Lambertian replaces a
 // near-zero one by the normal, material.zig:47-50; Metal absorbs dot(d, n) <= 0, :68; Dielectric's is a
 // unit-length reflection or refraction, :80-98).  The same values in the same registers: bit-identical.
-// The split shade of C4 moves 104 instead of 128 B per surviving ray (-19 %).
+// The 60-B form (every other scene class, and the split trace / shade kernels): ray_o = (o, time), ray_d =
+// (d, remaining depth), thr = (thr.xyz, pid), rng, and acc (radiance so far) in scenes with emitters.
 // the ray of slot `slot` of iteration it's input set; depth 0 = no path.  txy: packed only, thr.xy
 template <uint32_t FEAT>
 __device__ __forceinline__ Ray wf_load_ray_it(const rtw_launch& L, const rtw_wf_set& S, uint32_t slot, uint32_t it,
@@ -393,9 +377,17 @@ __device__ __forceinline__ void wf_load_rest(const rtw_launch& L, const rtw_wf_s
         pid = fbits(c.y);
         rng = (uint64_t)fbits(c.z) | ((uint64_t)fbits(c.w) << 32);
     } else {
-        pid = S.pid[slot];
+        const float4 t4 = S.thr[slot];
+        thr = mk(t4.x, t4.y, t4.z);
+        pid = fbits(t4.w);
         rng = S.rng[slot];
-        wf_load_state<FEAT>(L, S, slot, depth, thr, acc);
+        acc = mk(0, 0, 0);
+        if constexpr ((FEAT & RTW_F_LIGHT) != 0) {
+            const float4 l4 = S.acc[slot];
+            acc = mk(l4.x, l4.y, l4.z);
+        }
+        (void)L;
+        (void)depth;
     }
 }
 
@@ -412,9 +404,8 @@ __device__ __forceinline__ void wf_store_path(const rtw_wf_set& O, uint32_t out,
         (void)acc;
     } else {
         wf_store_ray(O, out, r, depth);
-        O.thr[out] = make_float4(thr.x, thr.y, thr.z, 0);
+        O.thr[out] = make_float4(thr.x, thr.y, thr.z, __uint_as_float(pid));
         O.rng[out] = rng;
-        O.pid[out] = pid;
         if constexpr ((FEAT & RTW_F_LIGHT) != 0) O.acc[out] = make_float4(acc.x, acc.y, acc.z, 0);
     }
 }
