@@ -296,6 +296,17 @@ __device__ __forceinline__ uint32_t wf_push_bucketed(const rtw_wf& W, uint32_t i
 // packed path state (see wf_load_ray_it)
 template <uint32_t FEAT>
 constexpr bool wf_packed() { return (FEAT & (RTW_F_MOVING | RTW_F_LIGHT | RTW_F_GEOM | RTW_F_MEDIUM)) == 0; }
+// the 60-B layout of scenes without ray time or medium keys (object scenes): the RNG state rides in the ray
+// records' spare words (time, remaining depth), so no rng stream; liveness and depth as in the packed state
+template <uint32_t FEAT>
+constexpr bool wf_rng_in_ray() { return (FEAT & (RTW_F_MOVING | RTW_F_MEDIUM)) == 0; }
+// max_depth - it as a per-lane value: left uniform, the compiler's handling of the split trace (C4) made its
+// walk 12-15 % slower with the same walk instructions (profiles/r4_c4_trace_probe/)
+__device__ __forceinline__ uint32_t wf_iter_depth(const rtw_launch& L, uint32_t it) {
+    uint32_t md = L.max_depth - it;
+    asm volatile("" : "+v"(md));
+    return md;
+}
 
 // the unused slots of the wave's partly filled blocks: dead (depth 0; packed state: d = 0), so the next
 // iteration skips them
@@ -343,8 +354,9 @@ __device__ __forceinline__ uint64_t wf_mkey(const rtw_wf_set& S, uint32_t slot) 
 // slot (a closed block's tail) has d = 0: no queued ray has a zero direction (Lambertian replaces a
 // near-zero one by the normal, material.zig:47-50; Metal absorbs dot(d, n) <= 0, :68; Dielectric's is a
 // unit-length reflection or refraction, :80-98).  The same values in the same registers: bit-identical.
-// The 60-B form (every other scene class, and the split trace / shade kernels): ray_o = (o, time), ray_d =
-// (d, remaining depth), thr = (thr.xyz, pid), rng, and acc (radiance so far) in scenes with emitters.
+// The 60-B form (every other scene class): ray_o = (o, time), ray_d = (d, remaining depth), thr = (thr.xyz,
+// pid), rng, and acc (radiance so far) in scenes with emitters; without ray time or media (wf_rng_in_ray)
+// the RNG state's halves replace time and depth and the rng stream is unused.
 // the ray of slot `slot` of iteration it's input set; depth 0 = no path.  txy: packed only, thr.xy
 template <uint32_t FEAT>
 __device__ __forceinline__ Ray wf_load_ray_it(const rtw_launch& L, const rtw_wf_set& S, uint32_t slot, uint32_t it,
@@ -356,8 +368,17 @@ __device__ __forceinline__ Ray wf_load_ray_it(const rtw_launch& L, const rtw_wf_
         r.o = mk(o.x, o.y, o.z);
         r.d = mk(o.w, d.x, d.y);
         r.time = 0.0f;
-        depth = ((fbits(o.w) | fbits(d.x) | fbits(d.y)) << 1) ? L.max_depth - it : 0u;  // +-0 components: d = 0
+        depth = ((fbits(o.w) | fbits(d.x) | fbits(d.y)) << 1) ? wf_iter_depth(L, it) : 0u;  // +-0 components: d = 0
         txy = make_float2(d.z, d.w);
+        return r;
+    } else if constexpr (wf_rng_in_ray<FEAT>()) {
+        const float4 o = S.ray_o[slot], d = S.ray_d[slot];
+        Ray r;
+        r.o = mk(o.x, o.y, o.z);
+        r.d = mk(d.x, d.y, d.z);
+        r.time = 0.0f;
+        depth = ((fbits(d.x) | fbits(d.y) | fbits(d.z)) << 1) ? wf_iter_depth(L, it) : 0u;
+        txy = make_float2(o.w, d.w);  // the RNG state's halves
         return r;
     } else {
         txy = make_float2(0.0f, 0.0f);
@@ -380,7 +401,8 @@ __device__ __forceinline__ void wf_load_rest(const rtw_launch& L, const rtw_wf_s
         const float4 t4 = S.thr[slot];
         thr = mk(t4.x, t4.y, t4.z);
         pid = fbits(t4.w);
-        rng = S.rng[slot];
+        if constexpr (wf_rng_in_ray<FEAT>()) rng = (uint64_t)fbits(txy.x) | ((uint64_t)fbits(txy.y) << 32);
+        else rng = S.rng[slot];
         acc = mk(0, 0, 0);
         if constexpr ((FEAT & RTW_F_LIGHT) != 0) {
             const float4 l4 = S.acc[slot];
@@ -403,9 +425,15 @@ __device__ __forceinline__ void wf_store_path(const rtw_wf_set& O, uint32_t out,
         (void)depth;
         (void)acc;
     } else {
-        wf_store_ray(O, out, r, depth);
+        if constexpr (wf_rng_in_ray<FEAT>()) {
+            O.ray_o[out] = make_float4(r.o.x, r.o.y, r.o.z, __uint_as_float((uint32_t)rng));
+            O.ray_d[out] = make_float4(r.d.x, r.d.y, r.d.z, __uint_as_float((uint32_t)(rng >> 32)));
+            (void)depth;
+        } else {
+            wf_store_ray(O, out, r, depth);
+            O.rng[out] = rng;
+        }
         O.thr[out] = make_float4(thr.x, thr.y, thr.z, __uint_as_float(pid));
-        O.rng[out] = rng;
         if constexpr ((FEAT & RTW_F_LIGHT) != 0) O.acc[out] = make_float4(acc.x, acc.y, acc.z, 0);
     }
 }
@@ -844,7 +872,7 @@ __global__ __launch_bounds__(256) void wf_trace(rtw_launch L, rtw_wf W, uint32_t
                     uint32_t depth;
                     rtw_rng rng;
                     float2 txy;
-                    const Ray r = wf_input_ray<FEAT, CAM>(G, W, S, slot, it, depth, rng, txy, false);
+                    const Ray r = wf_input_ray<FEAT, CAM>(G, W, S, slot, it, depth, rng, txy, true);
                     if (depth) {
                         float t;
                         const int h = traverse<FEAT>(wf_lds_nodes, G, r, t, cnt, CAM ? rng.s : wf_mkey<FEAT>(S, slot));
@@ -874,7 +902,7 @@ __global__ __launch_bounds__(256) void wf_trace(rtw_launch L, rtw_wf W, uint32_t
             uint32_t depth;
             rtw_rng rng;
             float2 txy;
-            const Ray r = wf_input_ray<FEAT, CAM>(L, W, S, slot, it, depth, rng, txy, false);
+            const Ray r = wf_input_ray<FEAT, CAM>(L, W, S, slot, it, depth, rng, txy, true);
             if (depth) {
                 float t = kInf;
                 int h = -1;
@@ -912,7 +940,7 @@ __global__ __launch_bounds__(1024) void wf_trace_clds(rtw_launch L, rtw_wf W, ui
             uint32_t depth;
             rtw_rng rng;
             float2 txy;
-            const Ray r = wf_input_ray<FEAT, CAM>(L, W, S, slot, it, depth, rng, txy, false);
+            const Ray r = wf_input_ray<FEAT, CAM>(L, W, S, slot, it, depth, rng, txy, true);
             if (depth) {
                 float t;
                 const int h = L.counters ? traverse_compact<true, true>(L, wf_clds, r, t, cnt)
@@ -961,7 +989,7 @@ __device__ __forceinline__ void wf_shade_body(const rtw_launch& L, const rtw_wf&
         bool hitp = false, need_uv = false;
         if (e.get(W, slot)) {
             float2 txy;
-            const Ray r = wf_input_ray<FEAT, CAM>(L, W, S, slot, it, depth, rng, txy, false);
+            const Ray r = wf_input_ray<FEAT, CAM>(L, W, S, slot, it, depth, rng, txy, true);
             if (depth) {
                 const float2 h = W.hit[slot];
                 const int hit = __float_as_int(h.y);
@@ -971,7 +999,7 @@ __device__ __forceinline__ void wf_shade_body(const rtw_launch& L, const rtw_wf&
                     acc = mk(0, 0, 0);
                 } else {
                     uint64_t rs;
-                    wf_load_rest<FEAT>(L, S, slot, depth, txy, thr, acc, rs, pid, false);
+                    wf_load_rest<FEAT>(L, S, slot, depth, txy, thr, acc, rs, pid, true);
                     rng.s = rs;
                 }
                 if (hit < 0) {
@@ -1010,9 +1038,9 @@ __device__ __forceinline__ void wf_shade_body(const rtw_launch& L, const rtw_wf&
         if (CAM && !depth) W.ls[slot] = rtw_rgb{0.0f, 0.0f, 0.0f};  // padding, rayColor(r, 0) = 0
         const uint32_t out = bucketed ? wf_push_bucketed(W, it, push, push ? wf_bucket(sc.d) & W.sort_mask : 0u, bb, bf)
                                       : wf_push(W, it, push);
-        if (push) wf_store_path<FEAT>(O, out, sc, depth - 1, thr, rng.s, pid, acc, false);
+        if (push) wf_store_path<FEAT>(O, out, sc, depth - 1, thr, rng.s, pid, acc, true);
     }
-    if (bucketed) wf_close_blocks<FEAT>(W, it, bb, bf, false);
+    if (bucketed) wf_close_blocks<FEAT>(W, it, bb, bf, true);
 }
 
 // tail: the paths still queued after the last wavefront iteration, each to
@@ -1682,9 +1710,7 @@ void wf_run(const rtw_launch& L, const rtw_wf& W0, hipStream_t st, int n_cu, rtw
         }
     }
     rtw_wf W = wf_coherence(W0, g.shade * 4u, W0.sort_iters_split);  // the split kernels' queues
-    // the split trace / shade kernels keep the 60-B state: their packed form measured C4 -3.8 % (shade -10 %,
-    // but wf_trace 12 % slower with the same walk instructions and node visits: profiles/r4_packed_state/)
-    W.packed = 0u;
+    W.packed = wf_packed<FEAT>() ? 1u : 0u;  // the split kernels (and their tail) use the packed state too
     const uint32_t iters = L.max_depth < W.iters ? L.max_depth : W.iters;
     // iteration 0's trace and shade generate the camera rays themselves (wf_camera); with no
     // iteration (max_depth 0) nothing writes W.ls and the reduce must add zeros
