@@ -3,7 +3,7 @@
 For N in (1, 2, 4, 8) renders every rank's shard (rtw_render_rows_device, the
 call bench.py makes per rank) back to back on this GPU and reports the slowest
 rank's render time: the N-GPU step time minus the RCCL gather (C2: 15.4 MB,
-~1-2 ms over xGMI).  Usage: python tools/shard_sim.py [config] [spp] [rows_per_block] [ranks, e.g. 1,8]
+~1-2 ms over xGMI).  Usage: [RTW_SHARD_TUNING=json] python tools/shard_sim.py [config] [spp] [rows_per_block] [ranks, e.g. 1,8]
 """
 import importlib
 import json
@@ -20,7 +20,8 @@ spp_override = int(sys.argv[2]) if len(sys.argv) > 2 else 0
 rpb = int(sys.argv[3]) if len(sys.argv) > 3 else 16
 ns = [int(v) for v in sys.argv[4].split(",")] if len(sys.argv) > 4 else [1, 2, 4, 8]
 cfg = pkg.configs.CONFIGS[cfg_name]
-world = pkg.World(pkg.flatten(cfg.objects()))
+# RTW_SHARD_TUNING='{"wf_iters": 16}': the rtw_tuning fields to override (every setting renders the same image)
+world = pkg.World(pkg.flatten(cfg.objects()), tuning=json.loads(os.environ.get("RTW_SHARD_TUNING", "{}")))
 cam = cfg.camera()
 if spp_override:
     cam.samples_per_pixel = spp_override
