@@ -61,6 +61,11 @@ def parse():
                          "GPU, for the CPU tests; never a headline number")
     ap.add_argument("--host-threads", type=int, default=2, help="--host-backend: render threads per rank")
     ap.add_argument("--dump-image", default="", help="rank 0 saves the reassembled float4 frame (.npy)")
+    ap.add_argument("--shard", default="",
+                    help="N,R: render only rank R's shard of an N-way split on this one GPU, no gather (the PMC "
+                         "passes of one rank at N, tools/pmc_shard.sh; never a headline number)")
+    ap.add_argument("--profiles-dir", default=os.path.join(REPO, "profiles"),
+                    help="where the committed PMC passes are read from (tests point it elsewhere)")
     return ap.parse_args()
 
 
@@ -80,6 +85,14 @@ def main():
         raise SystemExit("--gpus N > 1: launch one process per GPU with torchrun (the driver's scaling run), or "
                          "pass --single-process for the one-process rtw_multi path")
     n_shards = args.gpus if single else world_size
+    shard_rank = rank
+    emulated = bool(args.shard)
+    if emulated:  # one rank's shard of an N-way split, rendered alone on this GPU
+        if world_size > 1 or single or args.gpus > 1 or args.dump_image:
+            raise SystemExit("--shard N,R runs one process on one GPU (no torchrun, --single-process or --dump-image)")
+        n_shards, shard_rank = (int(v) for v in args.shard.split(","))
+        if not (n_shards >= 1 and 0 <= shard_rank < n_shards):
+            raise SystemExit("--shard N,R needs 0 <= R < N")
     host = args.host_backend
     if host and single:
         raise SystemExit("--host-backend is the torchrun (one process per rank) flow")
@@ -134,10 +147,10 @@ def main():
     if not host:
         torch.cuda.set_stream(stream)
     # the shard this process renders (single-process mode: device 0's, for the counted and timing passes)
-    shard = pkg.distributed.ShardedRender(world, cam, rank, n_shards, ROWS_PER_BLOCK,
+    shard = pkg.distributed.ShardedRender(world, cam, shard_rank, n_shards, ROWS_PER_BLOCK,
                                           device=torch.device("cpu") if host else None)
     my_rows = shard.rows
-    assert my_rows == L.rtw_shard_rows(H, ROWS_PER_BLOCK, n_shards, rank)
+    assert my_rows == L.rtw_shard_rows(H, ROWS_PER_BLOCK, n_shards, shard_rank)
     frame = torch.zeros((W * H, 4), dtype=torch.float32, device="cuda") if single else None
 
     def render_step(counters=None, w=None, timing=None):
@@ -148,7 +161,7 @@ def main():
             shard.world = saved
 
     def gather_step():
-        if not single:
+        if not single and not emulated:
             shard.gather()
 
     def frame_step():
@@ -227,7 +240,7 @@ def main():
         multi.close()
         for w in worlds[1:]:
             w.close()
-    total_samples = W * H * spp * args.steps
+    total_samples = (my_rows if emulated else H) * W * spp * args.steps
     value = total_samples / elapsed / 1e6
     render_s = sum(kernel_ms) / len(kernel_ms) / 1e3          # whole render call (all kernels) per step
     kms = {n: sum(t.ms[i] for t in timings) for i, n in enumerate(pkg._abi.RTW_K_NAMES)}
@@ -246,9 +259,13 @@ def main():
     # fused path (compact LDS stage): one gen+trace+shade kernel per iteration, timed as "trace"
     fused = kcalls["trace"] > 0 and kcalls["shade"] == 0
     knames = {"trace": "wf_step_clds" if fused else "wf_trace", "tail": "wf_tail", "mega": "render_persistent_v1"}
-    traffic, traffic_src = (None, None) if host else pmc_traffic(
+    # (the PMC passes are per shard: at N > 1 only a pass of this rank's shard at this N -- bench.py --shard N,R
+    # on one GPU, tools/pmc_shard.sh -- prices this rank's launches; anything else leaves the fractions null)
+    # (host backend: the lookup runs -- the CPU tests check it -- but there are no device launch times, so
+    # every fraction below stays null)
+    traffic, traffic_src = pmc_traffic(
         args, {"trace": "wf_step" if fused else "wf_trace", "tail": "wf_tail", "mega": "render_"}.get(dom, dom),
-        build_id)
+        build_id, n_shards, shard_rank, single)
 
     # ---- roofline of the dominant kernel: VALU issue.  The kernel is VALU-bound
     # (C2: VALU busy 0.85 of the quad-cycles, HBM 0.18 of peak), so `frac` = useful lane-instructions
@@ -257,7 +274,9 @@ def main():
     # the launch time is this run's HIP events.  HBM traffic (PMC) and the SURVEY §8d algorithmic
     # bytes are reported beside it; the latter is a diagnostic, not a fraction of any peak.
     dom_kind = {"trace": "wf_step" if fused else "wf_trace", "tail": "wf_tail", "mega": "render_"}.get(dom, dom)
-    valu, valu_src = (None, None) if host else pmc_valu(args, dom_kind, build_id, single)
+    valu, valu_src = pmc_valu(args, dom_kind, build_id, n_shards, shard_rank, single)
+    if host:
+        dom_launch_s = 0.0
     lane_ops = valu.get("lane_ops") if valu else None
     achieved_valu = lane_ops / dom_launch_s / 1e12 if (lane_ops and dom_launch_s > 0) else None
     # fraction of the SIMD cycles spent issuing VALU at the measured 2-clock wave64 rate
@@ -305,6 +324,11 @@ def main():
         "nodes_per_ray_device": round((cdev["nodes"] + cdev["leaves"]) / max(1, cdev["rays"]), 3),
         "bvh": args.bvh,
     }
+    # a fraction above 1 is not evidence (a pass of another shard or launch shape): never published
+    for sec in (roofline, roofline["hbm"]):
+        if sec["frac"] is not None and sec["frac"] > 1.0:
+            sec["guard"] = f"frac {sec['frac']} > 1 from {sec.get('source') or roofline['valu']['source']}: nulled"
+            sec["frac"] = sec["achieved"] = None
 
     cpu = None
     if rank == 0 and world_size == 1 and not args.no_cpu_baseline:
@@ -331,6 +355,8 @@ def main():
                        + ((" + gloo gather (host backend)" if host else " + RCCL gather") if distributed else "")
                        + (" (one process, rtw_multi: grouped RCCL send/recv)" if single else ""),
                        "rows_per_block": ROWS_PER_BLOCK, "exchange": rccl,
+                       "shard": {"n_shards": n_shards, "rank": shard_rank, "rows": my_rows,
+                                 "emulated": emulated},
                        "timed_scope": ("host contexts (rtw_render_rows) into host tiles, gathered over gloo: the "
                                        "CPU rehearsal of the torchrun flow" if host else
                                        "device API (rtw_render_rows_device / rtw_render_multi_device) into an "
@@ -353,38 +379,53 @@ def pmc_build_id(data):
     return b.get("build_id") if isinstance(b, dict) else None
 
 
-def pmc_traffic(args, kernel_prefix, build_id):
-    """HBM bytes per launch of the dominant kernel from the committed PMC pass
-    (tools/pmc_traffic.sh -> profiles/pmc_traffic_<config>_<bvh>.json; FETCH_SIZE x2 + WRITE_SIZE,
-    MI355X_MICROARCH.md § HBM).  PMC counters cannot be read inside the timed run.  A pass taken on
-    another build of the library (its _build.build_id differs from rtw_build_id()) is not used."""
-    f = os.path.join(REPO, "profiles", f"pmc_traffic_{args.config}_{args.bvh}.json")
-    if args.spp or args.tuning or os.environ.get("RTW_LIB") or not os.path.exists(f):
+def pmc_pass(args, kind, build_id, n_shards=1, rank=0, single=False):
+    """The committed PMC pass of `kind` ("valu" | "traffic") that prices THIS process's launches, or
+    (None, reason).  A pass counts one launch of the shard it was taken on: N = 1 the whole frame
+    (profiles/pmc_<kind>_<config>_<bvh>.json), N > 1 rank R's rows of an N-way split, rendered alone on
+    one GPU (bench.py --shard N,R: profiles/pmc_<kind>_<config>_<bvh>_n<N>_r<R>.json, stamped with
+    n_shards / rank).  Never another shard's pass: at N = 8 the whole-frame counts over a rank's ~1/6.5-length
+    launch would read as a fraction > 1.  Nor a pass of another library build, an A/B run (--spp, --tuning,
+    RTW_LIB) or the single-process multi path (other kernels)."""
+    if args.spp or args.tuning or single or os.environ.get("RTW_LIB"):
         return None, None
+    suffix = f"_n{n_shards}_r{rank}" if n_shards > 1 else ""
+    f = os.path.join(args.profiles_dir, f"pmc_{kind}_{args.config}_{args.bvh}{suffix}.json")
+    rel = os.path.relpath(f, REPO)
+    if not os.path.exists(f):
+        return None, (f"{rel}: no pass of this rank's shard at N = {n_shards} (fractions null)" if n_shards > 1
+                      else None)
     data = json.load(open(f))
     if pmc_build_id(data) != build_id:
-        return None, f"{os.path.relpath(f, REPO)}: build {pmc_build_id(data)} != loaded {build_id} (stale, unused)"
+        return None, f"{rel}: build {pmc_build_id(data)} != loaded {build_id} (stale, unused)"
+    b = data.get("_build") or {}
+    if (int(b.get("n_shards") or 1), int(b.get("rank") or 0)) != (n_shards, rank):
+        return None, f"{rel}: pass of shard {b.get('rank')}/{b.get('n_shards')}, not {rank}/{n_shards} (unused)"
+    return data, rel
+
+
+def pmc_traffic(args, kernel_prefix, build_id, n_shards=1, rank=0, single=False):
+    """HBM bytes per launch of the dominant kernel from the committed PMC pass
+    (tools/pmc_traffic.sh -> profiles/pmc_traffic_<config>_<bvh>[_n<N>_r<R>].json; FETCH_SIZE x2 + WRITE_SIZE,
+    MI355X_MICROARCH.md § HBM).  PMC counters cannot be read inside the timed run (pmc_pass)."""
+    data, src = pmc_pass(args, "traffic", build_id, n_shards, rank, single)
+    if data is None:
+        return None, src
     for name, e in data.items():
         if name.startswith(kernel_prefix) and isinstance(e, dict):
-            return round(e["traffic_bytes"]), os.path.relpath(f, REPO)
+            return round(e["traffic_bytes"]), src
     return None, None
 
 
-def pmc_valu(args, kind, build_id, single=False):
+def pmc_valu(args, kind, build_id, n_shards=1, rank=0, single=False):
     """VALU counters per launch of the dominant kernel kind from the committed SQ pass
-    (tools/pmc_valu.sh -> profiles/pmc_valu_<config>_<bvh>.json).  Returns (entry, path).
-    The pass was taken with the product defaults on one device: an A/B build (--tuning, RTW_LIB) or the
-    single-process multi path runs other kernels, so no roofline is derived from it there; nor from a
-    pass of another build of the library (roofline.frac is then null)."""
-    f = os.path.join(REPO, "profiles", f"pmc_valu_{args.config}_{args.bvh}.json")
-    if args.spp or args.tuning or single or os.environ.get("RTW_LIB") or not os.path.exists(f):
-        return None, None
-    data = json.load(open(f))
-    if pmc_build_id(data) != build_id:
-        return None, f"{os.path.relpath(f, REPO)}: build {pmc_build_id(data)} != loaded {build_id} (stale, unused)"
+    (tools/pmc_valu.sh -> profiles/pmc_valu_<config>_<bvh>[_n<N>_r<R>].json).  Returns (entry, path)."""
+    data, src = pmc_pass(args, "valu", build_id, n_shards, rank, single)
+    if data is None:
+        return None, src
     for name, e in data.items():
         if name.startswith(kind) and isinstance(e, dict) and e.get("lane_ops"):
-            return e, os.path.relpath(f, REPO)
+            return e, src
     return None, None
 
 

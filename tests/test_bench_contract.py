@@ -11,8 +11,9 @@ import sys
 import pytest
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-BENCH = "r4_c2_bench.json"
-SUMMARY = "r4_c2_timed_summary.txt"
+ROUND = "r4"
+BENCH = f"{ROUND}_c2_bench.json"
+SUMMARY = f"{ROUND}_c2_timed_summary.txt"
 
 
 def load(name):
@@ -52,11 +53,11 @@ def test_c2_bench_line_contract():
 def test_roofline_recomputes_from_profiles(config):
     """Every committed round-4 bench line: VALU and HBM fractions <= 1 and recomputable from
     the PMC passes in profiles/ (taken on the same build: the line's build_id) and its HIP-event launch time."""
-    line = os.path.join(REPO, "profiles", f"r4_{config}_bench.json")
+    line = os.path.join(REPO, "profiles", f"{ROUND}_{config}_bench.json")
     rc = subprocess.run([sys.executable, os.path.join(REPO, "tools", "roofline_check.py"), line],
                         capture_output=True, text=True)
     assert rc.returncode == 0, rc.stdout + rc.stderr
-    d = load(f"r4_{config}_bench.json")
+    d = load(f"{ROUND}_{config}_bench.json")
     r = d["roofline"]
     assert r["bound"] == "valu" and 0 < r["frac"] <= 1 and 0 < r["hbm"]["frac"] <= 1
     assert r["peak"] == 78.643 and "r4_valu_peak" in r["valu"]["peak_source"]
@@ -82,16 +83,18 @@ PMC_CONFIGS = ["c2", "c3", "c4", "c5", "cornell", "cornell_smoke", "simple_light
 
 
 @pytest.mark.parametrize("config", PMC_CONFIGS)
-def test_pmc_passes_are_from_this_build(rtw, config):
+def test_pmc_passes_pair_with_the_bench_lines(config):
     """Every committed PMC pass bench.py derives a roofline from (profiles/pmc_{valu,traffic}_<config>_sah.json)
-    was taken on the library these sources build: its _build.build_id is rtw_build_id() (test_abi.py checks
-    that the loaded library IS these sources).  bench.py uses no pass of another build (roofline.frac null)."""
-    want = rtw.lib().rtw_build_id().decode()
+    was taken on the build of the committed bench line it prices (its _build.build_id), for that config and for
+    the whole frame (n_shards 1).  (Whether a pass matches the library being run is bench.py's own check: it
+    leaves the fractions null for a pass of another build, test_bench_refuses_a_stale_pmc_pass.)"""
+    line = load(f"{ROUND}_{config}_bench.json")
     for kind in ("valu", "traffic"):
         with open(os.path.join(REPO, "profiles", f"pmc_{kind}_{config}_sah.json")) as f:
             d = json.load(f)
-        assert d.get("_build", {}).get("build_id") == want, (kind, config, d.get("_build"), want)
+        assert d.get("_build", {}).get("build_id") == line["build_id"], (kind, config, d.get("_build"))
         assert d["_build"].get("config") == config
+        assert int(d["_build"].get("n_shards") or 1) == 1
 
 
 def test_bench_refuses_a_stale_pmc_pass(tmp_path, monkeypatch):
@@ -111,10 +114,90 @@ def test_bench_refuses_a_stale_pmc_pass(tmp_path, monkeypatch):
     monkeypatch.delenv("RTW_LIB", raising=False)
 
     class A:
-        config, bvh, spp, tuning = "c2", "sah", 0, ""
+        config, bvh, spp, tuning, profiles_dir = "c2", "sah", 0, "", str(prof)
     assert bench.pmc_valu(A, "wf_step", "aaaa")[0] == entry
     assert bench.pmc_traffic(A, "wf_step", "aaaa")[0] == 10_000_000_000
     e, src = bench.pmc_valu(A, "wf_step", "bbbb")
     assert e is None and "stale" in src
     t, src = bench.pmc_traffic(A, "wf_step", "bbbb")
     assert t is None and "stale" in src
+
+
+def _bench_module():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(REPO, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    return bench
+
+
+def _fake_pass(path, build, kind, n_shards=1, rank=0):
+    b = {"build_id": build, "config": "c2", "n_shards": n_shards, "rank": rank}
+    if kind == "valu":
+        e = {"lane_ops": 1e11, "insts_valu": 3e9, "active_inst_valu": 3e9, "thread_cycles_valu": 1e11,
+             "kernels": ["wf_step_clds<0u>"], "lane_util": 0.5}
+    else:
+        e = {"traffic_bytes": 1e10}
+    json.dump({"wf_step": e, "_build": b}, open(path, "w"))
+
+
+def test_bench_prices_a_rank_only_with_its_own_shard_pass(tmp_path, monkeypatch):
+    """At N > 1 a rank's launches cover ~1/N of the frame: bench.py prices them only with a PMC pass of
+    that rank's shard at that N (profiles/pmc_*_<config>_sah_n<N>_r<R>.json, stamped n_shards / rank), never
+    with the whole-frame pass (which would read as frac ~1.5 at N = 8)."""
+    bench = _bench_module()
+    monkeypatch.delenv("RTW_LIB", raising=False)
+    for kind in ("valu", "traffic"):
+        _fake_pass(tmp_path / f"pmc_{kind}_c2_sah.json", "aaaa", kind)
+
+    class A:
+        config, bvh, spp, tuning, profiles_dir = "c2", "sah", 0, "", str(tmp_path)
+    assert bench.pmc_valu(A, "wf_step", "aaaa", 1, 0)[0] is not None
+    e, src = bench.pmc_valu(A, "wf_step", "aaaa", 8, 0)
+    assert e is None and "no pass of this rank's shard" in src
+    t, src = bench.pmc_traffic(A, "wf_step", "aaaa", 8, 0)
+    assert t is None and "no pass of this rank's shard" in src
+    # a shard pass: used for that (N, R) only
+    for kind in ("valu", "traffic"):
+        _fake_pass(tmp_path / f"pmc_{kind}_c2_sah_n8_r0.json", "aaaa", kind, 8, 0)
+    assert bench.pmc_valu(A, "wf_step", "aaaa", 8, 0)[0]["lane_ops"] == 1e11
+    assert bench.pmc_traffic(A, "wf_step", "aaaa", 8, 0)[0] == 10_000_000_000
+    assert bench.pmc_valu(A, "wf_step", "aaaa", 8, 1)[0] is None
+    assert bench.pmc_valu(A, "wf_step", "aaaa", 4, 0)[0] is None
+    # a file whose stamp does not match its name is refused
+    _fake_pass(tmp_path / "pmc_valu_c2_sah_n4_r0.json", "aaaa", "valu", 1, 0)
+    e, src = bench.pmc_valu(A, "wf_step", "aaaa", 4, 0)
+    assert e is None and "not 0/4" in src
+    # the single-process multi path runs other kernels: no pass at all
+    assert bench.pmc_valu(A, "wf_step", "aaaa", 1, 0, single=True)[0] is None
+
+
+@pytest.mark.parametrize("world_size", [2])
+def test_bench_torchrun_line_never_carries_a_whole_frame_roofline(tmp_path, world_size):
+    """bench.py's torchrun flow (--host-backend: no GPU) with a whole-frame PMC pass of the loaded build
+    present: the N > 1 line leaves every roofline fraction null (or <= 1) and names why."""
+    import socket
+    from conftest import load_pkg
+    build = load_pkg().lib().rtw_build_id().decode()
+    for kind in ("valu", "traffic"):
+        _fake_pass(tmp_path / f"pmc_{kind}_c1_sah.json", build, kind)
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    env.pop("RTW_LIB", None)
+    rn = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world_size}",
+                         "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(REPO, "bench.py"),
+                         "--gpus", str(world_size), "--host-backend", "--config", "c1", "--steps", "1", "--warmup", "0",
+                         "--no-cpu-baseline", "--profiles-dir", str(tmp_path)],
+                        capture_output=True, text=True, timeout=300, cwd=REPO, env=env)
+    assert rn.returncode == 0, rn.stderr[-2000:]
+    d = json.loads([ln for ln in rn.stdout.splitlines() if ln.startswith("{")][-1])
+    r = d["roofline"]
+    assert d["n_gpus"] == world_size and d["config"]["shard"]["n_shards"] == world_size
+    for frac in (r["frac"], r["hbm"]["frac"]):
+        assert frac is None or 0 < frac <= 1
+    assert r["valu"]["lane_ops_per_launch"] is None and r["traffic"] is None
+    assert "no pass of this rank's shard" in r["valu"]["source"]
+    assert "no pass of this rank's shard" in r["hbm"]["source"]

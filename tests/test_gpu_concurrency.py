@@ -69,3 +69,40 @@ def test_device_calls_on_two_streams(rtw, world):
     assert torch.equal(got[:, 3], ref[:, 3])
     # samples added in the same order (0, 1, 2, 3) per pixel: identical sums
     assert torch.equal(got, ref)
+
+
+def test_render_ex_and_render_rows_at_once(rtw, world):
+    """rtw_render_ex releases the context lock between spp batches with its chunk staged on the device;
+    an rtw_render_rows call on the same context in the meantime stages its tile in a buffer of its own
+    (ADVICE r4): both give the images they give alone, bit for bit."""
+    cam = rtw.book1_camera(image_width=200, aspect_ratio=1.5, spp=8).init()
+    W, H = cam.derived.image_width, cam.derived.image_height
+    rpb, n, shard = 8, 3, 1
+    rows = rtw.lib().rtw_shard_rows(H, rpb, n, shard)
+
+    def ex(buf, rc):
+        o = rtw._abi.render_opts(spp_batch=1)
+        rc[0] = rtw.lib().rtw_render_ex(world.handle, C.byref(cam.derived), 0, cam.size, 0, 8, 5, buf.ctypes.data,
+                                        C.byref(o))
+
+    def rows_call(tile, rc):
+        o = rtw._abi.render_opts(spp_batch=1)
+        rc[0] = rtw.lib().rtw_render_rows(world.handle, C.byref(cam.derived), rpb, n, shard, 0, 8, 5,
+                                          tile.ctypes.data, C.byref(o))
+
+    ref_img, ref_tile = np.zeros((cam.size, 4), np.float32), np.zeros((rows * W, 4), np.float32)
+    r1, r2 = [None], [None]
+    ex(ref_img, r1)
+    rows_call(ref_tile, r2)
+    assert r1 == [0] and r2 == [0]
+    for _ in range(3):
+        img, tile = np.zeros_like(ref_img), np.zeros_like(ref_tile)
+        r1, r2 = [None], [None]
+        ts = [threading.Thread(target=ex, args=(img, r1)), threading.Thread(target=rows_call, args=(tile, r2))]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join(timeout=120)
+        assert r1 == [0] and r2 == [0]
+        assert np.array_equal(img, ref_img)
+        assert np.array_equal(tile, ref_tile)

@@ -83,8 +83,9 @@ def main():
     # the library build of both passes (bench.py uses no pass of another build)
     ids = {bench_line(d, c).get("build_id") for c in ("FETCH_SIZE", "WRITE_SIZE")}
     bl = bench_line(d, "FETCH_SIZE")
+    sh = bl.get("config", {}).get("shard") or {}
     out["_build"] = {"build_id": ids.pop() if len(ids) == 1 else None, "config": bl.get("config", {}).get("config_id"),
-                     "value": bl.get("value")}
+                     "value": bl.get("value"), "n_shards": sh.get("n_shards", 1), "rank": sh.get("rank", 0)}
     json.dump(out, open(os.path.join(d, "pmc_traffic.json"), "w"), indent=1, sort_keys=True)
     print(f"build {out['_build']['build_id']}")
     for k, e in sorted(((k, e) for k, e in out.items() if not k.startswith("_")), key=lambda kv: -kv[1]["traffic_bytes"]):

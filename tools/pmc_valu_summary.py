@@ -47,8 +47,9 @@ def main():
             try:
                 bl = json.loads(line)
                 launches = bl["roofline"]["launches"]
+                sh = bl["config"].get("shard") or {}
                 build = {"build_id": bl.get("build_id"), "config": bl["config"].get("config_id"),
-                         "value": bl.get("value")}
+                         "value": bl.get("value"), "n_shards": sh.get("n_shards", 1), "rank": sh.get("rank", 0)}
             except (ValueError, KeyError):
                 pass
     byk = defaultdict(list)

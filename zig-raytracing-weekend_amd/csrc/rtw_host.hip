@@ -8,6 +8,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/rtw_gpu.h"
@@ -474,6 +475,7 @@ void rtw_scene_destroy(rtw_ctx* ctx) {
     if (ctx->last_done) (void)hipEventDestroy(ctx->last_done);
     if (ctx->d_blob) (void)hipFree(ctx->d_blob);
     if (ctx->d_scratch) (void)hipFree(ctx->d_scratch);
+    if (ctx->d_rows) (void)hipFree(ctx->d_rows);
     if (ctx->d_dbg) (void)hipFree(ctx->d_dbg);
     if (ctx->d_work) (void)hipFree(ctx->d_work);
     if (ctx->d_wf) (void)hipFree(ctx->d_wf);
@@ -569,8 +571,16 @@ int validate_cam(const rtw_camera* cam) {
     return RTW_OK;
 }
 
-// Enqueue [s0, s1) in batches on `stream`, polling cancel/progress between
-// batches when `sync_each` (host API).  Returns status.
+// Bytes of the wavefront state run_wavefront takes from one allocation: per slot set (two) the ray_o, ray_d,
+// thr, acc streams (16 B) and rng (8 B); the hit records (8 B) by slot; the radiance (12 B) by path; the three
+// stripe-counter sets; each take 256-B aligned.  RTW_WF_PATH_BYTES is the per-path part of the same sum.
+size_t wf_state_bytes(uint64_t Q, uint64_t P) {
+    auto al = [](uint64_t b) { return (size_t)((b + 255) & ~uint64_t(255)); };
+    return 2 * (4 * al(Q * 16) + al(Q * 8)) + al(Q * 8) + al(P * sizeof(rtw_rgb)) +
+           3 * al((uint64_t)RTW_WF_STRIPES * RTW_WF_LEN_STRIDE * 4);
+}
+static_assert(RTW_WF_PATH_BYTES == 2 * (4 * 16 + 8) + 8 + sizeof(rtw_rgb), "RTW_WF_PATH_BYTES = wf_state_bytes per path");
+
 // Wavefront (v2) render of samples [L.s0, L.s1): batches of n_s samples so that
 // n_pix * n_s paths fit the path-state buffer (grown on demand, kept in the ctx).
 int run_wavefront(rtw_ctx* ctx, rtw_launch L, hipStream_t stream, rtw_timer* T) {
@@ -601,9 +611,7 @@ int run_wavefront(rtw_ctx* ctx, rtw_launch L, hipStream_t stream, rtw_timer* T) 
         ctx->d_wf = nullptr;
         ctx->wf_cap = 0;
         for (;;) {  // device memory taken since scene creation (other contexts, torch): halve the batch
-            const uint64_t Q = slots(need);
-            const size_t bytes = 2 * Q * (4 * 16 + 8 + 4) + Q * 8 + need * 16 +
-                                 3 * (RTW_WF_STRIPES * RTW_WF_LEN_STRIDE * 4 + 256);
+            const size_t bytes = wf_state_bytes(slots(need), need);
             const hipError_t e = hipMalloc(&ctx->d_wf, bytes);
             if (e == hipSuccess) break;
             if (e != hipErrorOutOfMemory || n_s == 1) return hip_fail(e, "wavefront path state");
@@ -616,6 +624,7 @@ int run_wavefront(rtw_ctx* ctx, rtw_launch L, hipStream_t stream, rtw_timer* T) 
     }
     if (n_s * n_pix > ctx->wf_cap) n_s = std::max<uint64_t>(1, ctx->wf_cap / n_pix);
     const uint64_t P = ctx->wf_cap, Q = slots(P);
+    // (the takes below are the layout wf_state_bytes sizes)
     char* cur = static_cast<char*>(ctx->d_wf);
     auto take = [&](size_t nb) {
         char* p = cur;
@@ -703,8 +712,18 @@ int run_batches(rtw_ctx* ctx, rtw_launch L, uint32_t s0, uint32_t s1, uint32_t b
 
 // Host context: samples [s0, s1) in batches on host threads (rtw_cpu.hip), stop flags polled per pixel,
 // progress after each batch.  begin/end/out as rtw_cpu_render.
-int run_host(const rtw_ctx* ctx, rtw_launch L, uint32_t begin, uint32_t end, uint32_t s0, uint32_t s1,
+int run_host(rtw_ctx* ctx, rtw_launch L, uint32_t begin, uint32_t end, uint32_t s0, uint32_t s1,
              uint32_t batch, float* out, const rtw_render_opts* ctl, uint64_t pixels) {
+    // concurrent callers (the 8 Tasks on one host context) share the context's threads instead of each
+    // starting a pool of its own: a call takes cpu_threads / (calls in flight), at least 1
+    struct Count {
+        std::atomic<uint32_t>& c;
+        uint32_t n;
+        explicit Count(std::atomic<uint32_t>& a) : c(a), n(a.fetch_add(1) + 1) {}
+        ~Count() { c.fetch_sub(1); }
+    } in_flight(ctx->cpu_calls);
+    const uint32_t pool = ctx->cpu_threads ? ctx->cpu_threads : std::max(1u, std::thread::hardware_concurrency());
+    const uint32_t threads = std::max(1u, pool / in_flight.n);
     // stop flags: with an explicit spp_batch they are polled between batches only, so a stopped render
     // holds whole batches (every pixel's .w is the last finished batch's end, and a resume from it adds
     // no sample twice); without one, per pixel as Camera.render polls `running` (camera.zig:107) --
@@ -716,7 +735,7 @@ int run_host(const rtw_ctx* ctx, rtw_launch L, uint32_t begin, uint32_t end, uin
         if (!per_pixel && rtw_stop_requested(ctl)) return fail(RTW_E_CANCELLED, "cancelled");
         L.s0 = s;
         L.s1 = (s1 - s < batch) ? s1 : s + batch;
-        if (rtw_cpu_render(L, begin, end, out, ctx->cpu_threads, per_pixel ? ctl : nullptr) == RTW_E_CANCELLED)
+        if (rtw_cpu_render(L, begin, end, out, threads, per_pixel ? ctl : nullptr) == RTW_E_CANCELLED)
             return fail(RTW_E_CANCELLED, "cancelled");
         if (ctl && ctl->progress && ctl->progress(pixels * (uint64_t)(L.s1 - s0), total, ctl->user))
             return fail(RTW_E_CANCELLED, "cancelled by progress callback");
@@ -863,9 +882,9 @@ int rtw_render_ex(rtw_ctx* ctx, const rtw_camera* cam, uint32_t pix_begin, uint3
         ctx->host_cv.wait(lock, [&] { return ctx->scratch_bytes >= bytes || ctx->host_calls == 0; });
         if (int rc = stream_enter(ctx, ctx->stream)) return rc;
         if (int rc = ensure_scratch(ctx, bytes)) return rc;
-        HIP_TRY(hipEventCreateWithFlags(&done, hipEventDisableTiming));
         HIP_TRY(hipMemcpyAsync((char*)ctx->d_scratch + o, (char*)accum + o, nb, hipMemcpyHostToDevice, ctx->stream));
         if (int rc = stream_leave(ctx, ctx->stream)) return rc;
+        HIP_TRY(hipEventCreateWithFlags(&done, hipEventDisableTiming));  // (last: no early return leaks it)
         ctx->host_calls++;
         batch = ubatch ? ubatch : auto_batch(ctx, pixels, spp_end - spp_begin);
     }
@@ -1015,14 +1034,25 @@ int rtw_render_rows(rtw_ctx* ctx, const rtw_camera* cam, uint32_t rpb, uint32_t 
     }
     HIP_TRY(hipSetDevice(ctx->device));
     if (int rc = stream_enter(ctx, ctx->stream)) return rc;
+    // the tile is staged in its own buffer, never in d_scratch: rtw_render_ex calls on this context release
+    // the lock between batches with their chunks staged there
     const size_t nb = (size_t)rows * W * 16;
-    if (int rc = ensure_scratch(ctx, nb)) return rc;
-    HIP_TRY(hipMemcpyAsync(ctx->d_scratch, tile, nb, hipMemcpyHostToDevice, ctx->stream));
+    if (ctx->rows_bytes < nb) {
+        if (ctx->d_rows) {
+            HIP_TRY(hipStreamSynchronize(ctx->stream));
+            (void)hipFree(ctx->d_rows);
+        }
+        ctx->d_rows = nullptr;
+        ctx->rows_bytes = 0;
+        HIP_TRY(hipMalloc(&ctx->d_rows, nb));
+        ctx->rows_bytes = nb;
+    }
+    HIP_TRY(hipMemcpyAsync(ctx->d_rows, tile, nb, hipMemcpyHostToDevice, ctx->stream));
     rtw_render_opts ctl{};
     if (opts) ctl = *opts;
-    int rc = render_rows_locked(ctx, cam, rpb, n_shards, shard, spp_begin, spp_end, seed, ctx->d_scratch, ctx->stream,
+    int rc = render_rows_locked(ctx, cam, rpb, n_shards, shard, spp_begin, spp_end, seed, ctx->d_rows, ctx->stream,
                                 &ctl, rows);
-    hipError_t e = hipMemcpyAsync(tile, ctx->d_scratch, nb, hipMemcpyDeviceToHost, ctx->stream);
+    hipError_t e = hipMemcpyAsync(tile, ctx->d_rows, nb, hipMemcpyDeviceToHost, ctx->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
     if (e != hipSuccess) return hip_fail(e, "rtw_render_rows copy back");
     ctx->last_stream = nullptr;  // synchronised

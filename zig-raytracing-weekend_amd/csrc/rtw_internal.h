@@ -5,6 +5,7 @@
 #include <stdint.h>
 
 #include <condition_variable>
+#include <atomic>
 #include <mutex>
 #include <vector>
 
@@ -205,8 +206,10 @@ struct rtw_ctx {
     rtw_launch base{};
     rtw_scene_stats stats{};
     std::vector<rtw_node> nodes_host;
-    float* d_scratch = nullptr;    // host-API accum staging
+    float* d_scratch = nullptr;    // host-API accum staging (rtw_render_ex: the callers' chunks of one frame)
     size_t scratch_bytes = 0;
+    float* d_rows = nullptr;       // rtw_render_rows' tile staging (its own: render_ex chunks may be staged
+    size_t rows_bytes = 0;         //   in d_scratch while it runs)
     float* d_dbg = nullptr;        // debug kernels output
     uint32_t* d_work = nullptr;    // persistent-kernel work counter (zeroed before each launch)
     uint32_t feat = 0;             // RTW_F_* scene features
@@ -235,6 +238,7 @@ struct rtw_ctx {
     std::mutex mu;
     std::condition_variable host_cv;
     int host_calls = 0;
+    std::atomic<uint32_t> cpu_calls{0};  // host context: calls rendering now (they share cpu_threads)
     hipEvent_t last_done = nullptr;
     hipStream_t last_stream = nullptr;
 };
