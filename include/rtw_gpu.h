@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define RTW_ABI_VERSION 6
+#define RTW_ABI_VERSION 7
 
 enum rtw_status {
     RTW_OK = 0,
@@ -311,7 +311,9 @@ enum {  /* rtw_tuning.fuse */
 #define RTW_OTREE_NO_CULL 0x100u  /* rtw_tuning.object_tree */
 typedef struct rtw_tuning {
     uint32_t kernel;           /* rtw_kernel_kind (default WAVEFRONT) */
-    uint32_t bvh_orders;       /* 0 = auto (8 octant-ordered copies for SAH sphere scenes, else 1), 1 or 8 */
+    uint32_t bvh_orders;       /* 0 = auto (8 octant-ordered copies for SAH sphere scenes, else 1), 1, 4 or 8
+                                  (4: copies ordered by the x and z signs, the walk takes y's near/far per ray;
+                                  half the compact-LDS stage; ABI 7) */
     uint32_t sah_max_leaf;     /* spheres per SAH leaf (default 1) */
     uint32_t compact_nodes;    /* 1 = 16-B fp16 node walk for static sphere SAH trees (default) */
     uint32_t fast_box;         /* 1 = FMA slab test on the padded SAH boxes (default); 0 = aabb.zig arithmetic */
@@ -343,6 +345,9 @@ typedef struct rtw_tuning {
                                   SAH tree, default 90; | RTW_OTREE_NO_CULL: instance and medium leaves do not
                                   test the instance's world box before its transforms and members (ABI 5,
                                   formerly padding) */
+    uint32_t clds_blocks;      /* compact-LDS kernels (fused step, tail) of a 4-copy tree: 0 = two blocks of 640
+                                  threads per CU when the stage fits half the LDS (5 waves per SIMD), 1 = one
+                                  1024-thread block; the 8-copy stage always runs one block (ABI 7) */
 } rtw_tuning;
 
 void rtw_tuning_defaults(rtw_tuning* out);

@@ -29,7 +29,7 @@ def test_exports_every_header_symbol(rtw):
     for n in names:
         assert hasattr(lib, n), n
     assert set(names) == set(rtw._abi.SIGNATURES), set(names) ^ set(rtw._abi.SIGNATURES)
-    assert lib.rtw_version() == 6
+    assert lib.rtw_version() == 7
 
 
 def test_struct_sizes_match_header(rtw, tmp_path):

@@ -153,6 +153,20 @@ def test_c2_full_size_properties(rtw, oracle, book1, oracle_book1):
     assert close(a[pix, :3], ref[:, :3]).all()
 
 
+def test_four_copy_stage_full_c2(rtw, book1):
+    """BASELINE config 2 at its geometry (1200x800, 6 spp): the 4-copy compact stage at two blocks per CU
+    (tuning.bvh_orders 4: copies by the x and z signs, y's slabs by med3) renders the 8-copy image bit for bit,
+    as do its one-block and split-kernel forms."""
+    arr, world = book1
+    cam = rtw.book1_camera().init()
+    ref = render_rows(rtw, world, cam, 0, 800, 0, 6, 2)
+    for tu in ({"bvh_orders": 4}, {"bvh_orders": 4, "clds_blocks": 1}, {"bvh_orders": 4, "fuse": 0}):
+        w = rtw.World(arr, tuning=tu)
+        got = render_rows(rtw, w, cam, 0, 800, 0, 6, 2)
+        w.close()
+        assert np.array_equal(ref, got), tu
+
+
 def test_shard_rows_reassemble(rtw, book1):
     """rtw_render_rows_device (the multi-GPU unit) reassembles to the 1-GPU image."""
     import torch
@@ -318,7 +332,11 @@ def test_v1_knobs_invariant(rtw, book1, knob):
                                   {"lds": 127 & ~2, "wide_walk": 0}, {"fuse": 5}, {"lds": 127 & ~2, "fuse": 5},
                                   {"lds": 127 & ~2, "fuse": 5, "wide_walk": 0}, {"hoist": 0}, {"hoist": 0, "fuse": 0},
                                   {"sort_iters": 0}, {"sort_iters": 50}, {"sort_iters_split": 50, "fuse": 0}, {"sort_iters_split": 0, "fuse": 0},
-                                  {"sort_iters": 2, "wf_iters": 1}, {"sort_bits": 0}, {"sort_bits": 2, "fuse": 0}, {"wf_iters": 3, "fuse": 0}])
+                                  {"sort_iters": 2, "wf_iters": 1}, {"sort_bits": 0}, {"sort_bits": 2, "fuse": 0}, {"wf_iters": 3, "fuse": 0},
+                                  {"bvh_orders": 4}, {"bvh_orders": 4, "clds_blocks": 1}, {"bvh_orders": 4, "fuse": 0},
+                                  {"bvh_orders": 4, "lds": 127 & ~2}, {"bvh_orders": 4, "wide_walk": 0, "lds": 127 & ~2},
+                                  {"bvh_orders": 4, "compact_nodes": 0}, {"bvh_orders": 4, "kernel": 1},
+                                  {"bvh_orders": 4, "kernel": 2}])
 def test_wavefront_knobs_invariant(rtw, book1, knob):
     """Wavefront tuning (rtw_tuning: bounces before the tail kernel, batch size ->
     many batches, FMA vs reference slab test, LDS-staged nodes, SAH leaf runs of up
@@ -349,7 +367,8 @@ def test_compact_nodes_are_exact(rtw, n, seed):
     cam = rtw.book1_camera(image_width=480, aspect_ratio=16 / 9, spp=4).init()
     outs = []
     for tu in ({"compact_nodes": 0, "tile_lists": 0, "hoist": 0}, {"compact_nodes": 1, "wide_walk": 0},
-               {"compact_nodes": 1, "wide_walk": 1}, {"compact_nodes": 1, "wide_walk": 0, "hoist": 0}):
+               {"compact_nodes": 1, "wide_walk": 1}, {"compact_nodes": 1, "wide_walk": 0, "hoist": 0},
+               {"compact_nodes": 1, "wide_walk": 0, "bvh_orders": 4}):
         w = rtw.World(arr, tuning=tu)
         outs.append(render_rows(rtw, w, cam, 0, cam.derived.image_height, 0, 4, 6))
         w.close()
@@ -357,6 +376,7 @@ def test_compact_nodes_are_exact(rtw, n, seed):
     assert np.array_equal(outs[0], outs[1])
     assert np.array_equal(outs[0], outs[2])  # the two-wide stack walk (rtw_wide2_nodes): same hits
     assert np.array_equal(outs[0], outs[3])  # the ground sphere inside the tree (no hoisting)
+    assert np.array_equal(outs[0], outs[4])  # 4 (x, z)-sign copies, y near/far by med3 (traverse_compact<.., Y4>)
     # (the defaults also give camera rays the frustum-walked tile lists of large trees: same hits)
 
 

@@ -460,6 +460,11 @@ public:
         for (uint32_t o = 0; o < orders; o++) {
             float dir[3];
             for (int k = 0; k < 3; k++) dir[k] = orders == 1 ? dir_[k] : ((o >> k) & 1 ? -1.0f : 1.0f);
+            if (orders == 4) {  // copies by the x and z signs (order_of): diagonals in the xz plane
+                dir[0] = (o & 1u) ? -1.0f : 1.0f;
+                dir[1] = 0.0f;
+                dir[2] = (o & 2u) ? -1.0f : 1.0f;
+            }
             base_ = (uint32_t)nodes_.size();
             for (size_t k = 0; k < h; k++)
                 nodes_.push_back(geo_.leaf(objs_[idx_[k]], (uint32_t)nodes_.size() + 1 - base_));
@@ -774,8 +779,9 @@ uint16_t h_up(float x) {
 }  // namespace
 
 bool rtw_compact_nodes(const std::vector<rtw_node>& nodes, uint32_t orders, std::vector<rtw_cnode>& out) {
-    if (orders != 8 || nodes.size() % 8) return false;  // one copy per ray-direction octant
-    const size_t per = nodes.size() / 8;
+    // one copy per ray-direction octant, or (orders = 4) per sign pair of x and z
+    if ((orders != 8 && orders != 4) || nodes.size() % orders) return false;
+    const size_t per = nodes.size() / orders;
     out.resize(nodes.size());
     for (size_t i = 0; i < nodes.size(); i++) {
         const uint32_t oct = (uint32_t)(i / per);  // order_of: bit k set = negative direction on axis k
@@ -794,11 +800,13 @@ bool rtw_compact_nodes(const std::vector<rtw_node>& nodes, uint32_t orders, std:
         }
         // per axis the slab the copy's rays enter first (near) and leave last (far):
         // min/max for a non-negative direction component, swapped for a negative one
+        // (orders = 4: x and z by the copy's signs, y as min / max -- traverse_compact<.., Y4> takes the
+        // median of three, which needs no order between the two y slabs)
         uint16_t h[6];
         for (int k = 0; k < 3; k++) {
             if (!(std::fabs(n.a[k]) <= 60000.0f) || !(std::fabs(n.b[k]) <= 60000.0f)) return false;
             const uint16_t lo = h_down(n.a[k]), hi = h_up(n.b[k]);
-            const bool neg = (oct >> k) & 1u;
+            const bool neg = orders == 4 ? (k == 1 ? false : ((oct >> (k / 2)) & 1u)) : ((oct >> k) & 1u);
             h[k] = neg ? hi : lo;
             h[3 + k] = neg ? lo : hi;
         }

@@ -15,6 +15,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <cmath>
+
 #include "../../include/rtw_gpu.h"
 #include "rtw_internal.h"
 #include "rtw_layout.h"
@@ -825,9 +827,21 @@ RTW_DHD uint32_t trav_step(const float4* __restrict__ nodes, const rtw_launch& L
 // slower: more node visits and no gain in coherence).  The copy is recorded in
 // the hit id (bits 24..26; such scenes have no instance members there) so
 // shading finds the leaf.
+// 4 copies (round 5): ordered by the signs of x and z only -- the axes the Book-1 field spreads over
+// (the spheres lie within [0, 2] in y) -- so the compact stage is half the size (rtw_compact_nodes); the
+// walk then takes y's near/far per ray (traverse_compact<.., Y4>).
 RTW_DHD uint32_t order_of(const rtw_launch& L, const Ray& r) {
     if (L.n_orders <= 1) return 0;
+    if (L.n_orders == 4) return (r.d.x < 0 ? 1u : 0u) | (r.d.z < 0 ? 2u : 0u);
     return (r.d.x < 0 ? 1u : 0u) | (r.d.y < 0 ? 2u : 0u) | (r.d.z < 0 ? 4u : 0u);
+}
+// median of three (v_med3_f32 on the device); operands finite (the fast slab test's clamped reciprocals)
+RTW_DHD float med3f(float a, float b, float c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_fmed3f(a, b, c);
+#else
+    return std::fmax(std::fmin(a, b), std::fmin(std::fmax(a, b), c));
+#endif
 }
 RTW_DHD const float4* order_base(const float4* nodes, const rtw_launch& L, uint32_t oct) {
     return nodes + (size_t)oct * 2u * L.n_nodes;
@@ -884,7 +898,14 @@ RTW_DHD uint32_t lds_addr(const void* p) {
     return 0;
 #endif
 }
-template <bool COUNT, bool LDS = false>
+// Y4: the 4-copy layout (L.n_orders == 4; rtw_compact_nodes): x and z stored (near, far) for the copy's
+// signs, y as (min, max) in the near-y / far-y slots.  With ta, tb the two y slab distances, lo = max(X, min(ta,
+// tb)) and hi = min(Y, max(ta, tb)) (X = max(tmin, tnx, tnz), Y = min(closest, tfx, tfz)); the walk uses
+// lo' = med3(X, ta, tb) = min(lo, max(ta, tb)) and hi' = med3(Y, ta, tb) = max(hi, min(ta, tb)), and lo' < hi'
+// exactly when lo < hi (lo' <= lo and hi' >= hi; if lo > max(ta, tb) then hi' <= max(ta, tb) = lo', and if
+// hi < min(ta, tb) then lo' >= min(ta, tb) = hi').  Four min/max-class instructions per box, as the 8-copy
+// walk's max3 + max and min3 + min: the same test at the same cost, with half the stage.
+template <bool COUNT, bool LDS = false, bool Y4 = false>
 RTW_DHD int traverse_compact(const rtw_launch& L, const uint4* base, const Ray& r, float& t_out,
                                                 Counters& cnt) {
     const uint32_t oct = order_of(L, r);
@@ -898,9 +919,13 @@ RTW_DHD int traverse_compact(const rtw_launch& L, const uint4* base, const Ray& 
     // non-decreasing for inv >= 0.  The sign of inv must then follow the octant, which
     // tests d < 0: a -0.0 component (octant "positive", rcp = -inf) gets +1e30.
     RayTrav rt = ray_trav(r, true);
-    rt.inv = mk((oct & 1u) ? -__builtin_fabsf(rt.inv.x) : __builtin_fabsf(rt.inv.x),
-                (oct & 2u) ? -__builtin_fabsf(rt.inv.y) : __builtin_fabsf(rt.inv.y),
-                (oct & 4u) ? -__builtin_fabsf(rt.inv.z) : __builtin_fabsf(rt.inv.z));
+    if constexpr (Y4)  // y: either sign (med3 below is symmetric in the two y slabs)
+        rt.inv = mk((oct & 1u) ? -__builtin_fabsf(rt.inv.x) : __builtin_fabsf(rt.inv.x), rt.inv.y,
+                    (oct & 2u) ? -__builtin_fabsf(rt.inv.z) : __builtin_fabsf(rt.inv.z));
+    else
+        rt.inv = mk((oct & 1u) ? -__builtin_fabsf(rt.inv.x) : __builtin_fabsf(rt.inv.x),
+                    (oct & 2u) ? -__builtin_fabsf(rt.inv.y) : __builtin_fabsf(rt.inv.y),
+                    (oct & 4u) ? -__builtin_fabsf(rt.inv.z) : __builtin_fabsf(rt.inv.z));
     rt.oinv = mk(-(r.o.x * rt.inv.x), -(r.o.y * rt.inv.y), -(r.o.z * rt.inv.z));
     float closest = kInf;
     int hit = -1;  // the byte offset of the closest sphere's node
@@ -912,7 +937,7 @@ RTW_DHD int traverse_compact(const rtw_launch& L, const uint4* base, const Ray& 
     dgv.walks = 1;
 #endif
 #if defined(RTW_WALK_PREFETCH) && defined(__HIP_DEVICE_COMPILE__)
-    if constexpr (LDS) {
+    if constexpr (LDS && !Y4) {
         // A/B variant: the pre-order successor i + 16 (a leaf's next node, an entered box's first child)
         // is read while node i is tested; a lane whose next node is the skip target reads it then
         uint4 c = *(lds_uint4*)(uintptr_t)i;
@@ -946,7 +971,7 @@ RTW_DHD int traverse_compact(const rtw_launch& L, const uint4* base, const Ray& 
     }
 #endif
 #if defined(RTW_LEAF_POSTPONE) && defined(__HIP_DEVICE_COMPILE__)
-    if constexpr (LDS) {
+    if constexpr (LDS && !Y4) {
         // A/B variant: a lane that reaches a leaf waits there (its walk is unchanged: every box test and
         // sphere test of the lane happens in the same order with the same closest) until at least
         // 1/RTW_LEAF_POSTPONE of the wave's walking lanes wait too, or no walking lane is at an inner node;
@@ -1013,8 +1038,14 @@ RTW_DHD int traverse_compact(const rtw_launch& L, const uint4* base, const Ray& 
             const float tfx = __builtin_fmaf(h_hi(c.y), rt.inv.x, rt.oinv.x);
             const float tfy = __builtin_fmaf(h_lo(c.z), rt.inv.y, rt.oinv.y);
             const float tfz = __builtin_fmaf(h_hi(c.z), rt.inv.z, rt.oinv.z);
-            const float lo = __builtin_fmaxf(__builtin_fmaxf(kTmin, tnx), __builtin_fmaxf(tny, tnz));
-            const float hi = __builtin_fminf(__builtin_fminf(closest, tfx), __builtin_fminf(tfy, tfz));
+            float lo, hi;
+            if constexpr (Y4) {  // tny / tfy: the y slabs of min / max y, in either order
+                lo = med3f(__builtin_fmaxf(__builtin_fmaxf(kTmin, tnx), tnz), tny, tfy);
+                hi = med3f(__builtin_fminf(__builtin_fminf(closest, tfx), tfz), tny, tfy);
+            } else {
+                lo = __builtin_fmaxf(__builtin_fmaxf(kTmin, tnx), __builtin_fmaxf(tny, tnz));
+                hi = __builtin_fminf(__builtin_fminf(closest, tfx), __builtin_fminf(tfy, tfz));
+            }
             i = (hi <= lo) ? c.w : i + 16u;
         }
     }
@@ -1035,6 +1066,9 @@ RTW_DHD int traverse(const float4* __restrict__ nodes, const rtw_launch& L, cons
                                         float& t_out, Counters& cnt, uint64_t mkey = 0) {
     if constexpr (COMPACT && (FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING)) == 0) {
         if (L.cnodes && L.fast_box) {  // per-step counters only in counted passes
+            if (L.n_orders == 4)
+                return L.counters ? traverse_compact<true, false, true>(L, L.cnodes, r, t_out, cnt)
+                                  : traverse_compact<false, false, true>(L, L.cnodes, r, t_out, cnt);
             return L.counters ? traverse_compact<true>(L, L.cnodes, r, t_out, cnt)
                               : traverse_compact<false>(L, L.cnodes, r, t_out, cnt);
         }

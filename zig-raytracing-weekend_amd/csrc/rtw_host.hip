@@ -174,7 +174,9 @@ int rtw_scene_create_ex(const rtw_scene_desc* d, int device, const rtw_tuning* t
     rtw_tuning_defaults(&tu);
     if (tuning) tu = *tuning;
     if (tu.kernel > RTW_KERNEL_SIMPLE) return fail(RTW_E_INVALID, "tuning.kernel out of range");
-    if (tu.bvh_orders != 0 && tu.bvh_orders != 1 && tu.bvh_orders != 8) return fail(RTW_E_INVALID, "tuning.bvh_orders must be 0, 1 or 8");
+    if (tu.bvh_orders != 0 && tu.bvh_orders != 1 && tu.bvh_orders != 4 && tu.bvh_orders != 8)
+        return fail(RTW_E_INVALID, "tuning.bvh_orders must be 0, 1, 4 or 8");
+    if (tu.clds_blocks > 2) return fail(RTW_E_INVALID, "tuning.clds_blocks must be 0, 1 or 2");
     if (tu.wf_iters < 1 || tu.wf_iters > RTW_WF_MAX_ITERS) return fail(RTW_E_INVALID, "tuning.wf_iters out of range");
     if ((tu.object_tree & 0xFFu) > 100 || (tu.object_tree & ~(0xFFu | RTW_OTREE_NO_CULL)))
         return fail(RTW_E_INVALID, "tuning.object_tree: 0..100 [| RTW_OTREE_NO_CULL]");
@@ -216,12 +218,14 @@ int rtw_scene_create_ex(const rtw_scene_desc* d, int device, const rtw_tuning* t
     ctx->device = device;
     rtw_geometry geom;
     uint32_t depth = 0, draws = 0;
-    // SAH trees of sphere scenes: 8 octant-ordered copies of the node array (RTW_ORDERS=1: one, ordered
+    // SAH trees of sphere scenes: 8 octant-ordered copies of the node array (tuning.bvh_orders 4: copies by the
+    // x and z signs; 1: one, ordered
     // along order_dir).  Scenes with quads/instances/media keep one order: their leaf tests are costly, and
     // lanes walking different orders stop executing them together (Cornell: -31 % with 8 orders).
     const bool objects = d->n_quads || d->n_instances || d->n_media;
     uint32_t orders = (d->bvh_mode == RTW_BVH_SAH && !objects) ? 8u : 1u;
-    if (tu.bvh_orders) orders = (d->bvh_mode == RTW_BVH_SAH && tu.bvh_orders == 8) ? 8u : 1u;
+    // (object scenes keep one ordering: their hit ids carry an instance member where sphere scenes carry the copy)
+    if (tu.bvh_orders) orders = (d->bvh_mode == RTW_BVH_SAH && !objects && tu.bvh_orders > 1) ? tu.bvh_orders : 1u;
     uint32_t n_hoisted = 0;
     int rc = rtw_build_bvh(*d, ctx->nodes_host, geom, &depth, &draws, &ctx->box_pad, &ctx->extent, orders,
                            tu.sah_max_leaf, tu.hoist && !objects ? 1u : 0u, &n_hoisted, objects ? (tu.object_tree & 0xFFu) : 0u);
@@ -387,6 +391,7 @@ int rtw_scene_create_ex(const rtw_scene_desc* d, int device, const rtw_tuning* t
     L.images = dev + o_imgs;
     L.n_nodes = (uint32_t)n_nodes;
     L.n_orders = orders;
+    L.clds_blocks = tu.clds_blocks;
     L.n_perlin = d->n_perlins;
     ctx->feat = scene_features(d) | geom.feat;
     L.feat = ctx->feat;
@@ -649,7 +654,7 @@ int run_wavefront(rtw_ctx* ctx, rtw_launch L, hipStream_t stream, rtw_timer* T) 
     W.sort_mask = ctx->wf_sort_mask;
     W.run_log2 = 4;  // set per launch grid by wf_coherence (rtw_wavefront.hip)
     // camera-ray candidate lists (the compact-LDS fused step of static sphere scenes, rtw_tuning.tile_lists)
-    if (L.tile_lists && L.cnodes && L.n_orders == 8) {
+    if (L.tile_lists && L.cnodes && L.n_orders >= 4) {
         const uint64_t tiles = n_pix / 64;
         if (ctx->tl_cap < tiles) {
             if (ctx->d_tl) {

@@ -69,7 +69,8 @@ struct rtw_launch {
     uint32_t fast_box;           // 1 = FMA slab test on padded boxes (SAH trees only), 0 = aabb.zig arithmetic
     uint32_t inst_cull;          // 1 = instance / medium leaves test the instance's padded world box first
                                  // (only with fast_box; rtw_tuning.object_tree without RTW_OTREE_NO_CULL)
-    uint32_t n_orders;           // 1, or 8 octant-ordered copies of the node array (SAH sphere scenes)
+    uint32_t n_orders;           // 1, or 4 / 8 sign-ordered copies of the node array (SAH sphere scenes)
+    uint32_t clds_blocks;        // compact-LDS kernels of a 4-copy tree: 0 = two blocks per CU when they fit, 1 = one
     uint32_t wf_lds;             // wavefront trace: stage the node array(s) in LDS when they fit
     uint32_t wf_clds;            // wavefront trace: stage the compact nodes (all orders) in LDS when they fit
     uint32_t wf_fuse;            // with the compact LDS stage: one gen+trace+shade kernel per iteration,

@@ -926,7 +926,7 @@ __global__ __launch_bounds__(256) void wf_trace(rtw_launch L, rtw_wf W, uint32_t
 // trace over the compact nodes staged in LDS (all octant copies of a small tree,
 // e.g. BASELINE config 2: 8 x 969 x 16 B = 124 KB): 1024-thread blocks share one
 // copy (one block per CU), ds_read_b128 instead of vector-memory gathers
-template <uint32_t FEAT, bool CAM = false>
+template <uint32_t FEAT, bool CAM = false, bool Y4 = false>
 __global__ __launch_bounds__(1024) void wf_trace_clds(rtw_launch L, rtw_wf W, uint32_t it) {
     static_assert((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING)) == 0, "static sphere scenes");
     if (blockIdx.x == 0 && threadIdx.x < RTW_WF_STRIPES) W.len[(it + 1u) % 3u][threadIdx.x * RTW_WF_LEN_STRIDE] = 0;
@@ -943,8 +943,8 @@ __global__ __launch_bounds__(1024) void wf_trace_clds(rtw_launch L, rtw_wf W, ui
             const Ray r = wf_input_ray<FEAT, CAM>(L, W, S, slot, it, depth, rng, txy, true);
             if (depth) {
                 float t;
-                const int h = L.counters ? traverse_compact<true, true>(L, wf_clds, r, t, cnt)
-                                         : traverse_compact<false, true>(L, wf_clds, r, t, cnt);
+                const int h = L.counters ? traverse_compact<true, true, Y4>(L, wf_clds, r, t, cnt)
+                                         : traverse_compact<false, true, Y4>(L, wf_clds, r, t, cnt);
                 W.hit[slot] = make_float2(t, __int_as_float(h));
                 cnt.rays++;
             }
@@ -1046,7 +1046,7 @@ __device__ __forceinline__ void wf_shade_body(const rtw_launch& L, const rtw_wf&
 // tail: the paths still queued after the last wavefront iteration, each to
 // completion; a lane whose path ends takes the wave's next path at once.
 // CLDS: the walk reads the compact nodes staged in LDS (`lds`) instead of L1/L2.
-template <uint32_t FEAT, bool CLDS>
+template <uint32_t FEAT, bool CLDS, bool Y4 = false>
 __device__ __forceinline__ void wf_tail_body(const rtw_launch& L, const rtw_wf& W, uint32_t it, const uint4* lds,
                                              const float4* nodes = nullptr) {
     const uint32_t lane = __lane_id();
@@ -1091,8 +1091,8 @@ __device__ __forceinline__ void wf_tail_body(const rtw_launch& L, const rtw_wf& 
             float t;
             int hit;
             if constexpr (CLDS)
-                hit = L.counters ? traverse_compact<true, true>(L, lds, r, t, cnt)
-                                 : traverse_compact<false, true>(L, lds, r, t, cnt);
+                hit = L.counters ? traverse_compact<true, true, Y4>(L, lds, r, t, cnt)
+                                 : traverse_compact<false, true, Y4>(L, lds, r, t, cnt);
             else
                 hit = nodes ? traverse<FEAT, false>(nodes, L, r, t, cnt, rng.s)  // the LDS stage
                             : wf_traverse_global<FEAT>(L, r, t, cnt, rng.s);
@@ -1220,26 +1220,38 @@ __global__ __launch_bounds__(256) void wf_tail_lds(rtw_launch L, rtw_wf W, uint3
 }
 
 
-template <uint32_t FEAT>
+template <uint32_t FEAT, bool Y4 = false>
 __global__ __launch_bounds__(1024) void wf_tail_clds(rtw_launch L, rtw_wf W, uint32_t it) {
     static_assert((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING)) == 0, "static sphere scenes");
     extern __shared__ uint4 wf_clds[];
     stage_clds(L, wf_clds);
-    wf_tail_body<FEAT, true>(L, W, it, wf_clds);
+    wf_tail_body<FEAT, true, Y4>(L, W, it, wf_clds);
+}
+// the 4-copy stage (half the LDS) at two blocks per CU: 2 x 640 threads = 5 waves per SIMD (<= 96 VGPRs)
+template <uint32_t FEAT>
+__global__ __launch_bounds__(RTW_CLDS2_THREADS) __attribute__((amdgpu_waves_per_eu(5)))
+void wf_tail_clds2(rtw_launch L, rtw_wf W, uint32_t it) {
+    static_assert((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING)) == 0, "static sphere scenes");
+    extern __shared__ uint4 wf_clds[];
+    stage_clds(L, wf_clds);
+    wf_tail_body<FEAT, true, true>(L, W, it, wf_clds);
 }
 
 // Where the fused step's walk reads the tree:
 //   WALK_CLDS   the compact nodes of every octant copy staged in LDS (small static sphere SAH trees, C2)
 //   WALK_LDS    the 32-B node array of one ordering staged in LDS (small object scenes: Cornell)
 //   WALK_GLOBAL L.cnodes / L.nodes through L1/L2 (large trees: C4)
-enum { WALK_CLDS = 0, WALK_LDS = 1, WALK_GLOBAL = 2 };
+//   WALK_CLDS4  the compact nodes of the 4 (x, z)-sign copies staged in LDS (traverse_compact<.., Y4>)
+enum { WALK_CLDS = 0, WALK_LDS = 1, WALK_GLOBAL = 2, WALK_CLDS4 = 3 };
 
 template <uint32_t FEAT, int WALK>
 __device__ __forceinline__ int wf_walk(const rtw_launch& L, const void* lds, const Ray& r, float& t, Counters& cnt,
                                        uint64_t mkey) {
-    if constexpr (WALK == WALK_CLDS) {
+    if constexpr (WALK == WALK_CLDS || WALK == WALK_CLDS4) {
+        constexpr bool Y4 = WALK == WALK_CLDS4;
         const uint4* cn = static_cast<const uint4*>(lds);
-        return L.counters ? traverse_compact<true, true>(L, cn, r, t, cnt) : traverse_compact<false, true>(L, cn, r, t, cnt);
+        return L.counters ? traverse_compact<true, true, Y4>(L, cn, r, t, cnt)
+                          : traverse_compact<false, true, Y4>(L, cn, r, t, cnt);
     } else if constexpr (WALK == WALK_LDS) {
         return traverse<FEAT, false>(static_cast<const float4*>(lds), L, r, t, cnt, mkey);  // the LDS stage
     } else {
@@ -1390,8 +1402,27 @@ __device__ __forceinline__ void wf_step_zero_next(const rtw_wf& W, uint32_t it) 
     if (blockIdx.x == 0 && threadIdx.x < RTW_WF_STRIPES) W.len[(it + 2u) % 3u][threadIdx.x * RTW_WF_LEN_STRIDE] = 0;
 }
 
-// compact nodes of every octant copy in LDS (one 1024-thread block per CU)
-template <uint32_t FEAT>
+// compact nodes of every copy in LDS, then the materials when they fit
+template <uint32_t FEAT, int WALK>
+__device__ __forceinline__ void wf_step_clds_body(const rtw_launch& L, const rtw_wf& W, uint32_t it) {
+    wf_step_zero_next(W, it);
+    extern __shared__ uint4 wf_clds[];
+    stage_clds(L, wf_clds);
+    if (L.mat_lds) {  // the materials after the nodes (the host checked that they fit)
+        uint4* ml = wf_clds + L.n_nodes * L.n_orders;
+        const uint4* src = reinterpret_cast<const uint4*>(L.mats);
+        for (uint32_t k = threadIdx.x; k < L.mat_lds / 16u; k += blockDim.x) ml[k] = src[k];
+        __syncthreads();
+        rtw_launch Lm = L;
+        Lm.mats = reinterpret_cast<const rtw_dev_material*>(ml);
+        wf_step_body<FEAT, WALK>(Lm, W, it, wf_clds);
+        return;
+    }
+    wf_step_body<FEAT, WALK>(L, W, it, wf_clds);
+}
+
+// one 1024-thread block per CU (the 8-copy stage, 124 KB for C2, allows no second block)
+template <uint32_t FEAT, bool Y4 = false>
 __global__ __launch_bounds__(1024) void wf_step_clds(rtw_launch L, rtw_wf W, uint32_t it) {
     static_assert((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING)) == 0, "static sphere scenes");
 #if defined(RTW_SETPRIO)
@@ -1402,20 +1433,18 @@ __global__ __launch_bounds__(1024) void wf_step_clds(rtw_launch L, rtw_wf W, uin
         else if (pr == 3u) __builtin_amdgcn_s_setprio(3);
     }
 #endif
-    wf_step_zero_next(W, it);
-    extern __shared__ uint4 wf_clds[];
-    stage_clds(L, wf_clds);
-    if (L.mat_lds) {  // the materials after the nodes (the host checked that they fit)
-        uint4* ml = wf_clds + L.n_nodes * L.n_orders;
-        const uint4* src = reinterpret_cast<const uint4*>(L.mats);
-        for (uint32_t k = threadIdx.x; k < L.mat_lds / 16u; k += 1024u) ml[k] = src[k];
-        __syncthreads();
-        rtw_launch Lm = L;
-        Lm.mats = reinterpret_cast<const rtw_dev_material*>(ml);
-        wf_step_body<FEAT, WALK_CLDS>(Lm, W, it, wf_clds);
-        return;
-    }
-    wf_step_body<FEAT, WALK_CLDS>(L, W, it, wf_clds);
+    wf_step_clds_body<FEAT, Y4 ? WALK_CLDS4 : WALK_CLDS>(L, W, it);
+}
+
+// The 4-copy stage (C2: 62 KB + 15.5 KB of materials) at two blocks per CU: 2 x 640 threads = 5 waves
+// per SIMD instead of 4, register-capped at 96 VGPRs (MI355X_MICROARCH.md: 88-96 allocated -> 5 waves).
+// The fused step waits on its dependent ds_read_b128 41 % of the cycles at 4 waves (profiles/r4_stall/):
+// a fifth wave per SIMD has more ready work to issue in those waits.
+template <uint32_t FEAT>
+__global__ __launch_bounds__(RTW_CLDS2_THREADS) __attribute__((amdgpu_waves_per_eu(5)))
+void wf_step_clds2(rtw_launch L, rtw_wf W, uint32_t it) {
+    static_assert((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING)) == 0, "static sphere scenes");
+    wf_step_clds_body<FEAT, WALK_CLDS4>(L, W, it);
 }
 
 // wf_step's LDS extras by mask (bit 0 Perlin tables, 1 materials/textures, 2 geometry); masks a
@@ -1502,7 +1531,15 @@ uint32_t wf_grid(K kernel, int n_cu, size_t lds = 0, uint32_t threads = 256) {
     int b = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kernel, (int)threads, lds) != hipSuccess || b < 1) b = 1;
     uint32_t g = (uint32_t)(b * n_cu);
-    const uint32_t per = RTW_WF_STRIPES / (threads / 64);  // blocks per whole set of stripes
+    // whole sets of stripes: the grid's waves a multiple of RTW_WF_STRIPES (every stripe the same number of
+    // waves, WfIter), i.e. blocks a multiple of 256 / gcd(256, waves per block)
+    uint32_t wpb = threads / 64, gcd = RTW_WF_STRIPES;
+    for (uint32_t a = wpb; a;) {
+        const uint32_t t = gcd % a;
+        gcd = a;
+        a = t;
+    }
+    const uint32_t per = RTW_WF_STRIPES / gcd;
     g -= g % per;
     return g ? g : per;
 }
@@ -1615,11 +1652,26 @@ void wf_run_fused(const rtw_launch& L, const rtw_wf& W0, hipStream_t st, int n_c
                  gdyn = wf_w2_lds<FEAT>(L);
     thread_local uint32_t cgrid[2] = {0, 0}, tgrid[2] = {0, 0}, lgrid[2] = {0, 0}, ggrid[2] = {0, 0}, wtail[2] = {0, 0};
     uint32_t grid = 0;
+    // The compact stage's block shape: the 8-copy stage (C2: 124 KB) leaves room for one 1024-thread block
+    // per CU; the 4-copy stage (L.n_orders == 4, 62 KB) for two blocks of RTW_CLDS2_THREADS (5 waves per SIMD)
+    // when it fits half the LDS (rtw_tuning.clds_blocks: 0 = so, 1 = one 1024-thread block)
+    const bool y4 = L.n_orders == 4, two = clds && y4 && L.clds_blocks != 1 && cdyn0 <= RTW_WF_CLDS2_MAX;
+    const size_t cdyn2 = two && cdyn > RTW_WF_CLDS2_MAX ? cdyn0 : cdyn;  // materials only if they fit too
+    const uint32_t cthreads = two ? RTW_CLDS2_THREADS : 1024u;
     if constexpr ((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING)) == 0) {
-        if (clds && cgrid[1] != cdyn) {
-            cgrid[0] = wf_grid(wf_step_clds<FEAT>, n_cu, cdyn, 1024);
-            tgrid[0] = wf_grid(wf_tail_clds<FEAT>, n_cu, clds, 1024);
-            cgrid[1] = tgrid[1] = (uint32_t)cdyn;
+        const uint32_t key = (uint32_t)cdyn2 | (two ? 0x80000000u : 0u) | (y4 ? 0x40000000u : 0u);
+        if (clds && cgrid[1] != key) {
+            if (two) {
+                cgrid[0] = wf_grid(wf_step_clds2<FEAT>, n_cu, cdyn2, RTW_CLDS2_THREADS);
+                tgrid[0] = wf_grid(wf_tail_clds2<FEAT>, n_cu, clds, RTW_CLDS2_THREADS);
+            } else if (y4) {
+                cgrid[0] = wf_grid(wf_step_clds<FEAT, true>, n_cu, cdyn2, 1024);
+                tgrid[0] = wf_grid(wf_tail_clds<FEAT, true>, n_cu, clds, 1024);
+            } else {
+                cgrid[0] = wf_grid(wf_step_clds<FEAT, false>, n_cu, cdyn2, 1024);
+                tgrid[0] = wf_grid(wf_tail_clds<FEAT, false>, n_cu, clds, 1024);
+            }
+            cgrid[1] = tgrid[1] = key;
         }
     }
     if (clds) {
@@ -1636,7 +1688,7 @@ void wf_run_fused(const rtw_launch& L, const rtw_wf& W0, hipStream_t st, int n_c
     // iteration 0 appends to len[1]; every later iteration's output counters are
     // zeroed by the kernel two iterations before (wf_step_zero_next)
     (void)hipMemsetAsync(W0.len[1], 0, RTW_WF_STRIPES * RTW_WF_LEN_STRIDE * 4, st);
-    rtw_wf W = wf_coherence(W0, grid * (clds ? 16u : 4u), W0.sort_iters);
+    rtw_wf W = wf_coherence(W0, grid * (clds ? cthreads / 64u : 4u), W0.sort_iters);
     W.packed = wf_packed<FEAT>() ? 1u : 0u;  // the fused step and its tail: always the packed state
     const uint32_t iters = L.max_depth < W.iters ? L.max_depth : W.iters;
     rtw_wf Wt = W;  // the camera-ray lists serve the LDS-staged steps of static sphere scenes
@@ -1650,8 +1702,13 @@ void wf_run_fused(const rtw_launch& L, const rtw_wf& W0, hipStream_t st, int n_c
         if constexpr ((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING)) == 0) {
             if (clds) {
                 rtw_launch Lc = L;  // the materials are staged only when they fit
-                if (cdyn == cdyn0) Lc.mat_lds = 0;
-                hipLaunchKernelGGL(wf_step_clds<FEAT>, dim3(grid), dim3(1024), cdyn, st, Lc, Wt, it);
+                if (cdyn2 == cdyn0) Lc.mat_lds = 0;
+                if (two)
+                    hipLaunchKernelGGL(wf_step_clds2<FEAT>, dim3(grid), dim3(RTW_CLDS2_THREADS), cdyn2, st, Lc, Wt, it);
+                else if (y4)
+                    hipLaunchKernelGGL((wf_step_clds<FEAT, true>), dim3(grid), dim3(1024), cdyn2, st, Lc, Wt, it);
+                else
+                    hipLaunchKernelGGL((wf_step_clds<FEAT, false>), dim3(grid), dim3(1024), cdyn2, st, Lc, Wt, it);
                 RTW_TIME_END(T)
                 continue;
             }
@@ -1667,7 +1724,12 @@ void wf_run_fused(const rtw_launch& L, const rtw_wf& W0, hipStream_t st, int n_c
         bool done = false;
         if constexpr ((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING)) == 0) {
             if (clds && (L.wf_fuse & 2u)) {
-                hipLaunchKernelGGL(wf_tail_clds<FEAT>, dim3(tgrid[0]), dim3(1024), clds, st, L, W, iters);
+                if (two)
+                    hipLaunchKernelGGL(wf_tail_clds2<FEAT>, dim3(tgrid[0]), dim3(RTW_CLDS2_THREADS), clds, st, L, W, iters);
+                else if (y4)
+                    hipLaunchKernelGGL((wf_tail_clds<FEAT, true>), dim3(tgrid[0]), dim3(1024), clds, st, L, W, iters);
+                else
+                    hipLaunchKernelGGL((wf_tail_clds<FEAT, false>), dim3(tgrid[0]), dim3(1024), clds, st, L, W, iters);
                 done = true;
             }
         }
@@ -1732,7 +1794,7 @@ void wf_run(const rtw_launch& L, const rtw_wf& W0, hipStream_t st, int n_cu, rtw
     constexpr uint32_t clds_threads = 1024;  // one block per CU shares the stage (256 / 512: slower)
     if constexpr ((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING)) == 0) {
         if (clds && clds <= RTW_WF_CLDS_MAX) {
-            if (!clds_grid_cache[0] || clds_grid_cache[1] != clds) {
+            if (!clds_grid_cache[0] || clds_grid_cache[1] != clds) {  // (the Y4 forms: the same registers)
                 clds_grid_cache[0] = wf_grid(wf_trace_clds<FEAT>, n_cu, clds, clds_threads);
                 clds_grid_cache[2] = wf_grid(wf_trace_clds<FEAT, true>, n_cu, clds, clds_threads);
                 clds_grid_cache[1] = (uint32_t)clds;
@@ -1745,9 +1807,16 @@ void wf_run(const rtw_launch& L, const rtw_wf& W0, hipStream_t st, int n_cu, rtw
         RTW_TIME_BEGIN(T, RTW_K_TRACE)
         if constexpr ((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING)) == 0) {
             if (clds_grid) {
-                if (it == 0)
+                const bool y4 = L.n_orders == 4;
+                if (it == 0 && y4)
+                    hipLaunchKernelGGL((wf_trace_clds<FEAT, true, true>), dim3(clds_grid0), dim3(clds_threads), clds, st,
+                                       L, W, it);
+                else if (it == 0)
                     hipLaunchKernelGGL((wf_trace_clds<FEAT, true>), dim3(clds_grid0), dim3(clds_threads), clds, st, L,
                                        W, it);
+                else if (y4)
+                    hipLaunchKernelGGL((wf_trace_clds<FEAT, false, true>), dim3(clds_grid), dim3(clds_threads), clds, st,
+                                       L, W, it);
                 else
                     hipLaunchKernelGGL(wf_trace_clds<FEAT>, dim3(clds_grid), dim3(clds_threads), clds, st, L, W, it);
                 RTW_TIME_END(T)
@@ -1835,14 +1904,14 @@ void rtw_wavefront_batch(const rtw_launch& L, const rtw_wf& W, void* stream, int
 }
 
 uint32_t rtw_wavefront_max_waves(int n_cu) {
-    uint32_t m = rtw_wf_spheres_max_waves(n_cu);
+    uint32_t m = 0;
     auto mx = [&m](uint32_t a, uint32_t b) { m = std::max({m, a, b}); };
     mx(wf_grids<RTW_F_SPHERES>(n_cu).shade, wf_grids<RTW_F_SPHERES>(n_cu).shade0);
     mx(wf_grids<RTW_F_OBJECTS>(n_cu).shade, wf_grids<RTW_F_OBJECTS>(n_cu).shade0);
     mx(wf_grids<RTW_F_TEXTURED>(n_cu).shade, wf_grids<RTW_F_TEXTURED>(n_cu).shade0);
     mx(wf_grids<RTW_F_MEDIA>(n_cu).shade, wf_grids<RTW_F_MEDIA>(n_cu).shade0);
     mx(wf_grids<RTW_F_ALL>(n_cu).shade, wf_grids<RTW_F_ALL>(n_cu).shade0);
-    return 4 * m;
+    return std::max(4 * m, rtw_wf_spheres_max_waves(n_cu));
 }
 #else
 void rtw_wf_run_spheres(const rtw_launch& L, const rtw_wf& W, hipStream_t st, int n_cu, rtw_timer* T, uint32_t feat) {
@@ -1850,9 +1919,15 @@ void rtw_wf_run_spheres(const rtw_launch& L, const rtw_wf& W, hipStream_t st, in
     else wf_run<0u>(L, W, st, n_cu, T);
 }
 
+// (waves: the 256-thread shade grids and the compact-LDS kernels' grids, whichever launches more)
 uint32_t rtw_wf_spheres_max_waves(int n_cu) {
-    return std::max({wf_grids<0u>(n_cu).shade, wf_grids<0u>(n_cu).shade0, wf_grids<RTW_F_CHECKER>(n_cu).shade,
-                     wf_grids<RTW_F_CHECKER>(n_cu).shade0});
+    const uint32_t b = std::max({wf_grids<0u>(n_cu).shade, wf_grids<0u>(n_cu).shade0, wf_grids<RTW_F_CHECKER>(n_cu).shade,
+                                 wf_grids<RTW_F_CHECKER>(n_cu).shade0});
+    static const uint32_t c2 = std::max(wf_grid(wf_step_clds2<0u>, n_cu, 0, RTW_CLDS2_THREADS),
+                                        wf_grid(wf_step_clds2<RTW_F_CHECKER>, n_cu, 0, RTW_CLDS2_THREADS)) *
+                               (RTW_CLDS2_THREADS / 64u);
+    static const uint32_t c1 = std::max(wf_grid(wf_step_clds<0u>, n_cu, 0, 1024), wf_grid(wf_step_clds<RTW_F_CHECKER>, n_cu, 0, 1024)) * 16u;
+    return std::max({4u * b, c2, c1});
 }
 
 #if defined(RTW_DIAG_WALK)  // (the sphere-scene kernels' records and counters: this translation unit's)
