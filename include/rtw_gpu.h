@@ -315,7 +315,8 @@ typedef struct rtw_tuning {
                                   (4: copies ordered by the x and z signs, the walk takes y's near/far per ray;
                                   half the compact-LDS stage; ABI 7) */
     uint32_t sah_max_leaf;     /* spheres per SAH leaf (default 1) */
-    uint32_t compact_nodes;    /* 1 = 16-B fp16 node walk for static sphere SAH trees (default) */
+    uint32_t compact_nodes;    /* 1 = 16-B fp16 node walk for static sphere SAH trees (default); 2 = 32-B nodes
+                                  with fp32 boxes for packed FMAs, with bvh_orders 4 (else as 1; ABI 7) */
     uint32_t fast_box;         /* 1 = FMA slab test on the padded SAH boxes (default); 0 = aabb.zig arithmetic */
     uint32_t fast_reject;      /* 1 = exact sphere fast-reject filter (default) */
     uint32_t lds;              /* RTW_LDS_* (default RTW_LDS_ALL) */
@@ -345,9 +346,10 @@ typedef struct rtw_tuning {
                                   SAH tree, default 90; | RTW_OTREE_NO_CULL: instance and medium leaves do not
                                   test the instance's world box before its transforms and members (ABI 5,
                                   formerly padding) */
-    uint32_t clds_blocks;      /* compact-LDS kernels (fused step, tail) of a 4-copy tree: 0 = two blocks of 640
-                                  threads per CU when the stage fits half the LDS (5 waves per SIMD), 1 = one
-                                  1024-thread block; the 8-copy stage always runs one block (ABI 7) */
+    uint32_t clds_shape;       /* compact-LDS kernels (fused step, tail) of a 4-copy tree: 0 = auto, 1 = one
+                                  1024-thread block per CU, 2 / 3 / 4 = two blocks of 512 / 640 / 768 threads
+                                  (4 / 5 / 6 waves per SIMD) when the stage fits half the LDS; the 8-copy stage
+                                  always runs one block (ABI 7) */
 } rtw_tuning;
 
 void rtw_tuning_defaults(rtw_tuning* out);

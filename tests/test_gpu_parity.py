@@ -160,7 +160,9 @@ def test_four_copy_stage_full_c2(rtw, book1):
     arr, world = book1
     cam = rtw.book1_camera().init()
     ref = render_rows(rtw, world, cam, 0, 800, 0, 6, 2)
-    for tu in ({"bvh_orders": 4}, {"bvh_orders": 4, "clds_blocks": 1}, {"bvh_orders": 4, "fuse": 0}):
+    for tu in ({"bvh_orders": 4}, {"bvh_orders": 4, "clds_shape": 2}, {"bvh_orders": 4, "clds_shape": 3},
+               {"bvh_orders": 4, "clds_shape": 4}, {"bvh_orders": 4, "fuse": 0}, {"bvh_orders": 4, "compact_nodes": 2},
+               {"bvh_orders": 4, "compact_nodes": 2, "fuse": 0}):
         w = rtw.World(arr, tuning=tu)
         got = render_rows(rtw, w, cam, 0, 800, 0, 6, 2)
         w.close()
@@ -333,10 +335,14 @@ def test_v1_knobs_invariant(rtw, book1, knob):
                                   {"lds": 127 & ~2, "fuse": 5, "wide_walk": 0}, {"hoist": 0}, {"hoist": 0, "fuse": 0},
                                   {"sort_iters": 0}, {"sort_iters": 50}, {"sort_iters_split": 50, "fuse": 0}, {"sort_iters_split": 0, "fuse": 0},
                                   {"sort_iters": 2, "wf_iters": 1}, {"sort_bits": 0}, {"sort_bits": 2, "fuse": 0}, {"wf_iters": 3, "fuse": 0},
-                                  {"bvh_orders": 4}, {"bvh_orders": 4, "clds_blocks": 1}, {"bvh_orders": 4, "fuse": 0},
+                                  {"bvh_orders": 4}, {"bvh_orders": 4, "clds_shape": 3}, {"bvh_orders": 4, "fuse": 0},
                                   {"bvh_orders": 4, "lds": 127 & ~2}, {"bvh_orders": 4, "wide_walk": 0, "lds": 127 & ~2},
                                   {"bvh_orders": 4, "compact_nodes": 0}, {"bvh_orders": 4, "kernel": 1},
-                                  {"bvh_orders": 4, "kernel": 2}])
+                                  {"bvh_orders": 4, "kernel": 2}, {"bvh_orders": 4, "compact_nodes": 2},
+                                  {"bvh_orders": 4, "compact_nodes": 2, "fuse": 0},
+                                  {"bvh_orders": 4, "compact_nodes": 2, "lds": 127 & ~2},
+                                  {"bvh_orders": 4, "compact_nodes": 2, "tile_lists": 0},
+                                  {"bvh_orders": 8, "compact_nodes": 2}])
 def test_wavefront_knobs_invariant(rtw, book1, knob):
     """Wavefront tuning (rtw_tuning: bounces before the tail kernel, batch size ->
     many batches, FMA vs reference slab test, LDS-staged nodes, SAH leaf runs of up
@@ -368,7 +374,7 @@ def test_compact_nodes_are_exact(rtw, n, seed):
     outs = []
     for tu in ({"compact_nodes": 0, "tile_lists": 0, "hoist": 0}, {"compact_nodes": 1, "wide_walk": 0},
                {"compact_nodes": 1, "wide_walk": 1}, {"compact_nodes": 1, "wide_walk": 0, "hoist": 0},
-               {"compact_nodes": 1, "wide_walk": 0, "bvh_orders": 4}):
+               {"compact_nodes": 1, "wide_walk": 0, "bvh_orders": 4}, {"compact_nodes": 2, "bvh_orders": 4}):
         w = rtw.World(arr, tuning=tu)
         outs.append(render_rows(rtw, w, cam, 0, cam.derived.image_height, 0, 4, 6))
         w.close()
@@ -377,6 +383,7 @@ def test_compact_nodes_are_exact(rtw, n, seed):
     assert np.array_equal(outs[0], outs[2])  # the two-wide stack walk (rtw_wide2_nodes): same hits
     assert np.array_equal(outs[0], outs[3])  # the ground sphere inside the tree (no hoisting)
     assert np.array_equal(outs[0], outs[4])  # 4 (x, z)-sign copies, y near/far by med3 (traverse_compact<.., Y4>)
+    assert np.array_equal(outs[0], outs[5])  # their 32-B fp32-box form, packed FMAs (traverse_compact<.., F32>)
     # (the defaults also give camera rays the frustum-walked tile lists of large trees: same hits)
 
 

@@ -135,7 +135,7 @@ class RtwTuning(C.Structure):
                 ("wide_walk", C.c_uint32), ("wf_paths", C.c_uint64),
                 ("tile_lists", C.c_uint32), ("hoist", C.c_uint32), ("sort_iters", C.c_uint32),
                 ("sort_bits", C.c_uint32),
-                ("sort_iters_split", C.c_uint32), ("object_tree", C.c_uint32), ("clds_blocks", C.c_uint32)]
+                ("sort_iters_split", C.c_uint32), ("object_tree", C.c_uint32), ("clds_shape", C.c_uint32)]
 
 
 def tuning(**fields) -> RtwTuning:

@@ -778,10 +778,53 @@ uint16_t h_up(float x) {
 
 }  // namespace
 
-bool rtw_compact_nodes(const std::vector<rtw_node>& nodes, uint32_t orders, std::vector<rtw_cnode>& out) {
+// The 32-B fp32 form (fp32 = true, 4 copies only; rtw_tuning.compact_nodes 2): two uint4 per node, the
+// padded fp32 box of the 32-B array itself (the box_next fast test's operands: no rounding outward needed)
+// laid out for packed FMAs -- v_pk_fma_f32 does two of the slab test's FMAs in the time v_fma_mix_f32 does one:
+//   inner: (near x, min y, far x, max y), (near z, far z, skip, 0)   near / far by the copy's x and z signs;
+//          skip = the target's byte offset from the array start (32 B per node)
+//   leaf:  (center.xyz, bits(radius * radius)), (0, 0, RTW_LEAF_BIT, 0)
+bool rtw_compact_nodes(const std::vector<rtw_node>& nodes, uint32_t orders, std::vector<rtw_cnode>& out, bool fp32) {
     // one copy per ray-direction octant, or (orders = 4) per sign pair of x and z
-    if ((orders != 8 && orders != 4) || nodes.size() % orders) return false;
+    if ((orders != 8 && orders != 4) || nodes.size() % orders || (fp32 && orders != 4)) return false;
     const size_t per = nodes.size() / orders;
+    if (fp32) {
+        out.assign(2 * nodes.size(), rtw_cnode{});
+        auto fb = [](float f) {
+            uint32_t b;
+            std::memcpy(&b, &f, 4);
+            return b;
+        };
+        for (size_t i = 0; i < nodes.size(); i++) {
+            const uint32_t oct = (uint32_t)(i / per);
+            const rtw_node& n = nodes[i];
+            rtw_cnode& c0 = out[2 * i];
+            rtw_cnode& c1 = out[2 * i + 1];
+            uint32_t w;
+            std::memcpy(&w, &n.a[3], 4);
+            if (w & RTW_LEAF_BIT) {
+                const float rr = n.b[0] * n.b[0];  // objects.zig:126, as the 16-B form
+                if (!(rr >= 0) || !std::isfinite(rr)) return false;
+                std::memcpy(&c0.v[0], &n.a[0], 12);
+                c0.v[3] = fb(rr);
+                c1.v[2] = RTW_LEAF_BIT;
+                continue;
+            }
+            for (int k = 0; k < 3; k++)
+                if (!std::isfinite(n.a[k]) || !std::isfinite(n.b[k])) return false;
+            const bool nx = oct & 1u, nz = (oct >> 1) & 1u;
+            c0.v[0] = fb(nx ? n.b[0] : n.a[0]);
+            c0.v[1] = fb(n.a[1]);
+            c0.v[2] = fb(nx ? n.a[0] : n.b[0]);
+            c0.v[3] = fb(n.b[1]);
+            c1.v[0] = fb(nz ? n.b[2] : n.a[2]);
+            c1.v[1] = fb(nz ? n.a[2] : n.b[2]);
+            const uint64_t skip_bytes = ((uint64_t)oct * per + (w & RTW_SKIP_MASK)) * 32u;
+            if (skip_bytes >= RTW_LEAF_BIT) return false;
+            c1.v[2] = (uint32_t)skip_bytes;
+        }
+        return true;
+    }
     out.resize(nodes.size());
     for (size_t i = 0; i < nodes.size(); i++) {
         const uint32_t oct = (uint32_t)(i / per);  // order_of: bit k set = negative direction on axis k

@@ -905,9 +905,16 @@ RTW_DHD uint32_t lds_addr(const void* p) {
 // exactly when lo < hi (lo' <= lo and hi' >= hi; if lo > max(ta, tb) then hi' <= max(ta, tb) = lo', and if
 // hi < min(ta, tb) then lo' >= min(ta, tb) = hi').  Four min/max-class instructions per box, as the 8-copy
 // walk's max3 + max and min3 + min: the same test at the same cost, with half the stage.
-template <bool COUNT, bool LDS = false, bool Y4 = false>
+// F32 (with Y4; rtw_compact_nodes fp32): 32-B nodes with the padded fp32 boxes -- the x pair (near, far) and
+// the y pair (min, max) sit in the first uint4 as (x near, y min, x far, y max), so two v_pk_fma_f32 give
+// (tnx, ty0) and (tfx, ty1) with the ray's (inv.x, inv.y) / (oinv.x, oinv.y) register pairs, and z's two FMAs
+// pair up on their own: the box step's six FMAs cost 4 + 4 + 2 x 2 clocks instead of six 4-clock
+// v_fma_mix_f32 (profiles/r4_valu_peak/).  The same t = fma(P, inv, -o * inv) on the same fp32 boxes as
+// box_next's fast test: the same visits as the 32-B walk of those boxes, a subset of the fp16 walk's.
+template <bool COUNT, bool LDS = false, bool Y4 = false, bool F32 = false>
 RTW_DHD int traverse_compact(const rtw_launch& L, const uint4* base, const Ray& r, float& t_out,
                                                 Counters& cnt) {
+    static_assert(!F32 || Y4, "the fp32 nodes are the 4-copy layout");
     const uint32_t oct = order_of(L, r);
     const char* __restrict__ cb = reinterpret_cast<const char*>(base);
     uint32_t a_base = 0;  // LDS: the stage's LDS address
@@ -929,8 +936,64 @@ RTW_DHD int traverse_compact(const rtw_launch& L, const uint4* base, const Ray& 
     rt.oinv = mk(-(r.o.x * rt.inv.x), -(r.o.y * rt.inv.y), -(r.o.z * rt.inv.z));
     float closest = kInf;
     int hit = -1;  // the byte offset of the closest sphere's node
-    const uint32_t a0 = a_base + oct * L.n_nodes * 16u, end = a0 + L.n_nodes * 16u;
+    constexpr uint32_t NB = F32 ? 32u : 16u;  // bytes per node
+    const uint32_t a0 = a_base + oct * L.n_nodes * NB, end = a0 + L.n_nodes * NB;
     uint32_t i = a0;
+    if constexpr (F32) {
+#if defined(__HIP_DEVICE_COMPILE__)
+        typedef float f2v __attribute__((ext_vector_type(2)));
+#else
+        struct f2v { float x, y; };
+#endif
+        const f2v inv_xy = {rt.inv.x, rt.inv.y}, oinv_xy = {rt.oinv.x, rt.oinv.y};
+        while (i < end) {
+            uint4 c0, c1;
+#if defined(__HIP_DEVICE_COMPILE__)
+            if constexpr (LDS) {
+                c0 = *(lds_uint4*)(uintptr_t)i;
+                c1 = *(lds_uint4*)(uintptr_t)(i + 16u);
+            } else
+#endif
+            {
+                c0 = *reinterpret_cast<const uint4*>(cb + i);
+                c1 = *reinterpret_cast<const uint4*>(cb + i + 16u);
+            }
+#if defined(__HIP_DEVICE_COMPILE__)
+            // both halves in one round trip: left to itself the compiler reads z's pair inside the box branch,
+            // a second dependent LDS latency on every inner step
+            asm volatile("" ::"v"(c1.x), "v"(c1.y), "v"(c1.z));
+#endif
+            if (c1.z & RTW_LEAF_BIT) {
+                if constexpr (COUNT) cnt.leaves++;
+                sphere_leaf(L, r, rt, mk(ubits(c0.x), ubits(c0.y), ubits(c0.z)), ubits(c0.w), i, closest, hit);
+                i += 32u;
+            } else {
+                if constexpr (COUNT) cnt.nodes++;
+                float tnx, ty0, tfx, ty1;
+#if defined(__HIP_DEVICE_COMPILE__)
+                const f2v pn = {ubits(c0.x), ubits(c0.y)}, pf = {ubits(c0.z), ubits(c0.w)};
+                const f2v tn = __builtin_elementwise_fma(pn, inv_xy, oinv_xy);
+                const f2v tf = __builtin_elementwise_fma(pf, inv_xy, oinv_xy);
+                tnx = tn.x;
+                ty0 = tn.y;
+                tfx = tf.x;
+                ty1 = tf.y;
+#else
+                tnx = std::fma(ubits(c0.x), inv_xy.x, oinv_xy.x);
+                ty0 = std::fma(ubits(c0.y), inv_xy.y, oinv_xy.y);
+                tfx = std::fma(ubits(c0.z), inv_xy.x, oinv_xy.x);
+                ty1 = std::fma(ubits(c0.w), inv_xy.y, oinv_xy.y);
+#endif
+                const float tnz = __builtin_fmaf(ubits(c1.x), rt.inv.z, rt.oinv.z);
+                const float tfz = __builtin_fmaf(ubits(c1.y), rt.inv.z, rt.oinv.z);
+                const float lo = med3f(__builtin_fmaxf(__builtin_fmaxf(kTmin, tnx), tnz), ty0, ty1);
+                const float hi = med3f(__builtin_fminf(__builtin_fminf(closest, tfx), tfz), ty0, ty1);
+                i = (hi <= lo) ? c1.z : i + 32u;
+            }
+        }
+        t_out = closest;
+        return hit_with_order(hit < 0 ? hit : (int)(((uint32_t)hit - a0) >> 5), oct);
+    }
 #if defined(RTW_DIAG_WALK) && defined(__HIP_DEVICE_COMPILE__)
     WalkDiag dgv;
     WalkDiag* dg = &dgv;
@@ -1066,6 +1129,9 @@ RTW_DHD int traverse(const float4* __restrict__ nodes, const rtw_launch& L, cons
                                         float& t_out, Counters& cnt, uint64_t mkey = 0) {
     if constexpr (COMPACT && (FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING)) == 0) {
         if (L.cnodes && L.fast_box) {  // per-step counters only in counted passes
+            if (L.cnode32)
+                return L.counters ? traverse_compact<true, false, true, true>(L, L.cnodes, r, t_out, cnt)
+                                  : traverse_compact<false, false, true, true>(L, L.cnodes, r, t_out, cnt);
             if (L.n_orders == 4)
                 return L.counters ? traverse_compact<true, false, true>(L, L.cnodes, r, t_out, cnt)
                                   : traverse_compact<false, false, true>(L, L.cnodes, r, t_out, cnt);

@@ -176,7 +176,7 @@ int rtw_scene_create_ex(const rtw_scene_desc* d, int device, const rtw_tuning* t
     if (tu.kernel > RTW_KERNEL_SIMPLE) return fail(RTW_E_INVALID, "tuning.kernel out of range");
     if (tu.bvh_orders != 0 && tu.bvh_orders != 1 && tu.bvh_orders != 4 && tu.bvh_orders != 8)
         return fail(RTW_E_INVALID, "tuning.bvh_orders must be 0, 1, 4 or 8");
-    if (tu.clds_blocks > 2) return fail(RTW_E_INVALID, "tuning.clds_blocks must be 0, 1 or 2");
+    if (tu.clds_shape > 4) return fail(RTW_E_INVALID, "tuning.clds_shape must be 0..4");
     if (tu.wf_iters < 1 || tu.wf_iters > RTW_WF_MAX_ITERS) return fail(RTW_E_INVALID, "tuning.wf_iters out of range");
     if ((tu.object_tree & 0xFFu) > 100 || (tu.object_tree & ~(0xFFu | RTW_OTREE_NO_CULL)))
         return fail(RTW_E_INVALID, "tuning.object_tree: 0..100 [| RTW_OTREE_NO_CULL]");
@@ -240,16 +240,19 @@ int rtw_scene_create_ex(const rtw_scene_desc* d, int device, const rtw_tuning* t
     const std::vector<float>& cvec = geom.cvec;
     // compact 16-B walk for static sphere SAH trees (rtw_compact_nodes)
     std::vector<rtw_cnode> cnodes;
+    bool cnode32 = false;
     {
         bool want = d->bvh_mode == RTW_BVH_SAH && !objects && ctx->box_pad > 0 && tu.compact_nodes && !host;
         for (uint32_t i = 0; want && i < d->n_spheres; i++) want = !d->spheres[i].is_moving;
-        if (want && !rtw_compact_nodes(ctx->nodes_host, orders, cnodes)) cnodes.clear();
+        // compact_nodes 2: the 32-B fp32-box form where it applies (4 copies), else the 16-B fp16 form
+        cnode32 = want && tu.compact_nodes == 2 && orders == 4 && rtw_compact_nodes(ctx->nodes_host, orders, cnodes, true);
+        if (want && !cnode32 && !rtw_compact_nodes(ctx->nodes_host, orders, cnodes)) cnodes.clear();
     }
     // two-wide records for the stack walk of trees read through L1/L2 (rtw_wide2_nodes)
     std::vector<rtw_cnode> w2;
     std::vector<uint32_t> w2leaf;
     uint32_t w2_stack = 0;
-    if (!cnodes.empty() && tu.wide_walk && tu.sah_max_leaf <= 1 &&
+    if (!cnodes.empty() && !cnode32 && tu.wide_walk && tu.sah_max_leaf <= 1 &&
         !rtw_wide2_nodes(ctx->nodes_host, (uint32_t)(ctx->nodes_host.size() / orders), w2, w2leaf, &w2_stack))
         w2.clear();
     if (w2_stack > RTW_W2_STACK_MAX) w2.clear();
@@ -391,7 +394,8 @@ int rtw_scene_create_ex(const rtw_scene_desc* d, int device, const rtw_tuning* t
     L.images = dev + o_imgs;
     L.n_nodes = (uint32_t)n_nodes;
     L.n_orders = orders;
-    L.clds_blocks = tu.clds_blocks;
+    L.clds_shape = tu.clds_shape;
+    L.cnode32 = cnode32 ? 1u : 0u;
     L.n_perlin = d->n_perlins;
     ctx->feat = scene_features(d) | geom.feat;
     L.feat = ctx->feat;

@@ -19,7 +19,8 @@ struct rtw_scene_desc;
 struct rtw_launch {
     // scene (device pointers)
     const float4* nodes;
-    const uint4* cnodes;         // compact 16-B copy of `nodes` (static sphere SAH trees) or null
+    const uint4* cnodes;         // compact 16-B copy of `nodes` (static sphere SAH trees) or null; with cnode32
+                                 // the 32-B fp32-box form (two uint4 per node, 4-copy trees)
     const uint4* w2nodes;        // two-wide records of ordering 0 (rtw_wide2_nodes) or null
     const uint32_t* w2leaf;      // their leaf slots' hit ids (ordering-0 leaf index)
     const float4* cvec;          // per-sphere center_vec (moving spheres)
@@ -70,7 +71,9 @@ struct rtw_launch {
     uint32_t inst_cull;          // 1 = instance / medium leaves test the instance's padded world box first
                                  // (only with fast_box; rtw_tuning.object_tree without RTW_OTREE_NO_CULL)
     uint32_t n_orders;           // 1, or 4 / 8 sign-ordered copies of the node array (SAH sphere scenes)
-    uint32_t clds_blocks;        // compact-LDS kernels of a 4-copy tree: 0 = two blocks per CU when they fit, 1 = one
+    uint32_t cnode32;            // 1: cnodes are the 32-B fp32-box nodes (rtw_tuning.compact_nodes 2)
+    uint32_t clds_shape;         // compact-LDS kernels of a 4-copy tree: 0 / 1 = one 1024-thread block per CU,
+                                 // 2 / 3 / 4 = two blocks of 512 / 640 / 768 threads (rtw_tuning.clds_shape)
     uint32_t wf_lds;             // wavefront trace: stage the node array(s) in LDS when they fit
     uint32_t wf_clds;            // wavefront trace: stage the compact nodes (all orders) in LDS when they fit
     uint32_t wf_fuse;            // with the compact LDS stage: one gen+trace+shade kernel per iteration,
@@ -181,8 +184,10 @@ struct rtw_geometry {
 struct rtw_cnode {
     uint32_t v[4];
 };
-// false: the tree cannot be encoded (coordinates beyond fp16 range, non-finite radius)
-bool rtw_compact_nodes(const std::vector<rtw_node>& nodes, uint32_t orders, std::vector<rtw_cnode>& out);
+// false: the tree cannot be encoded (coordinates beyond fp16 range, non-finite radius).
+// fp32 (4 copies only): 32-B nodes with fp32 boxes instead (2 rtw_cnode per node; rtw_compact_nodes)
+bool rtw_compact_nodes(const std::vector<rtw_node>& nodes, uint32_t orders, std::vector<rtw_cnode>& out,
+                       bool fp32 = false);
 
 // two-wide 32-B records (2 x rtw_cnode per inner node) of ordering 0 for the stack walk of large static
 // sphere SAH trees (rtw_bvh.hip rtw_wide2_nodes); false: not encodable (leaf runs, fp16 range)

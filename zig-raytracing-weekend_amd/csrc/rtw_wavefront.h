@@ -14,7 +14,6 @@
 #define RTW_TL_MAX 64          // camera-ray candidate list capacity per 8x8 tile (rtw_tuning.tile_lists caps it)
 #define RTW_TL_WALK 0xFFFFFFFFu
 #define RTW_TL_BYTES (RTW_TL_MAX * 32 + 4)  // per tile
-#define RTW_CLDS2_THREADS 640   // two-block compact-LDS kernels: 2 x 10 waves per CU = 5 waves per SIMD
 #define RTW_WF_CLDS2_MAX (80u * 1024u)  // their stage (+ materials) per block: half the CU's LDS
 #define RTW_W2_STACK_MAX 32   // deepest per-lane LDS stack of the two-wide walk (256 threads x 32 x 4 B = 32 KiB)
 

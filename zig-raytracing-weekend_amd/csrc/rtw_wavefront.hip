@@ -494,14 +494,34 @@ __device__ __forceinline__ rtw_launch stage_geom(const rtw_launch& L, float4* ld
     return G;
 }
 
-// every octant copy of the compact nodes into this block's LDS, inner nodes' skip offsets rebased to
+// The compact node forms a walk can read (traverse_compact):
+//   CN_F16_8  16-B nodes, fp16 boxes, 8 octant copies (the default)
+//   CN_F16_4  16-B nodes, fp16 boxes, 4 copies by the x and z signs (y slabs by med3)
+//   CN_F32_4  32-B nodes, fp32 boxes for packed FMAs, 4 copies (rtw_tuning.compact_nodes 2)
+enum { CN_F16_8 = 0, CN_F16_4 = 1, CN_F32_4 = 2 };
+// uint4s per node of the launch's compact form
+__device__ __forceinline__ uint32_t cn_quads(const rtw_launch& L) { return L.cnode32 ? 2u : 1u; }
+template <bool COUNT, bool LDS, int CN>
+__device__ __forceinline__ int walk_compact(const rtw_launch& L, const uint4* base, const Ray& r, float& t, Counters& cnt) {
+    return traverse_compact<COUNT, LDS, CN != CN_F16_8, CN == CN_F32_4>(L, base, r, t, cnt);
+}
+
+// every copy of the compact nodes into this block's LDS, inner nodes' skip offsets rebased to
 // absolute LDS addresses (traverse_compact<.., true> steps through them as they are)
 __device__ __forceinline__ void stage_clds(const rtw_launch& L, uint4* lds) {
-    const uint32_t n4 = L.n_nodes * L.n_orders, lb = lds_addr(lds);
-    for (uint32_t k = threadIdx.x; k < n4; k += blockDim.x) {
-        uint4 c = L.cnodes[k];
-        if (!(c.w & RTW_LEAF_BIT)) c.w += lb;
-        lds[k] = c;
+    const uint32_t n4 = L.n_nodes * L.n_orders * cn_quads(L), lb = lds_addr(lds);
+    if (L.cnode32) {  // the skip / leaf word is the second uint4's z
+        for (uint32_t k = threadIdx.x; k < n4; k += blockDim.x) {
+            uint4 c = L.cnodes[k];
+            if ((k & 1u) && !(c.z & RTW_LEAF_BIT)) c.z += lb;
+            lds[k] = c;
+        }
+    } else {
+        for (uint32_t k = threadIdx.x; k < n4; k += blockDim.x) {
+            uint4 c = L.cnodes[k];
+            if (!(c.w & RTW_LEAF_BIT)) c.w += lb;
+            lds[k] = c;
+        }
     }
     __syncthreads();
 }
@@ -725,8 +745,9 @@ __global__ __launch_bounds__(64) void wf_tile_lists(rtw_launch L, rtw_wf W) {
         bool cand = false;
         float tlow = 0.0f;
         if (k < L.n_nodes) {
-            const uint4 c = L.cnodes[k];  // ordering 0
-            if (c.w & RTW_LEAF_BIT)
+            const uint4 c = L.cnodes[k * cn_quads(L)];  // ordering 0 (the 32-B form: leaf flag in the second uint4)
+            const bool leaf = L.cnode32 ? (L.cnodes[2u * k + 1u].z & RTW_LEAF_BIT) != 0 : (c.w & RTW_LEAF_BIT) != 0;
+            if (leaf)
                 cand = tile_reach(F, mk(ubits(c.x), ubits(c.y), ubits(c.z)), __builtin_sqrtf(ubits(c.w & ~RTW_LEAF_BIT)),
                                   tlow);
         }
@@ -926,7 +947,7 @@ __global__ __launch_bounds__(256) void wf_trace(rtw_launch L, rtw_wf W, uint32_t
 // trace over the compact nodes staged in LDS (all octant copies of a small tree,
 // e.g. BASELINE config 2: 8 x 969 x 16 B = 124 KB): 1024-thread blocks share one
 // copy (one block per CU), ds_read_b128 instead of vector-memory gathers
-template <uint32_t FEAT, bool CAM = false, bool Y4 = false>
+template <uint32_t FEAT, bool CAM = false, int CN = CN_F16_8>
 __global__ __launch_bounds__(1024) void wf_trace_clds(rtw_launch L, rtw_wf W, uint32_t it) {
     static_assert((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING)) == 0, "static sphere scenes");
     if (blockIdx.x == 0 && threadIdx.x < RTW_WF_STRIPES) W.len[(it + 1u) % 3u][threadIdx.x * RTW_WF_LEN_STRIDE] = 0;
@@ -943,8 +964,8 @@ __global__ __launch_bounds__(1024) void wf_trace_clds(rtw_launch L, rtw_wf W, ui
             const Ray r = wf_input_ray<FEAT, CAM>(L, W, S, slot, it, depth, rng, txy, true);
             if (depth) {
                 float t;
-                const int h = L.counters ? traverse_compact<true, true, Y4>(L, wf_clds, r, t, cnt)
-                                         : traverse_compact<false, true, Y4>(L, wf_clds, r, t, cnt);
+                const int h = L.counters ? walk_compact<true, true, CN>(L, wf_clds, r, t, cnt)
+                                         : walk_compact<false, true, CN>(L, wf_clds, r, t, cnt);
                 W.hit[slot] = make_float2(t, __int_as_float(h));
                 cnt.rays++;
             }
@@ -1046,7 +1067,7 @@ __device__ __forceinline__ void wf_shade_body(const rtw_launch& L, const rtw_wf&
 // tail: the paths still queued after the last wavefront iteration, each to
 // completion; a lane whose path ends takes the wave's next path at once.
 // CLDS: the walk reads the compact nodes staged in LDS (`lds`) instead of L1/L2.
-template <uint32_t FEAT, bool CLDS, bool Y4 = false>
+template <uint32_t FEAT, bool CLDS, int CN = CN_F16_8>
 __device__ __forceinline__ void wf_tail_body(const rtw_launch& L, const rtw_wf& W, uint32_t it, const uint4* lds,
                                              const float4* nodes = nullptr) {
     const uint32_t lane = __lane_id();
@@ -1091,8 +1112,8 @@ __device__ __forceinline__ void wf_tail_body(const rtw_launch& L, const rtw_wf& 
             float t;
             int hit;
             if constexpr (CLDS)
-                hit = L.counters ? traverse_compact<true, true, Y4>(L, lds, r, t, cnt)
-                                 : traverse_compact<false, true, Y4>(L, lds, r, t, cnt);
+                hit = L.counters ? walk_compact<true, true, CN>(L, lds, r, t, cnt)
+                                 : walk_compact<false, true, CN>(L, lds, r, t, cnt);
             else
                 hit = nodes ? traverse<FEAT, false>(nodes, L, r, t, cnt, rng.s)  // the LDS stage
                             : wf_traverse_global<FEAT>(L, r, t, cnt, rng.s);
@@ -1220,21 +1241,21 @@ __global__ __launch_bounds__(256) void wf_tail_lds(rtw_launch L, rtw_wf W, uint3
 }
 
 
-template <uint32_t FEAT, bool Y4 = false>
+template <uint32_t FEAT, int CN = CN_F16_8>
 __global__ __launch_bounds__(1024) void wf_tail_clds(rtw_launch L, rtw_wf W, uint32_t it) {
     static_assert((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING)) == 0, "static sphere scenes");
     extern __shared__ uint4 wf_clds[];
     stage_clds(L, wf_clds);
-    wf_tail_body<FEAT, true, Y4>(L, W, it, wf_clds);
+    wf_tail_body<FEAT, true, CN>(L, W, it, wf_clds);
 }
-// the 4-copy stage (half the LDS) at two blocks per CU: 2 x 640 threads = 5 waves per SIMD (<= 96 VGPRs)
-template <uint32_t FEAT>
-__global__ __launch_bounds__(RTW_CLDS2_THREADS) __attribute__((amdgpu_waves_per_eu(5)))
+// the 4-copy stage (half the LDS) at two blocks of T threads per CU: 2T / 256 waves per SIMD
+template <uint32_t FEAT, uint32_t T>
+__global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(2 * T / 256)))
 void wf_tail_clds2(rtw_launch L, rtw_wf W, uint32_t it) {
     static_assert((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING)) == 0, "static sphere scenes");
     extern __shared__ uint4 wf_clds[];
     stage_clds(L, wf_clds);
-    wf_tail_body<FEAT, true, true>(L, W, it, wf_clds);
+    wf_tail_body<FEAT, true, CN_F16_4>(L, W, it, wf_clds);
 }
 
 // Where the fused step's walk reads the tree:
@@ -1242,16 +1263,18 @@ void wf_tail_clds2(rtw_launch L, rtw_wf W, uint32_t it) {
 //   WALK_LDS    the 32-B node array of one ordering staged in LDS (small object scenes: Cornell)
 //   WALK_GLOBAL L.cnodes / L.nodes through L1/L2 (large trees: C4)
 //   WALK_CLDS4  the compact nodes of the 4 (x, z)-sign copies staged in LDS (traverse_compact<.., Y4>)
-enum { WALK_CLDS = 0, WALK_LDS = 1, WALK_GLOBAL = 2, WALK_CLDS4 = 3 };
+//   WALK_CLDS32 the 32-B fp32-box nodes of the 4 copies staged in LDS (traverse_compact<.., Y4, F32>)
+enum { WALK_CLDS = 0, WALK_LDS = 1, WALK_GLOBAL = 2, WALK_CLDS4 = 3, WALK_CLDS32 = 4 };
+template <int WALK>
+constexpr int walk_cn() { return WALK == WALK_CLDS32 ? CN_F32_4 : WALK == WALK_CLDS4 ? CN_F16_4 : CN_F16_8; }
 
 template <uint32_t FEAT, int WALK>
 __device__ __forceinline__ int wf_walk(const rtw_launch& L, const void* lds, const Ray& r, float& t, Counters& cnt,
                                        uint64_t mkey) {
-    if constexpr (WALK == WALK_CLDS || WALK == WALK_CLDS4) {
-        constexpr bool Y4 = WALK == WALK_CLDS4;
+    if constexpr (WALK == WALK_CLDS || WALK == WALK_CLDS4 || WALK == WALK_CLDS32) {
         const uint4* cn = static_cast<const uint4*>(lds);
-        return L.counters ? traverse_compact<true, true, Y4>(L, cn, r, t, cnt)
-                          : traverse_compact<false, true, Y4>(L, cn, r, t, cnt);
+        return L.counters ? walk_compact<true, true, walk_cn<WALK>()>(L, cn, r, t, cnt)
+                          : walk_compact<false, true, walk_cn<WALK>()>(L, cn, r, t, cnt);
     } else if constexpr (WALK == WALK_LDS) {
         return traverse<FEAT, false>(static_cast<const float4*>(lds), L, r, t, cnt, mkey);  // the LDS stage
     } else {
@@ -1409,7 +1432,7 @@ __device__ __forceinline__ void wf_step_clds_body(const rtw_launch& L, const rtw
     extern __shared__ uint4 wf_clds[];
     stage_clds(L, wf_clds);
     if (L.mat_lds) {  // the materials after the nodes (the host checked that they fit)
-        uint4* ml = wf_clds + L.n_nodes * L.n_orders;
+        uint4* ml = wf_clds + L.n_nodes * L.n_orders * cn_quads(L);
         const uint4* src = reinterpret_cast<const uint4*>(L.mats);
         for (uint32_t k = threadIdx.x; k < L.mat_lds / 16u; k += blockDim.x) ml[k] = src[k];
         __syncthreads();
@@ -1422,7 +1445,7 @@ __device__ __forceinline__ void wf_step_clds_body(const rtw_launch& L, const rtw
 }
 
 // one 1024-thread block per CU (the 8-copy stage, 124 KB for C2, allows no second block)
-template <uint32_t FEAT, bool Y4 = false>
+template <uint32_t FEAT, int CN = CN_F16_8>
 __global__ __launch_bounds__(1024) void wf_step_clds(rtw_launch L, rtw_wf W, uint32_t it) {
     static_assert((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING)) == 0, "static sphere scenes");
 #if defined(RTW_SETPRIO)
@@ -1433,15 +1456,16 @@ __global__ __launch_bounds__(1024) void wf_step_clds(rtw_launch L, rtw_wf W, uin
         else if (pr == 3u) __builtin_amdgcn_s_setprio(3);
     }
 #endif
-    wf_step_clds_body<FEAT, Y4 ? WALK_CLDS4 : WALK_CLDS>(L, W, it);
+    wf_step_clds_body<FEAT, CN == CN_F32_4 ? WALK_CLDS32 : CN == CN_F16_4 ? WALK_CLDS4 : WALK_CLDS>(L, W, it);
 }
 
-// The 4-copy stage (C2: 62 KB + 15.5 KB of materials) at two blocks per CU: 2 x 640 threads = 5 waves
-// per SIMD instead of 4, register-capped at 96 VGPRs (MI355X_MICROARCH.md: 88-96 allocated -> 5 waves).
+// The 4-copy stage (C2: 62 KB + 15.5 KB of materials) at two blocks per CU (rtw_tuning.clds_shape): 2 x 512
+// threads (4 waves per SIMD, as one 1024-thread block), 2 x 640 (5 waves, <= 96 VGPRs) or 2 x 768 (6 waves,
+// <= 80 VGPRs; MI355X_MICROARCH.md: 88-96 allocated -> 5 waves, 80 -> 6).
 // The fused step waits on its dependent ds_read_b128 41 % of the cycles at 4 waves (profiles/r4_stall/):
 // a fifth wave per SIMD has more ready work to issue in those waits.
-template <uint32_t FEAT>
-__global__ __launch_bounds__(RTW_CLDS2_THREADS) __attribute__((amdgpu_waves_per_eu(5)))
+template <uint32_t FEAT, uint32_t T>
+__global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(2 * T / 256)))
 void wf_step_clds2(rtw_launch L, rtw_wf W, uint32_t it) {
     static_assert((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING)) == 0, "static sphere scenes");
     wf_step_clds_body<FEAT, WALK_CLDS4>(L, W, it);
@@ -1653,23 +1677,35 @@ void wf_run_fused(const rtw_launch& L, const rtw_wf& W0, hipStream_t st, int n_c
     thread_local uint32_t cgrid[2] = {0, 0}, tgrid[2] = {0, 0}, lgrid[2] = {0, 0}, ggrid[2] = {0, 0}, wtail[2] = {0, 0};
     uint32_t grid = 0;
     // The compact stage's block shape: the 8-copy stage (C2: 124 KB) leaves room for one 1024-thread block
-    // per CU; the 4-copy stage (L.n_orders == 4, 62 KB) for two blocks of RTW_CLDS2_THREADS (5 waves per SIMD)
-    // when it fits half the LDS (rtw_tuning.clds_blocks: 0 = so, 1 = one 1024-thread block)
-    const bool y4 = L.n_orders == 4, two = clds && y4 && L.clds_blocks != 1 && cdyn0 <= RTW_WF_CLDS2_MAX;
+    // per CU; the 4-copy stage (L.n_orders == 4, 62 KB) for two blocks (rtw_tuning.clds_shape 2..4: of 512,
+    // 640 or 768 threads) when it fits half the LDS
+    const bool y4 = L.n_orders == 4;
+    const int cn = L.cnode32 ? CN_F32_4 : y4 ? CN_F16_4 : CN_F16_8;
+    const uint32_t shape = clds && cn == CN_F16_4 && cdyn0 <= RTW_WF_CLDS2_MAX && L.clds_shape >= 2 ? L.clds_shape : 1u;
+    const bool two = shape >= 2;
     const size_t cdyn2 = two && cdyn > RTW_WF_CLDS2_MAX ? cdyn0 : cdyn;  // materials only if they fit too
-    const uint32_t cthreads = two ? RTW_CLDS2_THREADS : 1024u;
+    const uint32_t cthreads = shape == 2 ? 512u : shape == 3 ? 640u : shape == 4 ? 768u : 1024u;
     if constexpr ((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING)) == 0) {
-        const uint32_t key = (uint32_t)cdyn2 | (two ? 0x80000000u : 0u) | (y4 ? 0x40000000u : 0u);
+        const uint32_t key = (uint32_t)cdyn2 | (shape << 24) | ((uint32_t)cn << 28);
         if (clds && cgrid[1] != key) {
-            if (two) {
-                cgrid[0] = wf_grid(wf_step_clds2<FEAT>, n_cu, cdyn2, RTW_CLDS2_THREADS);
-                tgrid[0] = wf_grid(wf_tail_clds2<FEAT>, n_cu, clds, RTW_CLDS2_THREADS);
-            } else if (y4) {
-                cgrid[0] = wf_grid(wf_step_clds<FEAT, true>, n_cu, cdyn2, 1024);
-                tgrid[0] = wf_grid(wf_tail_clds<FEAT, true>, n_cu, clds, 1024);
+            if (shape == 2) {
+                cgrid[0] = wf_grid(wf_step_clds2<FEAT, 512>, n_cu, cdyn2, 512);
+                tgrid[0] = wf_grid(wf_tail_clds2<FEAT, 512>, n_cu, clds, 512);
+            } else if (shape == 3) {
+                cgrid[0] = wf_grid(wf_step_clds2<FEAT, 640>, n_cu, cdyn2, 640);
+                tgrid[0] = wf_grid(wf_tail_clds2<FEAT, 640>, n_cu, clds, 640);
+            } else if (shape == 4) {
+                cgrid[0] = wf_grid(wf_step_clds2<FEAT, 768>, n_cu, cdyn2, 768);
+                tgrid[0] = wf_grid(wf_tail_clds2<FEAT, 768>, n_cu, clds, 768);
+            } else if (cn == CN_F32_4) {
+                cgrid[0] = wf_grid(wf_step_clds<FEAT, CN_F32_4>, n_cu, cdyn2, 1024);
+                tgrid[0] = wf_grid(wf_tail_clds<FEAT, CN_F32_4>, n_cu, clds, 1024);
+            } else if (cn == CN_F16_4) {
+                cgrid[0] = wf_grid(wf_step_clds<FEAT, CN_F16_4>, n_cu, cdyn2, 1024);
+                tgrid[0] = wf_grid(wf_tail_clds<FEAT, CN_F16_4>, n_cu, clds, 1024);
             } else {
-                cgrid[0] = wf_grid(wf_step_clds<FEAT, false>, n_cu, cdyn2, 1024);
-                tgrid[0] = wf_grid(wf_tail_clds<FEAT, false>, n_cu, clds, 1024);
+                cgrid[0] = wf_grid(wf_step_clds<FEAT, CN_F16_8>, n_cu, cdyn2, 1024);
+                tgrid[0] = wf_grid(wf_tail_clds<FEAT, CN_F16_8>, n_cu, clds, 1024);
             }
             cgrid[1] = tgrid[1] = key;
         }
@@ -1703,12 +1739,18 @@ void wf_run_fused(const rtw_launch& L, const rtw_wf& W0, hipStream_t st, int n_c
             if (clds) {
                 rtw_launch Lc = L;  // the materials are staged only when they fit
                 if (cdyn2 == cdyn0) Lc.mat_lds = 0;
-                if (two)
-                    hipLaunchKernelGGL(wf_step_clds2<FEAT>, dim3(grid), dim3(RTW_CLDS2_THREADS), cdyn2, st, Lc, Wt, it);
-                else if (y4)
-                    hipLaunchKernelGGL((wf_step_clds<FEAT, true>), dim3(grid), dim3(1024), cdyn2, st, Lc, Wt, it);
+                if (shape == 2)
+                    hipLaunchKernelGGL((wf_step_clds2<FEAT, 512>), dim3(grid), dim3(512), cdyn2, st, Lc, Wt, it);
+                else if (shape == 3)
+                    hipLaunchKernelGGL((wf_step_clds2<FEAT, 640>), dim3(grid), dim3(640), cdyn2, st, Lc, Wt, it);
+                else if (shape == 4)
+                    hipLaunchKernelGGL((wf_step_clds2<FEAT, 768>), dim3(grid), dim3(768), cdyn2, st, Lc, Wt, it);
+                else if (cn == CN_F32_4)
+                    hipLaunchKernelGGL((wf_step_clds<FEAT, CN_F32_4>), dim3(grid), dim3(1024), cdyn2, st, Lc, Wt, it);
+                else if (cn == CN_F16_4)
+                    hipLaunchKernelGGL((wf_step_clds<FEAT, CN_F16_4>), dim3(grid), dim3(1024), cdyn2, st, Lc, Wt, it);
                 else
-                    hipLaunchKernelGGL((wf_step_clds<FEAT, false>), dim3(grid), dim3(1024), cdyn2, st, Lc, Wt, it);
+                    hipLaunchKernelGGL((wf_step_clds<FEAT, CN_F16_8>), dim3(grid), dim3(1024), cdyn2, st, Lc, Wt, it);
                 RTW_TIME_END(T)
                 continue;
             }
@@ -1724,12 +1766,18 @@ void wf_run_fused(const rtw_launch& L, const rtw_wf& W0, hipStream_t st, int n_c
         bool done = false;
         if constexpr ((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING)) == 0) {
             if (clds && (L.wf_fuse & 2u)) {
-                if (two)
-                    hipLaunchKernelGGL(wf_tail_clds2<FEAT>, dim3(tgrid[0]), dim3(RTW_CLDS2_THREADS), clds, st, L, W, iters);
-                else if (y4)
-                    hipLaunchKernelGGL((wf_tail_clds<FEAT, true>), dim3(tgrid[0]), dim3(1024), clds, st, L, W, iters);
+                if (shape == 2)
+                    hipLaunchKernelGGL((wf_tail_clds2<FEAT, 512>), dim3(tgrid[0]), dim3(512), clds, st, L, W, iters);
+                else if (shape == 3)
+                    hipLaunchKernelGGL((wf_tail_clds2<FEAT, 640>), dim3(tgrid[0]), dim3(640), clds, st, L, W, iters);
+                else if (shape == 4)
+                    hipLaunchKernelGGL((wf_tail_clds2<FEAT, 768>), dim3(tgrid[0]), dim3(768), clds, st, L, W, iters);
+                else if (cn == CN_F32_4)
+                    hipLaunchKernelGGL((wf_tail_clds<FEAT, CN_F32_4>), dim3(tgrid[0]), dim3(1024), clds, st, L, W, iters);
+                else if (cn == CN_F16_4)
+                    hipLaunchKernelGGL((wf_tail_clds<FEAT, CN_F16_4>), dim3(tgrid[0]), dim3(1024), clds, st, L, W, iters);
                 else
-                    hipLaunchKernelGGL((wf_tail_clds<FEAT, false>), dim3(tgrid[0]), dim3(1024), clds, st, L, W, iters);
+                    hipLaunchKernelGGL((wf_tail_clds<FEAT, CN_F16_8>), dim3(tgrid[0]), dim3(1024), clds, st, L, W, iters);
                 done = true;
             }
         }
@@ -1758,7 +1806,7 @@ void wf_run(const rtw_launch& L, const rtw_wf& W0, hipStream_t st, int n_cu, rtw
         // (textured scenes keep the 32-B node stage: it leaves LDS for the Perlin tables and the
         // 1024-thread compact kernel would spill at its 128-VGPR cap -- C5 -20 % measured)
         if constexpr ((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING | RTW_F_IMAGE | RTW_F_NOISE)) == 0) {
-            const size_t c = (size_t)L.n_nodes * L.n_orders * 16u;
+            const size_t c = (size_t)L.n_nodes * L.n_orders * (L.cnode32 ? 32u : 16u);
             if (L.cnodes && L.fast_box && L.wf_clds && c <= RTW_WF_CLDS_MAX) fclds = c;
         }
         const size_t need = (size_t)L.n_nodes * L.n_orders * 32u;
@@ -1788,7 +1836,7 @@ void wf_run(const rtw_launch& L, const rtw_wf& W0, hipStream_t st, int n_cu, rtw
                    lds_grid0 = lds ? wf_lds_grid<FEAT, true>(n_cu, tlds) : 0;
     // compact nodes of every octant copy in LDS (small static sphere trees)
     const size_t clds = (L.cnodes && L.fast_box && L.wf_clds)
-                            ? (size_t)L.n_nodes * L.n_orders * 16u : 0;
+                            ? (size_t)L.n_nodes * L.n_orders * (L.cnode32 ? 32u : 16u) : 0;
     thread_local uint32_t clds_grid_cache[3] = {0, 0, 0};
     uint32_t clds_grid = 0, clds_grid0 = 0;
     constexpr uint32_t clds_threads = 1024;  // one block per CU shares the stage (256 / 512: slower)
@@ -1807,18 +1855,14 @@ void wf_run(const rtw_launch& L, const rtw_wf& W0, hipStream_t st, int n_cu, rtw
         RTW_TIME_BEGIN(T, RTW_K_TRACE)
         if constexpr ((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING)) == 0) {
             if (clds_grid) {
-                const bool y4 = L.n_orders == 4;
-                if (it == 0 && y4)
-                    hipLaunchKernelGGL((wf_trace_clds<FEAT, true, true>), dim3(clds_grid0), dim3(clds_threads), clds, st,
-                                       L, W, it);
-                else if (it == 0)
-                    hipLaunchKernelGGL((wf_trace_clds<FEAT, true>), dim3(clds_grid0), dim3(clds_threads), clds, st, L,
-                                       W, it);
-                else if (y4)
-                    hipLaunchKernelGGL((wf_trace_clds<FEAT, false, true>), dim3(clds_grid), dim3(clds_threads), clds, st,
-                                       L, W, it);
-                else
-                    hipLaunchKernelGGL(wf_trace_clds<FEAT>, dim3(clds_grid), dim3(clds_threads), clds, st, L, W, it);
+                const int cn = L.cnode32 ? CN_F32_4 : L.n_orders == 4 ? CN_F16_4 : CN_F16_8;
+                const dim3 g(it == 0 ? clds_grid0 : clds_grid), b(clds_threads);
+                if (it == 0 && cn == CN_F32_4) hipLaunchKernelGGL((wf_trace_clds<FEAT, true, CN_F32_4>), g, b, clds, st, L, W, it);
+                else if (it == 0 && cn == CN_F16_4) hipLaunchKernelGGL((wf_trace_clds<FEAT, true, CN_F16_4>), g, b, clds, st, L, W, it);
+                else if (it == 0) hipLaunchKernelGGL((wf_trace_clds<FEAT, true, CN_F16_8>), g, b, clds, st, L, W, it);
+                else if (cn == CN_F32_4) hipLaunchKernelGGL((wf_trace_clds<FEAT, false, CN_F32_4>), g, b, clds, st, L, W, it);
+                else if (cn == CN_F16_4) hipLaunchKernelGGL((wf_trace_clds<FEAT, false, CN_F16_4>), g, b, clds, st, L, W, it);
+                else hipLaunchKernelGGL((wf_trace_clds<FEAT, false, CN_F16_8>), g, b, clds, st, L, W, it);
                 RTW_TIME_END(T)
                 goto shade_step;
             }
@@ -1923,9 +1967,12 @@ void rtw_wf_run_spheres(const rtw_launch& L, const rtw_wf& W, hipStream_t st, in
 uint32_t rtw_wf_spheres_max_waves(int n_cu) {
     const uint32_t b = std::max({wf_grids<0u>(n_cu).shade, wf_grids<0u>(n_cu).shade0, wf_grids<RTW_F_CHECKER>(n_cu).shade,
                                  wf_grids<RTW_F_CHECKER>(n_cu).shade0});
-    static const uint32_t c2 = std::max(wf_grid(wf_step_clds2<0u>, n_cu, 0, RTW_CLDS2_THREADS),
-                                        wf_grid(wf_step_clds2<RTW_F_CHECKER>, n_cu, 0, RTW_CLDS2_THREADS)) *
-                               (RTW_CLDS2_THREADS / 64u);
+    static const uint32_t c2 = std::max({wf_grid(wf_step_clds2<0u, 512>, n_cu, 0, 512) * 8u,
+                                         wf_grid(wf_step_clds2<0u, 640>, n_cu, 0, 640) * 10u,
+                                         wf_grid(wf_step_clds2<0u, 768>, n_cu, 0, 768) * 12u,
+                                         wf_grid(wf_step_clds2<RTW_F_CHECKER, 512>, n_cu, 0, 512) * 8u,
+                                         wf_grid(wf_step_clds2<RTW_F_CHECKER, 640>, n_cu, 0, 640) * 10u,
+                                         wf_grid(wf_step_clds2<RTW_F_CHECKER, 768>, n_cu, 0, 768) * 12u});
     static const uint32_t c1 = std::max(wf_grid(wf_step_clds<0u>, n_cu, 0, 1024), wf_grid(wf_step_clds<RTW_F_CHECKER>, n_cu, 0, 1024)) * 16u;
     return std::max({4u * b, c2, c1});
 }
