@@ -37,6 +37,9 @@ VALU_PEAK_TLOPS = round(N_SIMD * 64 / VALU_CYCLES_PER_INST * CLOCK_HZ / 1e12, 3)
 VALU_PEAK_SRC = "profiles/r4_valu_peak/summary.txt"
 NODE_BYTES = 32                # one BVH node / leaf record (rtw_layout.h)
 ROWS_PER_BLOCK = 8   # row blocks interleaved over ranks: C2 at 8 GPUs 6.97x predicted (16: 6.87x; tools/shard_sim.py)
+# the rows left over after whole rounds of blocks split evenly (RTW_ROWS_BALANCED): C2 at 8 ranks renders 100 rows per
+# rank instead of 104 on four ranks and 96 on the others (profiles/r5_shard/)
+ROWS_BALANCED = True
 
 
 def parse():
@@ -124,7 +127,8 @@ def main():
     world = pkg.World(arr, device=pkg._abi.RTW_DEVICE_CPU if host else local_rank, tuning=tun)
     # single-process multi-GPU: one context per device + the RCCL communicators of rtw_multi
     worlds = [world] + [pkg.World(arr, device=k, tuning=tun) for k in range(1, n_shards)] if single else [world]
-    multi = pkg.distributed.MultiDeviceRender(worlds, ROWS_PER_BLOCK) if single else None
+    rpb_arg = ROWS_PER_BLOCK | (pkg._abi.RTW_ROWS_BALANCED if ROWS_BALANCED else 0)
+    multi = pkg.distributed.MultiDeviceRender(worlds, rpb_arg) if single else None
     # the exchange's participants as the collective layer reports them: rtw_multi's RCCL communicator
     # (ncclCommCount), or torch.distributed's process group (backend "nccl" = RCCL on ROCm)
     if single:
@@ -147,10 +151,10 @@ def main():
     if not host:
         torch.cuda.set_stream(stream)
     # the shard this process renders (single-process mode: device 0's, for the counted and timing passes)
-    shard = pkg.distributed.ShardedRender(world, cam, shard_rank, n_shards, ROWS_PER_BLOCK,
+    shard = pkg.distributed.ShardedRender(world, cam, shard_rank, n_shards, rpb_arg,
                                           device=torch.device("cpu") if host else None)
     my_rows = shard.rows
-    assert my_rows == L.rtw_shard_rows(H, ROWS_PER_BLOCK, n_shards, shard_rank)
+    assert my_rows == L.rtw_shard_rows(H, rpb_arg, n_shards, shard_rank)
     frame = torch.zeros((W * H, 4), dtype=torch.float32, device="cuda") if single else None
 
     def render_step(counters=None, w=None, timing=None):
@@ -354,7 +358,8 @@ def main():
                        "bvh_depth": stats["depth"], "parallelism": f"row-interleaved tiles x{n_shards}"
                        + ((" + gloo gather (host backend)" if host else " + RCCL gather") if distributed else "")
                        + (" (one process, rtw_multi: grouped RCCL send/recv)" if single else ""),
-                       "rows_per_block": ROWS_PER_BLOCK, "exchange": rccl,
+                       "rows_per_block": ROWS_PER_BLOCK, "row_split": "balanced" if ROWS_BALANCED else "blocks",
+                       "exchange": rccl,
                        "shard": {"n_shards": n_shards, "rank": shard_rank, "rows": my_rows,
                                  "emulated": emulated},
                        "timed_scope": ("host contexts (rtw_render_rows) into host tiles, gathered over gloo: the "

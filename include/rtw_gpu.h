@@ -350,6 +350,8 @@ typedef struct rtw_tuning {
                                   1024-thread block per CU, 2 / 3 / 4 = two blocks of 512 / 640 / 768 threads
                                   (4 / 5 / 6 waves per SIMD) when the stage fits half the LDS; the 8-copy stage
                                   always runs one block (ABI 7) */
+    uint32_t deal;             /* wavefront iteration 0: 0 = runs of a tile's samples dealt round-robin over the
+                                  waves, 1 = waves claim runs of 16 from a counter as they finish (ABI 7) */
 } rtw_tuning;
 
 void rtw_tuning_defaults(rtw_tuning* out);
@@ -396,6 +398,16 @@ uint32_t rtw_shard_rows(uint32_t height, uint32_t rows_per_block, uint32_t n_sha
 /* Image row of row `tile_row` of a shard's compact tile (>= height: padding; 0xFFFFFFFF: bad spec).
  * The same function places rows in the render kernels and the multi-GPU gather. */
 uint32_t rtw_shard_image_row(uint32_t rows_per_block, uint32_t n_shards, uint32_t shard, uint32_t tile_row);
+/* ABI 7: rows_per_block | RTW_ROWS_BALANCED (every shard entry point, rtw_render_multi* included): rounds of
+ * n_shards row blocks dealt in alternating order (round k: shard s takes the round's block s if k is even, block
+ * n_shards - 1 - s if odd, so no shard always gets the lowest block of a round), then the rows left over (height
+ * mod (rows_per_block * n_shards)) split evenly -- `sub` = ceil(rest / n_shards) consecutive rows per shard, in the
+ * same alternating position, in one more block slot of its tile -- so the shards' row counts differ by at most sub
+ * instead of by one block.  rtw_shard_image_row_h: the image row of a tile row under either layout (>= height:
+ * padding; 0xFFFFFFFF: bad spec). */
+#define RTW_ROWS_BALANCED 0x80000000u
+uint32_t rtw_shard_image_row_h(uint32_t height, uint32_t rows_per_block, uint32_t n_shards, uint32_t shard,
+                               uint32_t tile_row);
 
 /* ---------------------------------------------------------------------------
  * Multi-GPU frame in one process (the north star's "8-GPU tile shard

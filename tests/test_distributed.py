@@ -56,6 +56,47 @@ def test_shard_image_row_matches_reassembly(rtw):
     assert L.rtw_shard_image_row(8, 2, 2, 0) == 0xFFFFFFFF
 
 
+BAL = 0x80000000  # RTW_ROWS_BALANCED
+
+
+def test_balanced_shards_split_the_rest_evenly(rtw):
+    """rows_per_block | RTW_ROWS_BALANCED: the library's row map (rtw_shard_image_row_h, rtw_shard_rows -- the
+    render kernels' and the multi-GPU pack/unpack's rtw_shard_row) equals the Python restatement and the
+    reassembly index, places every image row exactly once, and the shards' row counts differ by at most the
+    left-over share `sub` (C2 at 8 ranks, 8-row blocks: 100 rows each instead of 104 / 96)."""
+    L = rtw.lib()
+    d = rtw.distributed
+    for H in (1, 7, 15, 17, 225, 800, 1080, 2160):
+        for rpb in (1, 4, 8, 16):
+            for n in (1, 2, 3, 4, 8):
+                f = rpb | BAL
+                cap = d.tile_rows_capacity(H, f, n)
+                src, dst = d.reassembly_index(H, f, n)
+                got, counts = {}, []
+                for sh in range(n):
+                    rows = d.shard_rows(H, f, n, sh)
+                    assert len(rows) == L.rtw_shard_rows(H, f, n, sh)
+                    counts.append(len(rows))
+                    assert d.shard_tile_rows(H, f, n, sh) <= cap and cap % rpb == 0
+                    for r in range(cap):
+                        y = L.rtw_shard_image_row_h(H, f, n, sh, r)
+                        assert y == (d.shard_row(H, f, n, sh, r) if r < d.shard_tile_rows(H, f, n, sh) or y >= H else y)
+                        if y < H and r < d.shard_tile_rows(H, f, n, sh):
+                            assert y not in got.values()
+                            got[sh * cap + r] = y
+                assert got == dict(zip(src, dst))
+                assert sorted(got.values()) == list(range(H))
+                full = H // (rpb * n)
+                sub = -(-(H - full * rpb * n) // n)
+                assert max(counts) - min(counts) <= sub
+                # plain layout: the same rows as rtw_shard_image_row
+                for sh in range(n):
+                    for r in range(d.tile_rows_capacity(H, rpb, n)):
+                        assert L.rtw_shard_image_row_h(H, rpb, n, sh, r) == L.rtw_shard_image_row(rpb, n, sh, r)
+    assert [len(d.shard_rows(800, 8 | BAL, 8, sh)) for sh in range(8)] == [100] * 8
+    assert L.rtw_shard_image_row(8 | BAL, 2, 0, 0) == 0xFFFFFFFF  # the plain map has no height: refused
+
+
 def test_multi_create_rejects_bad_args(rtw):
     import ctypes as C
     h = C.c_void_p()
@@ -134,7 +175,7 @@ def _render_worker(rank, world_size, port, W, spp, rpb, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world_size,rpb", [(2, 8), (3, 4)])
+@pytest.mark.parametrize("world_size,rpb", [(2, 8), (3, 4), (3, 8 | BAL)])
 def test_gather_of_rendered_shards_gloo(rtw, world_size, rpb):
     """Each rank renders its row-interleaved shard (main.zig:314-326's split, made shardable) and rank 0
     gathers and reassembles: the image equals a single-process host render of the whole frame bit for bit

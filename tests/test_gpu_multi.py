@@ -29,7 +29,7 @@ def setup(rtw):
         w.close()
 
 
-@pytest.mark.parametrize("rpb", [8, 3])
+@pytest.mark.parametrize("rpb", [8, 3, 8 | 0x80000000])
 def test_multi_device_bit_identical(rtw, setup, rpb):
     import torch
     arr, worlds = setup

@@ -176,17 +176,19 @@ def test_shard_rows_reassemble(rtw, book1):
     cam = rtw.book1_camera(image_width=600, aspect_ratio=1.5, spp=4).init()
     H, W = cam.derived.image_height, cam.derived.image_width
     full = render_rows(rtw, world, cam, 0, H, 0, 4, 9)
-    for n_shards, rpb in ((3, 8), (8, 16), (2, 1)):
+    BAL = rtw._abi.RTW_ROWS_BALANCED
+    for n_shards, rpb in ((3, 8), (8, 16), (2, 1), (8, 8 | BAL), (3, 8 | BAL), (7, 16 | BAL)):
         img = np.zeros((H, W, 4), np.float32)
+        d = rtw.distributed
         for s in range(n_shards):
             rows = rtw.lib().rtw_shard_rows(H, rpb, n_shards, s)
-            nblk_owned = (((H + rpb - 1) // rpb) - s + n_shards - 1) // n_shards
-            tile = torch.zeros((max(1, nblk_owned * rpb) * W, 4), dtype=torch.float32, device="cuda")
+            tr = d.shard_tile_rows(H, rpb, n_shards, s)
+            tile = torch.zeros((max(1, tr) * W, 4), dtype=torch.float32, device="cuda")
             rc = rtw.lib().rtw_render_rows_device(world.handle, C.byref(cam.derived), rpb, n_shards, s, 0, 4, 9,
                                                   tile.data_ptr(), None, None)
             rtw._abi.check(rc, "rtw_render_rows_device")
             t = tile.cpu().numpy().reshape(-1, W, 4)
-            ys = [((r // rpb) * n_shards + s) * rpb + r % rpb for r in range(nblk_owned * rpb)]
+            ys = [d.shard_row(H, rpb, n_shards, s, r) for r in range(tr)]
             k = 0
             for r, y in enumerate(ys):
                 if y < H:
@@ -342,7 +344,8 @@ def test_v1_knobs_invariant(rtw, book1, knob):
                                   {"bvh_orders": 4, "compact_nodes": 2, "fuse": 0},
                                   {"bvh_orders": 4, "compact_nodes": 2, "lds": 127 & ~2},
                                   {"bvh_orders": 4, "compact_nodes": 2, "tile_lists": 0},
-                                  {"bvh_orders": 8, "compact_nodes": 2}])
+                                  {"bvh_orders": 8, "compact_nodes": 2}, {"deal": 1}, {"deal": 1, "fuse": 0},
+                                  {"deal": 1, "lds": 127 & ~2}, {"deal": 1, "wf_paths": 4096}])
 def test_wavefront_knobs_invariant(rtw, book1, knob):
     """Wavefront tuning (rtw_tuning: bounces before the tail kernel, batch size ->
     many batches, FMA vs reference slab test, LDS-staged nodes, SAH leaf runs of up

@@ -22,6 +22,7 @@ RTW_BVH_REFERENCE, RTW_BVH_SAH = 0, 1
 RTW_PPM_WRITECOLOR, RTW_PPM_STDOUT = 0, 1
 RTW_RENDER_NO_SYNC = 1
 RTW_RENDER_FRESH = 2
+RTW_ROWS_BALANCED = 0x80000000  # rows_per_block flag: the left-over rows split evenly over the shards (ABI 7)
 RTW_STAT_RAYS, RTW_STAT_NODES, RTW_STAT_LEAVES, RTW_STAT_SAMPLES, RTW_STAT_NAN, RTW_STAT_TAIL_RAYS = 0, 1, 2, 3, 4, 5
 RTW_STAT_COUNT = 8
 RTW_K_GEN, RTW_K_TRACE, RTW_K_SHADE, RTW_K_TAIL, RTW_K_REDUCE, RTW_K_MEGA, RTW_K_COUNT = 0, 1, 2, 3, 4, 5, 8
@@ -135,7 +136,7 @@ class RtwTuning(C.Structure):
                 ("wide_walk", C.c_uint32), ("wf_paths", C.c_uint64),
                 ("tile_lists", C.c_uint32), ("hoist", C.c_uint32), ("sort_iters", C.c_uint32),
                 ("sort_bits", C.c_uint32),
-                ("sort_iters_split", C.c_uint32), ("object_tree", C.c_uint32), ("clds_shape", C.c_uint32)]
+                ("sort_iters_split", C.c_uint32), ("object_tree", C.c_uint32), ("clds_shape", C.c_uint32), ("deal", C.c_uint32)]
 
 
 def tuning(**fields) -> RtwTuning:
@@ -184,6 +185,7 @@ SIGNATURES = {
                                          C.POINTER(RtwRenderOpts)]),
     "rtw_shard_rows": (C.c_uint32, [C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32]),
     "rtw_shard_image_row": (C.c_uint32, [C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32]),
+    "rtw_shard_image_row_h": (C.c_uint32, [C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32]),
     "rtw_multi_create": (C.c_int, [C.POINTER(C.c_void_p), C.c_uint32, C.POINTER(C.c_void_p)]),
     "rtw_multi_destroy": (None, [C.c_void_p]),
     "rtw_render_multi_device": (C.c_int, [C.c_void_p, C.POINTER(RtwCamera), C.c_uint32, C.c_uint32, C.c_uint32,

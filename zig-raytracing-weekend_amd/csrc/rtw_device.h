@@ -1437,7 +1437,7 @@ __host__ __device__ f3 sample_radiance(const float4* __restrict__ nodes, const r
 
 RTW_DHD bool map_row(const rtw_launch& L, uint32_t r, uint32_t& y) {
     if (L.n_shards) {
-        y = rtw_tile_row_image(L.rpb, L.n_shards, L.shard, r);
+        y = rtw_shard_row(L.H, L.rpb, L.n_shards, L.shard, r);
     } else {
         y = r;
     }

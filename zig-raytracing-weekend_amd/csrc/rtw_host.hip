@@ -177,6 +177,7 @@ int rtw_scene_create_ex(const rtw_scene_desc* d, int device, const rtw_tuning* t
     if (tu.bvh_orders != 0 && tu.bvh_orders != 1 && tu.bvh_orders != 4 && tu.bvh_orders != 8)
         return fail(RTW_E_INVALID, "tuning.bvh_orders must be 0, 1, 4 or 8");
     if (tu.clds_shape > 4) return fail(RTW_E_INVALID, "tuning.clds_shape must be 0..4");
+    if (tu.deal > 1) return fail(RTW_E_INVALID, "tuning.deal must be 0 or 1");
     if (tu.wf_iters < 1 || tu.wf_iters > RTW_WF_MAX_ITERS) return fail(RTW_E_INVALID, "tuning.wf_iters out of range");
     if ((tu.object_tree & 0xFFu) > 100 || (tu.object_tree & ~(0xFFu | RTW_OTREE_NO_CULL)))
         return fail(RTW_E_INVALID, "tuning.object_tree: 0..100 [| RTW_OTREE_NO_CULL]");
@@ -395,6 +396,7 @@ int rtw_scene_create_ex(const rtw_scene_desc* d, int device, const rtw_tuning* t
     L.n_nodes = (uint32_t)n_nodes;
     L.n_orders = orders;
     L.clds_shape = tu.clds_shape;
+    ctx->wf_deal = tu.deal;
     L.cnode32 = cnode32 ? 1u : 0u;
     L.n_perlin = d->n_perlins;
     ctx->feat = scene_features(d) | geom.feat;
@@ -586,7 +588,7 @@ int validate_cam(const rtw_camera* cam) {
 size_t wf_state_bytes(uint64_t Q, uint64_t P) {
     auto al = [](uint64_t b) { return (size_t)((b + 255) & ~uint64_t(255)); };
     return 2 * (4 * al(Q * 16) + al(Q * 8)) + al(Q * 8) + al(P * sizeof(rtw_rgb)) +
-           3 * al((uint64_t)RTW_WF_STRIPES * RTW_WF_LEN_STRIDE * 4);
+           3 * al((uint64_t)RTW_WF_STRIPES * RTW_WF_LEN_STRIDE * 4) + al(RTW_WF_DEAL_COUNTERS * 4);
 }
 static_assert(RTW_WF_PATH_BYTES == 2 * (4 * 16 + 8) + 8 + sizeof(rtw_rgb), "RTW_WF_PATH_BYTES = wf_state_bytes per path");
 
@@ -651,6 +653,8 @@ int run_wavefront(rtw_ctx* ctx, rtw_launch L, hipStream_t stream, rtw_timer* T) 
     W.hit = reinterpret_cast<float2*>(take(Q * 8));
     W.ls = reinterpret_cast<rtw_rgb*>(take(P * sizeof(rtw_rgb)));
     for (int k = 0; k < 3; k++) W.len[k] = reinterpret_cast<uint32_t*>(take(RTW_WF_STRIPES * RTW_WF_LEN_STRIDE * 4));
+    uint32_t* deal = reinterpret_cast<uint32_t*>(take(RTW_WF_DEAL_COUNTERS * 4));
+    W.deal = ctx->wf_deal ? deal : nullptr;
     W.n_pix = (uint32_t)n_pix;
     W.iters = ctx->wf_iters;
     W.sort_iters = ctx->wf_sort_iters;
@@ -816,10 +820,8 @@ int render_rows_locked(rtw_ctx* ctx, const rtw_camera* cam, uint32_t rpb, uint32
     rtw_launch L = make_launch(ctx, cam, seed);
     L.accum = reinterpret_cast<float4*>(d_tile);
     L.row0 = 0;
-    // logical rows 0 .. (#blocks owned * rpb); rows past H are masked in-kernel
-    const uint32_t nblk = (cam->image_height + rpb - 1) / rpb;
-    const uint32_t owned = nblk > shard ? (nblk - shard + n_shards - 1) / n_shards : 0;
-    L.n_rows = owned * rpb;
+    // logical rows 0 .. (the shard's whole blocks); rows past H (or past a balanced shard's share) are masked
+    L.n_rows = rtw_shard_tile_rows(cam->image_height, rpb, n_shards, shard);
     L.rpb = rpb;
     L.n_shards = n_shards;
     L.shard = shard;
@@ -990,19 +992,22 @@ int rtw_render_device(rtw_ctx* ctx, const rtw_camera* cam, uint32_t pix_begin, u
 }
 
 uint32_t rtw_shard_rows(uint32_t H, uint32_t rpb, uint32_t n_shards, uint32_t shard) {
-    if (!rpb || !n_shards || shard >= n_shards) return 0;
+    if (!(rpb & ~RTW_ROWS_FLAGS) || !n_shards || shard >= n_shards) return 0;
     uint32_t rows = 0;
-    const uint32_t nblk = (H + rpb - 1) / rpb;
-    for (uint32_t b = shard; b < nblk; b += n_shards) {
-        const uint32_t y0 = b * rpb;
-        rows += (H - y0 < rpb) ? H - y0 : rpb;
-    }
+    const uint32_t t = rtw_shard_tile_rows(H, rpb, n_shards, shard);
+    for (uint32_t r = 0; r < t; r++) rows += rtw_shard_row(H, rpb, n_shards, shard, r) < H ? 1u : 0u;
     return rows;
 }
 
 uint32_t rtw_shard_image_row(uint32_t rpb, uint32_t n_shards, uint32_t shard, uint32_t tile_row) {
-    if (!rpb || !n_shards || shard >= n_shards) return 0xFFFFFFFFu;
+    if (!rpb || (rpb & RTW_ROWS_FLAGS) || !n_shards || shard >= n_shards) return 0xFFFFFFFFu;
     return rtw_tile_row_image(rpb, n_shards, shard, tile_row);
+}
+
+uint32_t rtw_shard_image_row_h(uint32_t H, uint32_t rpb, uint32_t n_shards, uint32_t shard, uint32_t tile_row) {
+    if (!(rpb & ~RTW_ROWS_FLAGS) || (rpb & RTW_ROWS_FLAGS & ~RTW_ROWS_BALANCED) || !n_shards || shard >= n_shards)
+        return 0xFFFFFFFFu;
+    return rtw_shard_row(H, rpb, n_shards, shard, tile_row);
 }
 
 int rtw_render_rows_device(rtw_ctx* ctx, const rtw_camera* cam, uint32_t rpb, uint32_t n_shards, uint32_t shard,
@@ -1011,7 +1016,7 @@ int rtw_render_rows_device(rtw_ctx* ctx, const rtw_camera* cam, uint32_t rpb, ui
     if (!ctx || !d_tile) return fail(RTW_E_INVALID, "null ctx/tile");
     if (ctx->device == RTW_DEVICE_CPU) return fail(RTW_E_INVALID, "host context: use rtw_render_rows");
     if (int rc = validate_cam(cam)) return rc;
-    if (!rpb || !n_shards || shard >= n_shards) return fail(RTW_E_INVALID, "bad shard spec");
+    if (!(rpb & ~RTW_ROWS_FLAGS) || !n_shards || shard >= n_shards) return fail(RTW_E_INVALID, "bad shard spec");
     if (spp_begin > spp_end) return fail(RTW_E_INVALID, "bad sample range");
     const uint32_t rows = rtw_shard_rows(cam->image_height, rpb, n_shards, shard);
     if (rows == 0 || spp_begin == spp_end) return RTW_OK;
@@ -1027,7 +1032,7 @@ int rtw_render_rows(rtw_ctx* ctx, const rtw_camera* cam, uint32_t rpb, uint32_t 
     if (!ctx || !tile) return fail(RTW_E_INVALID, "null ctx/tile");
     if (int rc = validate_cam(cam)) return rc;
     if (int rc = check_host_opts(opts)) return rc;
-    if (!rpb || !n_shards || shard >= n_shards) return fail(RTW_E_INVALID, "bad shard spec");
+    if (!(rpb & ~RTW_ROWS_FLAGS) || !n_shards || shard >= n_shards) return fail(RTW_E_INVALID, "bad shard spec");
     if (spp_begin > spp_end) return fail(RTW_E_INVALID, "bad sample range");
     const uint32_t rows = rtw_shard_rows(cam->image_height, rpb, n_shards, shard);
     if (rows == 0 || spp_begin == spp_end) return RTW_OK;

@@ -231,6 +231,7 @@ struct rtw_ctx {
     uint32_t wf_sort_iters_split = 1;  // the same for the split kernels (rtw_tuning.sort_iters_split)
     uint32_t wf_sort_iters = 3;    // iterations whose survivors are filed by direction (rtw_tuning.sort_iters)
     uint32_t cpu_threads = 0;      // host context: worker threads (rtw_tuning.cpu_threads; 0 = all)
+    uint32_t wf_deal = 0;          // iteration 0's runs dealt dynamically (rtw_tuning.deal)
     int n_cu = 256;                // compute units of the device (wavefront grids)
     std::vector<hipEvent_t> ev_pool;  // recycled timing events
     uint64_t scene_hash = 0;       // FNV-1a 64 of the uploaded scene image

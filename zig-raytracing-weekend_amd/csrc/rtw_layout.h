@@ -112,3 +112,41 @@ struct rtw_dev_image {
 __host__ __device__ inline uint32_t rtw_tile_row_image(uint32_t rpb, uint32_t n_shards, uint32_t shard, uint32_t r) {
     return ((r / rpb) * n_shards + shard) * rpb + r % rpb;
 }
+
+// Balanced shards (rows_per_block | RTW_ROWS_BALANCED, include/rtw_gpu.h):
+//  * rounds of n blocks are dealt in alternating order -- round k gives its block k * n + s to shard s when k is
+//    even and to shard n - 1 - s when k is odd -- so no shard always takes the lowest block of a round (the
+//    plain order gives shard n - 1 the bottom rpb rows of every n * rpb: where the image's cost grows downwards,
+//    as Book-1's ground does, C2's shard 7 at 8 ranks rendered 7 % more than shard 0);
+//  * the rows left over after the whole rounds (H mod (rpb * n)) are split evenly -- `sub` = ceil(rest / n)
+//    consecutive rows each, in one more block slot of the tile -- so every shard renders the same number of rows
+//    (+- sub) instead of one block more for the first rest / rpb shards (C2 at 8: 100 rows each, not 104 / 96).
+// The tiles keep rpb-row blocks, so a shard's 8x8 pixel tiles still cover adjacent image rows.  Needs the image
+// height; every function below takes it.
+#define RTW_ROWS_FLAGS 0x80000000u
+__host__ __device__ inline uint32_t rtw_shard_row(uint32_t H, uint32_t rpbf, uint32_t n, uint32_t s, uint32_t r) {
+    const uint32_t rpb = rpbf & ~RTW_ROWS_FLAGS;
+    if (!(rpbf & RTW_ROWS_FLAGS)) return rtw_tile_row_image(rpb, n, s, r);
+    const uint32_t full = H / (rpb * n), fr = full * rpb;  // whole rounds; a shard's tile rows in them
+    const uint32_t k = r / rpb, pos = (k & 1u) ? n - 1u - s : s;  // round k, the shard's block in it
+    if (r < fr) return (k * n + pos) * rpb + r % rpb;
+    const uint32_t y0 = full * rpb * n, sub = (H - y0 + n - 1) / n, i = r - fr;
+    return i < sub ? y0 + pos * sub + i : 0xFFFFFFFFu;  // (>= H: padding)
+}
+// tile rows of shard s (padded: whole blocks), and the largest over the shards (every tile's capacity)
+__host__ __device__ inline uint32_t rtw_shard_tile_rows(uint32_t H, uint32_t rpbf, uint32_t n, uint32_t s) {
+    const uint32_t rpb = rpbf & ~RTW_ROWS_FLAGS;
+    if (!(rpbf & RTW_ROWS_FLAGS)) {
+        const uint32_t nblk = (H + rpb - 1) / rpb;
+        return nblk > s ? (nblk - s + n - 1) / n * rpb : 0u;
+    }
+    const uint32_t full = H / (rpb * n), y0 = full * rpb * n, sub = (H - y0 + n - 1) / n;
+    const uint32_t pos = (full & 1u) ? n - 1u - s : s;  // the shard's place in the last (partial) round
+    return full * rpb + (pos * sub < H - y0 ? rpb : 0u);
+}
+__host__ __device__ inline uint32_t rtw_shard_capacity(uint32_t H, uint32_t rpbf, uint32_t n) {
+    const uint32_t rpb = rpbf & ~RTW_ROWS_FLAGS;
+    if (!(rpbf & RTW_ROWS_FLAGS)) return rtw_shard_tile_rows(H, rpbf, n, 0);
+    const uint32_t full = H / (rpb * n);
+    return full * rpb + (H > full * rpb * n ? rpb : 0u);
+}

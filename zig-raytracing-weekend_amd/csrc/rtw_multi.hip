@@ -86,7 +86,7 @@ __global__ __launch_bounds__(256) void shard_rows_copy(float4* __restrict__ fram
     const uint32_t k = (uint32_t)(i / per);
     const uint32_t rem = (uint32_t)(i - (uint64_t)k * per);
     const uint32_t r = rem / W, x = rem - r * W;
-    const uint32_t y = rtw_tile_row_image(rpb, n, k, r);
+    const uint32_t y = rtw_shard_row(H, rpb, n, k, r);
     if (y >= H) return;
     float4* f = frame + (size_t)y * W + x;
     if (dir == 0) stacked[i] = *f;
@@ -135,8 +135,7 @@ int multi_render(rtw_multi* m, const rtw_camera* cam, uint32_t rpb, uint32_t s0,
                  float4* frame, hipStream_t stream, uint32_t spp_batch, uint32_t flags, const rtw_render_opts* ctl) {
     const uint32_t n = (uint32_t)m->ctx.size();
     const uint32_t W = cam->image_width, H = cam->image_height;
-    const uint32_t nblk = (H + rpb - 1) / rpb;
-    const uint32_t cap = (nblk + n - 1) / n * rpb;
+    const uint32_t cap = rtw_shard_capacity(H, rpb, n);
     const size_t per = (size_t)cap * W;
     if (rtw_stop_requested(ctl)) return mfail(RTW_E_CANCELLED, "cancelled");  // nothing touched
     if (int rc = ensure_buffers(m, per, 0)) return rc;
@@ -219,7 +218,7 @@ int check_args(rtw_multi* m, const rtw_camera* cam, uint32_t rpb, uint32_t s0, u
     if (!m) return mfail(RTW_E_INVALID, "null rtw_multi");
     if (!cam || cam->image_width == 0 || cam->image_height == 0) return mfail(RTW_E_INVALID, "camera not initialised");
     if ((uint64_t)cam->image_width * cam->image_height > 0xFFFFFFFFull) return mfail(RTW_E_INVALID, "image too large");
-    if (rpb == 0) return mfail(RTW_E_INVALID, "rows_per_block == 0");
+    if ((rpb & ~RTW_ROWS_FLAGS) == 0) return mfail(RTW_E_INVALID, "rows_per_block == 0");
     if (s0 > s1) return mfail(RTW_E_INVALID, "bad sample range");
     return RTW_OK;
 }

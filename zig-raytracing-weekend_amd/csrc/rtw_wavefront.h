@@ -66,9 +66,12 @@ struct rtw_wf {
     uint32_t sort_mask;   // the bucket key bits they use ((1 << rtw_tuning.sort_bits) - 1)
     uint32_t run_log2;    // iteration 0's tile runs: 2^run_log2 samples of one tile per run (wf_coherence)
     uint32_t packed;      // this render's queues hold the packed path state (wf_packed; set by wf_run*)
+    uint32_t* deal;       // dynamic dealing (rtw_tuning.deal): this launch's run and single-chunk counters (two,
+                          // zeroed per batch), or null for the static round-robin deal
 };
+#define RTW_WF_DEAL_COUNTERS 64  // run counters per batch (one per launch that deals iteration 0)
 
-// bytes of device state per path (two slot sets + hit + ls)
+// bytes of device state per path (two slot sets + hit + ls; the batch's counters aside)
 #define RTW_WF_PATH_BYTES (2 * (4 * 16 + 8) + 8 + 12)
 
 void rtw_wavefront_batch(const rtw_launch& L, const rtw_wf& W, void* stream, int n_cu, rtw_timer* T);

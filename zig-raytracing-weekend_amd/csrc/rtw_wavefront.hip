@@ -76,11 +76,26 @@ __device__ __forceinline__ void wf_path(const rtw_wf& W, uint32_t p, uint32_t& s
     q = (t << 6) | (p & 63u);
 }
 
+// Dynamic dealing of iteration 0 (W.deal, rtw_tuning.deal): a wave claims whole runs (RUN chunks of one tile,
+// tile-major) from the launch's counter W.deal[0] -- one atomic per run, issued a run ahead so its latency is
+// hidden -- until the runs run out.  Waves that draw cheap tiles (sky) take more runs, so the launch drains
+// evenly however few runs each wave gets: the runs keep their full 16 samples on small batches (a shard of a
+// multi-GPU render), where the static deal must shorten them to keep every wave's share even.  The last
+// 4 x (waves) chunks go one at a time (counter W.deal[1]), so the drain waits for a chunk, not a run.
+__device__ __forceinline__ uint32_t wf_claim(uint32_t* c) {  // lane 0 holds the claimed run
+    uint32_t v = 0;
+    if (__lane_id() == 0) v = atomicAdd(c, 1u);
+    return v;
+}
+
 // The slots of iteration `it` handed to this wave, 64 at a time:
 //   for (WfIter e(W, it); e.more(); e.next()) { uint32_t slot; if (e.get(W, slot)) ... }
 // (wave-uniform loop; get() is per lane)
 struct WfIter {
     uint32_t it, j, step, n, base, off, w, nw, slot0;
+    uint32_t run, kk, next_run;  // dynamic iteration 0: the run (or single chunk), the chunk in it, the next claim
+    uint32_t runs;               //   (lane 0); runs dealt whole, then single chunks
+    bool single;
     bool live0;  // iteration 0: chunk j exists
     __device__ WfIter(const rtw_wf& W, uint32_t it_) : it(it_) {
         w = wf_wave();
@@ -88,7 +103,18 @@ struct WfIter {
         if (it == 0) {
             j = 0;
             step = 1;
-            live0 = wf_chunk0(W, w, nw, 0, slot0);
+            if (W.deal) {
+                const uint32_t nc = W.n_paths >> 6, tail = 4u * nw;
+                runs = nc > tail ? (nc - tail) >> W.run_log2 : 0u;
+                single = false;
+                run = __builtin_amdgcn_readfirstlane(wf_claim(W.deal));
+                next_run = wf_claim(W.deal);
+                kk = 0;
+                if (run >= runs) to_single(W);
+                live0 = dyn_chunk(W);
+            } else {
+                live0 = wf_chunk0(W, w, nw, 0, slot0);
+            }
         } else {
             const uint32_t s = w % RTW_WF_STRIPES;
             j = w / RTW_WF_STRIPES;
@@ -100,10 +126,35 @@ struct WfIter {
         W_ = &W;
     }
     const rtw_wf* W_;
+    __device__ void to_single(const rtw_wf& W) {
+        single = true;
+        run = __builtin_amdgcn_readfirstlane(wf_claim(W.deal + 1));
+        next_run = wf_claim(W.deal + 1);
+    }
+    __device__ bool dyn_chunk(const rtw_wf& W) {
+        const uint32_t c = single ? (runs << W.run_log2) + run : (run << W.run_log2) + kk;
+        slot0 = c << 6;
+        return c < (W.n_paths >> 6);
+    }
     __device__ bool more() const { return it == 0 ? live0 : j < n; }
     __device__ void next() {
         j += step;
-        if (it == 0) live0 = wf_chunk0(*W_, w, nw, j, slot0);
+        if (it == 0) {
+            if (W_->deal) {
+                if (single) {
+                    run = __builtin_amdgcn_readfirstlane(next_run);
+                    next_run = wf_claim(W_->deal + 1);
+                } else if (++kk == (1u << W_->run_log2)) {
+                    run = __builtin_amdgcn_readfirstlane(next_run);
+                    next_run = wf_claim(W_->deal);
+                    kk = 0;
+                    if (run >= runs) to_single(*W_);
+                }
+                live0 = dyn_chunk(*W_);
+            } else {
+                live0 = wf_chunk0(*W_, w, nw, j, slot0);
+            }
+        }
     }
     __device__ bool get(const rtw_wf& W, uint32_t& slot) const {
         if (it == 0) {
@@ -1534,8 +1585,26 @@ __global__ __launch_bounds__(256) void wf_reduce(rtw_launch L, rtw_wf W) {
         uint32_t pixel, out_idx, x, y;
         if (wf_pixel(L, W, q, pixel, out_idx, x, y)) {
             float4 a = L.accum[out_idx];
-            for (uint32_t s = 0; s < W.n_s; s++) {
-                const rtw_rgb c = W.ls[((((size_t)(q >> 6) * W.n_s) + s) << 6) | (q & 63u)];  // wf_path
+            // the samples' radiances in groups of R loads issued together, then added in sample order (the same
+            // sums): one memory latency per group instead of per sample -- a shard of a multi-GPU render has too
+            // few pixels (waves) per SIMD to hide a latency per sample (C2 at 8 ranks: 2.2x the N = 1 time / 8)
+            constexpr uint32_t R = 8;
+            const rtw_rgb* __restrict__ ls = W.ls + (((size_t)(q >> 6) * W.n_s) << 6) + (q & 63u);  // wf_path
+            uint32_t s = 0;
+            for (; s + R <= W.n_s; s += R) {
+                rtw_rgb c[R];
+#pragma unroll
+                for (uint32_t k = 0; k < R; k++) c[k] = ls[(size_t)(s + k) << 6];
+#pragma unroll
+                for (uint32_t k = 0; k < R; k++) {
+                    if (is_nan3(mk(c[k].x, c[k].y, c[k].z))) cnt.nans++;
+                    a.x += c[k].x;
+                    a.y += c[k].y;
+                    a.z += c[k].z;
+                }
+            }
+            for (; s < W.n_s; s++) {
+                const rtw_rgb c = ls[(size_t)s << 6];
                 if (is_nan3(mk(c.x, c.y, c.z))) cnt.nans++;
                 a.x += c.x;
                 a.y += c.y;
@@ -1627,6 +1696,7 @@ rtw_wf wf_coherence(const rtw_wf& W, uint32_t nw, uint32_t sort_iters) {
     const uint32_t per_wave = nw ? (W.n_paths >> 6) / nw : 0u;
     uint32_t lg = 0;
     while (lg < 4 && (per_wave >> (lg + 1)) >= 64u) lg++;
+    if (W.deal) lg = 4;  // dynamic deal: the waves balance themselves, runs keep 16 samples of a tile
     C.run_log2 = lg;
     C.sort_iters = per_wave >= RTW_WF_SORT_MIN_CHUNKS ? sort_iters : 0u;
     return C;
@@ -1724,6 +1794,7 @@ void wf_run_fused(const rtw_launch& L, const rtw_wf& W0, hipStream_t st, int n_c
     // iteration 0 appends to len[1]; every later iteration's output counters are
     // zeroed by the kernel two iterations before (wf_step_zero_next)
     (void)hipMemsetAsync(W0.len[1], 0, RTW_WF_STRIPES * RTW_WF_LEN_STRIDE * 4, st);
+    if (W0.deal) (void)hipMemsetAsync(W0.deal, 0, RTW_WF_DEAL_COUNTERS * 4, st);
     rtw_wf W = wf_coherence(W0, grid * (clds ? cthreads / 64u : 4u), W0.sort_iters);
     W.packed = wf_packed<FEAT>() ? 1u : 0u;  // the fused step and its tail: always the packed state
     const uint32_t iters = L.max_depth < W.iters ? L.max_depth : W.iters;
@@ -1735,6 +1806,7 @@ void wf_run_fused(const rtw_launch& L, const rtw_wf& W0, hipStream_t st, int n_c
     if (iters == 0) (void)hipMemsetAsync(W.ls, 0, (size_t)W.n_paths * sizeof(rtw_rgb), st);
     for (uint32_t it = 0; it < iters; it++) {
         RTW_TIME_BEGIN(T, RTW_K_TRACE)
+        Wt.deal = W.deal;  // (only iteration 0 deals from it: counters 0-1)
         if constexpr ((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING)) == 0) {
             if (clds) {
                 rtw_launch Lc = L;  // the materials are staged only when they fit
@@ -1821,11 +1893,15 @@ void wf_run(const rtw_launch& L, const rtw_wf& W0, hipStream_t st, int n_cu, rtw
     }
     rtw_wf W = wf_coherence(W0, g.shade * 4u, W0.sort_iters_split);  // the split kernels' queues
     W.packed = wf_packed<FEAT>() ? 1u : 0u;  // the split kernels (and their tail) use the packed state too
+    // dynamic deal: iteration 0's trace deals from counters 0-1, its shade from counters 2-3
+    if (W0.deal) (void)hipMemsetAsync(W0.deal, 0, RTW_WF_DEAL_COUNTERS * 4, st);
     const uint32_t iters = L.max_depth < W.iters ? L.max_depth : W.iters;
     // iteration 0's trace and shade generate the camera rays themselves (wf_camera); with no
     // iteration (max_depth 0) nothing writes W.ls and the reduce must add zeros
     if (iters == 0) (void)hipMemsetAsync(W.ls, 0, (size_t)W.n_paths * sizeof(rtw_rgb), st);
     const rtw_wf Wt = iters ? wf_lists<FEAT>(L, W, st) : W;  // camera rays: iteration 0 of wf_trace (L1/L2)
+    rtw_wf Ws0 = W;  // iteration 0's shade: its own counters
+    if (W.deal) Ws0.deal = W.deal + 2;
     const size_t w2l = wf_w2_lds<FEAT>(L);  // the two-wide walk's stacks (trace / tail through L1/L2)
     thread_local uint32_t wtrace[2] = {0, 0}, wtrace0[2] = {0, 0}, wtail[2] = {0, 0};
     const size_t lds_need = (size_t)L.n_nodes * L.n_orders * 32u;
@@ -1883,7 +1959,7 @@ void wf_run(const rtw_launch& L, const rtw_wf& W0, hipStream_t st, int n_cu, rtw
         RTW_TIME_BEGIN(T, RTW_K_SHADE)
         if (it == 0)
             hipLaunchKernelGGL((wf_shade<FEAT, true>), dim3(g.shade0), dim3(256), (FEAT & RTW_F_GEOM) ? L.geom_lds : 0u,
-                               st, L, W, it);
+                               st, L, Ws0, it);
         else
             hipLaunchKernelGGL(wf_shade<FEAT>, dim3(g.shade), dim3(256), (FEAT & RTW_F_GEOM) ? L.geom_lds : 0u, st, L,
                                W, it);

@@ -18,22 +18,52 @@ from typing import List, Optional, Tuple
 from . import _abi
 
 
+def shard_row(height: int, rows_per_block: int, n_shards: int, shard: int, r: int) -> int:
+    """Image row of tile row r of `shard` (>= height: padding): rtw_shard_row (rtw_layout.h) restated.  Plain
+    layout: row block b of rpb rows goes to shard b % n_shards.  rows_per_block | RTW_ROWS_BALANCED: rounds of
+    n_shards blocks dealt in alternating order (round k: shard s takes block position s if k is even, else
+    n_shards - 1 - s), then the left-over rows split evenly (`sub` consecutive rows each, in one more block slot
+    of the tile)."""
+    rpb = rows_per_block & ~_abi.RTW_ROWS_BALANCED
+    if not rows_per_block & _abi.RTW_ROWS_BALANCED:
+        return ((r // rpb) * n_shards + shard) * rpb + r % rpb
+    full = height // (rpb * n_shards)
+    k = r // rpb
+    pos = n_shards - 1 - shard if k % 2 else shard  # rounds dealt in alternating order
+    if r < full * rpb:
+        return (k * n_shards + pos) * rpb + r % rpb
+    y0 = full * rpb * n_shards
+    sub = (height - y0 + n_shards - 1) // n_shards
+    i = r - full * rpb
+    return y0 + pos * sub + i if i < sub else 0xFFFFFFFF
+
+
+def shard_tile_rows(height: int, rows_per_block: int, n_shards: int, shard: int) -> int:
+    """Tile rows (whole blocks, padding included) of `shard` (rtw_shard_tile_rows)."""
+    rpb = rows_per_block & ~_abi.RTW_ROWS_BALANCED
+    if rows_per_block & _abi.RTW_ROWS_BALANCED:
+        full = height // (rpb * n_shards)
+        y0 = full * rpb * n_shards
+        sub = (height - y0 + n_shards - 1) // n_shards
+        pos = n_shards - 1 - shard if full % 2 else shard
+        return full * rpb + (rpb if pos * sub < height - y0 else 0)
+    n_blk = (height + rpb - 1) // rpb
+    return ((n_blk - shard + n_shards - 1) // n_shards) * rpb if n_blk > shard else 0
+
+
 def shard_rows(height: int, rows_per_block: int, n_shards: int, shard: int) -> List[int]:
     """Image rows owned by `shard`, in tile order (rtw_shard_rows / map_row)."""
     rows = []
-    n_blk = (height + rows_per_block - 1) // rows_per_block
-    for b in range(shard, n_blk, n_shards):
-        for k in range(rows_per_block):
-            y = b * rows_per_block + k
-            if y < height:
-                rows.append(y)
+    for r in range(shard_tile_rows(height, rows_per_block, n_shards, shard)):
+        y = shard_row(height, rows_per_block, n_shards, shard, r)
+        if y < height:
+            rows.append(y)
     return rows
 
 
 def tile_rows_capacity(height: int, rows_per_block: int, n_shards: int) -> int:
-    """Rows of the (padded) per-rank tile: equal on every rank so the gather is uniform."""
-    n_blk = (height + rows_per_block - 1) // rows_per_block
-    return ((n_blk + n_shards - 1) // n_shards) * rows_per_block
+    """Rows of the (padded) per-rank tile: equal on every rank so the gather is uniform (rtw_shard_capacity)."""
+    return max(shard_tile_rows(height, rows_per_block, n_shards, s) for s in range(n_shards))
 
 
 def reassembly_index(height: int, rows_per_block: int, n_shards: int) -> Tuple[List[int], List[int]]:
@@ -42,7 +72,7 @@ def reassembly_index(height: int, rows_per_block: int, n_shards: int) -> Tuple[L
     src, dst = [], []
     for s in range(n_shards):
         for r in range(cap):
-            y = ((r // rows_per_block) * n_shards + s) * rows_per_block + r % rows_per_block
+            y = shard_row(height, rows_per_block, n_shards, s, r)
             if y < height:
                 src.append(s * cap + r)
                 dst.append(y)
