@@ -328,6 +328,21 @@ def main():
         "nodes_per_ray_device": round((cdev["nodes"] + cdev["leaves"]) / max(1, cdev["rays"]), 3),
         "bvh": args.bvh,
     }
+    # ---- the work-normalised walk roofline: the render's device node visits (inner boxes +
+    # sphere tests of the SAH walk, the counted pass) per second against the walk ceiling -- the same compact
+    # LDS walk alone on the config's camera (+ bounce) rays, measured on this build (diag/trav_bench.hip,
+    # diag/run_walk_ceiling.py -> profiles/walk_ceiling_<config>.json).  Redundant lanes (the cooperative
+    # rejection loop's idle-lane candidates, hoisted spheres every lane tests) do not count here: a visit is
+    # one lane's step of its own walk.
+    dev_steps = cdev["nodes"] + cdev["leaves"]
+    walk_achieved = dev_steps / render_s if (render_s > 0 and not host) else None
+    ceiling, ceil_src = walk_ceiling(args, build_id)
+    roofline["walk"] = {
+        "unit": "node-steps/s", "achieved": walk_achieved, "ceiling": ceiling,
+        "frac": round(walk_achieved / ceiling, 4) if (walk_achieved and ceiling) else None,
+        "device_steps_per_render": dev_steps, "render_ms": round(render_s * 1e3, 3), "source": ceil_src,
+        "note": "device walk steps (inner boxes + sphere tests, one lane's own walk each) of a whole render per "
+                "second of render, over the compact LDS walk's rate alone on the config's rays (the ceiling)"}
     # a fraction above 1 is not evidence (a pass of another shard or launch shape): never published
     for sec in (roofline, roofline["hbm"]):
         if sec["frac"] is not None and sec["frac"] > 1.0:
@@ -432,6 +447,23 @@ def pmc_valu(args, kind, build_id, n_shards=1, rank=0, single=False):
         if name.startswith(kind) and isinstance(e, dict) and e.get("lane_ops"):
             return e, src
     return None, None
+
+
+def walk_ceiling(args, build_id):
+    """The walk ceiling of this config measured on this build (diag/run_walk_ceiling.py ->
+    profiles/walk_ceiling_<config>.json), or (None, reason).  Only the product defaults on the whole frame
+    (an A/B build or tuning, a shard at N > 1 -- whose per-rank render time prices fewer visits -- still
+    compare: the rate is per second, not per launch), but never a measurement of another build."""
+    if args.spp or args.tuning or args.bvh != "sah" or os.environ.get("RTW_LIB"):
+        return None, None
+    f = os.path.join(args.profiles_dir, f"walk_ceiling_{args.config}.json")
+    if not os.path.exists(f):
+        return None, None
+    d = json.load(open(f))
+    rel = os.path.relpath(f, REPO)
+    if d.get("build_id") != build_id:
+        return None, f"{rel}: build {d.get('build_id')} != loaded {build_id} (stale, unused)"
+    return d["ceiling"], rel
 
 
 def cpu_quota_cores():

@@ -121,12 +121,13 @@ def test_fused_step_bit_identical(rtw, name):
         kw = SCENES[name][1]
     cam = rtw.Camera(image_width=80, samples_per_pixel=6, max_depth=50, **kw).init()
     outs = {}
-    for v in ("0111", "3111", "7111", "3011", "3101", "3110"):  # fuse, Perlin / geometry / material LDS
+    for v in ("0111", "3111", "7111", "3011", "3101", "3110", "3111d", "0111d", "7111d"):
+        # fuse, Perlin / geometry / material LDS; d: the dynamic deal of iteration 0 and the tail (tuning.deal)
         lds = 127 & ~((32 if v[1] == "0" else 0) | (16 if v[2] == "0" else 0) | (8 if v[3] == "0" else 0))
-        world = rtw.World(arr, tuning={"fuse": int(v[0]), "lds": lds})
+        world = rtw.World(arr, tuning={"fuse": int(v[0]), "lds": lds, "deal": 1 if v.endswith("d") else 0})
         outs[v] = render_all(rtw, world, cam, 6, 5)
         world.close()
-    for k in ("3111", "7111", "3011", "3101", "3110"):
+    for k in ("3111", "7111", "3011", "3101", "3110", "3111d", "0111d", "7111d"):
         assert np.array_equal(outs["0111"], outs[k]), k
 
 

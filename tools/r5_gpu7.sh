@@ -8,3 +8,6 @@ rc=$?; tail -3 gpurun_out/r5/gpu7_tests.txt; [ $rc = 0 ] || exit $rc
 TAG=alt_deal1 bash tools/r5_shard_breakdown.sh c2 8 '{"deal": 1}' || exit 1
 TAG=alt_deal1 bash tools/r5_shard_breakdown.sh c2 4 '{"deal": 1}' || exit 1
 TAG=alt_deal1 bash tools/r5_shard_breakdown.sh c2 2 '{"deal": 1}' || exit 1
+mkdir -p gpurun_out/r5/walk
+RTW_LIB=build/rtw_trav.so timeout -k 10 300 python diag/run_walk_ceiling.py c2 gpurun_out/r5/walk/ceiling_c2.json > gpurun_out/r5/walk/c2.log 2>&1 || { tail gpurun_out/r5/walk/c2.log; exit 1; }
+cat gpurun_out/r5/walk/c2.log

@@ -44,6 +44,11 @@ def recompute(line):
     if hsrc:
         t = json.load(open(os.path.join(REPO, hsrc)))[r["hbm"]["kind"]]["traffic_bytes"]
         out["hbm_frac"] = t / launch_s / 1e9 / bench.HBM_PEAK_GBS
+    wk = r.get("walk") or {}
+    if wk.get("source") and wk.get("frac") is not None:  # the walk roofline (round 5)
+        c = json.load(open(os.path.join(REPO, wk["source"])))
+        assert c["build_id"] == line["build_id"], "walk ceiling of another build"
+        out["walk_frac"] = wk["device_steps_per_render"] / (wk["render_ms"] / 1e3) / c["ceiling"]
     return out
 
 
@@ -53,14 +58,14 @@ def main():
     got = recompute(line)
     ok = True
     pairs = (("valu_frac", r["frac"]), ("hbm_frac", r["hbm"]["frac"]), ("valu_lane_util", r["valu"]["lane_util"]),
-             ("valu_issue_busy", r["valu"]["issue_busy"]))
+             ("valu_issue_busy", r["valu"]["issue_busy"]), ("walk_frac", (r.get("walk") or {}).get("frac")))
     for k, v in pairs:
         if k not in got:
             continue
         good = v is not None and abs(got[k] - v) <= 5e-3 * max(abs(v), 1e-9) + 1e-4
         ok &= good
         print(f"{k:16s} line {v}  recomputed {got[k]:.4f}  {'ok' if good else 'MISMATCH'}")
-    for k in ("valu_frac", "hbm_frac"):
+    for k in ("valu_frac", "hbm_frac", "walk_frac"):
         if k in got and not got[k] <= 1.0:
             print(f"{k} > 1")
             ok = False

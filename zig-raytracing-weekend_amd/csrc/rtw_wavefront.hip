@@ -1131,9 +1131,47 @@ __device__ __forceinline__ void wf_tail_body(const rtw_launch& L, const rtw_wf& 
     f3 thr = mk(0, 0, 0), acc = mk(0, 0, 0);
     rtw_rng rng;
     rng.s = 0;
+    // Dynamic input (W.deal, rtw_tuning.deal): the wave claims 64-slot chunks of the input stripes from the
+    // launch's counter as its lanes run dry -- chunk g is chunk g / 256 of stripe g % 256 -- one claim issued a
+    // chunk ahead.  The tail's end is then set by its longest paths, not by a wave whose static share held more
+    // of them (C2 at 8 ranks: the tail was 1.3-1.5x its share of the 1-GPU tail).
+    const uint32_t* lens = W.len[it % 3u];
+    uint32_t gcur = 0, gnext = 0, limit = 0;  // wave-uniform; gnext lane 0's
+    if (W.deal) {
+        uint32_t mx = 0;
+        for (uint32_t k = lane; k < RTW_WF_STRIPES; k += 64u) mx = max(mx, lens[k * RTW_WF_LEN_STRIDE]);
+        for (int o = 32; o > 0; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
+        limit = ((mx + 63u) >> 6) * RTW_WF_STRIPES;
+        gcur = __builtin_amdgcn_readfirstlane(wf_claim(W.deal));
+        gnext = wf_claim(W.deal);
+        exhausted = gcur >= limit;
+    }
     for (;;) {
         const uint64_t need = __ballot(!active);
-        if (need && !exhausted) {
+        if (need && !exhausted && W.deal) {
+            const uint32_t m = cursor + (uint32_t)__popcll(need & lt);  // element m of the wave's claimed chunks
+            const uint32_t n_need = (uint32_t)__popcll(need);
+            const uint32_t gn = __builtin_amdgcn_readfirstlane(gnext);
+            if (!active) {
+                const uint32_t g = (m >> 6) == (cursor >> 6) ? gcur : gn;
+                const uint32_t s = g % RTW_WF_STRIPES, e = ((g / RTW_WF_STRIPES) << 6) | (m & 63u);
+                if (g < limit && e < lens[s * RTW_WF_LEN_STRIDE]) {
+                    float2 txy;
+                    const uint32_t slot = s * W.stripe_cap + e;
+                    r = wf_load_ray_it<FEAT>(L, S, slot, it, depth, txy, W.packed != 0u);
+                    uint64_t rs = 0;
+                    if (depth) wf_load_rest<FEAT>(L, S, slot, depth, txy, thr, acc, rs, pid, W.packed != 0u);
+                    rng.s = rs;
+                    active = depth != 0;
+                }
+            }
+            if (((cursor + n_need) >> 6) != (cursor >> 6)) {  // the current chunk is used up: the next one
+                gcur = gn;
+                gnext = wf_claim(W.deal);
+            }
+            cursor += n_need;
+            exhausted = gcur >= limit;
+        } else if (need && !exhausted) {
             const uint32_t m = cursor + (uint32_t)__popcll(need & lt);
             cursor += (uint32_t)__popcll(need);
             bool end = false;
@@ -1838,6 +1876,9 @@ void wf_run_fused(const rtw_launch& L, const rtw_wf& W0, hipStream_t st, int n_c
         bool done = false;
         if constexpr ((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING)) == 0) {
             if (clds && (L.wf_fuse & 2u)) {
+                rtw_wf Wd = W;  // the tail's input claims: counter 2 (iteration 0 took 0-1)
+                if (W.deal) Wd.deal = W.deal + 2;
+                const rtw_wf& W = Wd;
                 if (shape == 2)
                     hipLaunchKernelGGL((wf_tail_clds2<FEAT, 512>), dim3(tgrid[0]), dim3(512), clds, st, L, W, iters);
                 else if (shape == 3)
@@ -1853,16 +1894,18 @@ void wf_run_fused(const rtw_launch& L, const rtw_wf& W0, hipStream_t st, int n_c
                 done = true;
             }
         }
+        rtw_wf Wd = W;  // the tail's input claims: counter 2 (iteration 0 took 0-1)
+        if (W.deal) Wd.deal = W.deal + 2;
         if (!done && lds && (L.wf_fuse & 2u)) {  // the node array in LDS for the tail too
             thread_local uint32_t tl[2] = {0, 0};
             if (tl[1] != tdyn) {
                 tl[0] = wf_grid(wf_tail_lds<FEAT>, n_cu, tdyn);
                 tl[1] = (uint32_t)tdyn;
             }
-            hipLaunchKernelGGL(wf_tail_lds<FEAT>, dim3(tl[0]), dim3(256), tdyn, st, L, W, iters);
+            hipLaunchKernelGGL(wf_tail_lds<FEAT>, dim3(tl[0]), dim3(256), tdyn, st, L, Wd, iters);
             done = true;
         }
-        if (!done) wf_launch_tail<FEAT>(L, W, st, n_cu, gdyn, wtail, iters);
+        if (!done) wf_launch_tail<FEAT>(L, Wd, st, n_cu, gdyn, wtail, iters);
         RTW_TIME_END(T)
     }
     RTW_TIME_BEGIN(T, RTW_K_REDUCE)
@@ -1967,6 +2010,8 @@ void wf_run(const rtw_launch& L, const rtw_wf& W0, hipStream_t st, int n_cu, rtw
     }
     if (iters < L.max_depth) {
         RTW_TIME_BEGIN(T, RTW_K_TAIL)
+        rtw_wf Wd = W;  // the tail's input claims: counter 4 (iteration 0's trace and shade took 0-3)
+        if (W.deal) Wd.deal = W.deal + 4;
         if (lds && (L.wf_fuse & 2u)) {  // the node array (+ geometry) in LDS for the tail (smoke +5 %)
             thread_local uint32_t tl[2] = {0, 0};
             const size_t tdyn = tlds + L.shade_lds;  // wf_tail_lds stages the materials too
@@ -1974,9 +2019,9 @@ void wf_run(const rtw_launch& L, const rtw_wf& W0, hipStream_t st, int n_cu, rtw
                 tl[0] = wf_grid(wf_tail_lds<FEAT>, n_cu, tdyn);
                 tl[1] = (uint32_t)tdyn;
             }
-            hipLaunchKernelGGL(wf_tail_lds<FEAT>, dim3(tl[0]), dim3(256), tdyn, st, L, W, iters);
+            hipLaunchKernelGGL(wf_tail_lds<FEAT>, dim3(tl[0]), dim3(256), tdyn, st, L, Wd, iters);
         } else {
-            wf_launch_tail<FEAT>(L, W, st, n_cu, w2l, wtail, iters);
+            wf_launch_tail<FEAT>(L, Wd, st, n_cu, w2l, wtail, iters);
         }
         RTW_TIME_END(T)
     }
