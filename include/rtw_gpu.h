@@ -350,8 +350,12 @@ typedef struct rtw_tuning {
                                   1024-thread block per CU, 2 / 3 / 4 = two blocks of 512 / 640 / 768 threads
                                   (4 / 5 / 6 waves per SIMD) when the stage fits half the LDS; the 8-copy stage
                                   always runs one block (ABI 7) */
-    uint32_t deal;             /* wavefront iteration 0: 0 = runs of a tile's samples dealt round-robin over the
-                                  waves, 1 = waves claim runs of 16 from a counter as they finish (ABI 7) */
+    uint32_t deal;             /* how the wavefront's waves share work (ABI 7), bits: 1 = iteration 0's runs of 16
+                                  (the last chunks singly) claimed from a counter per stripe group as its waves
+                                  finish, instead of dealt round-robin; 2 = the tail's input chunks claimed from one
+                                  counter, or 4 = from a counter per stripe (its own group's waves), instead of
+                                  each wave's own list; 0 = all static.  Default 3.  A batch with fewer than 192
+                                  chunks of 64 paths per wave keeps the static shares unless bit 8 is set. */
 } rtw_tuning;
 
 void rtw_tuning_defaults(rtw_tuning* out);

@@ -344,10 +344,14 @@ def test_v1_knobs_invariant(rtw, book1, knob):
                                   {"bvh_orders": 4, "compact_nodes": 2, "fuse": 0},
                                   {"bvh_orders": 4, "compact_nodes": 2, "lds": 127 & ~2},
                                   {"bvh_orders": 4, "compact_nodes": 2, "tile_lists": 0},
-                                  {"bvh_orders": 8, "compact_nodes": 2}, {"deal": 1}, {"deal": 1, "fuse": 0},
-                                  {"deal": 1, "lds": 127 & ~2}, {"deal": 1, "wf_paths": 4096},
-                                  {"deal": 1, "wf_iters": 1}, {"deal": 1, "fuse": 0, "wf_iters": 2},
-                                  {"deal": 1, "lds": 127 & ~2, "fuse": 5}, {"deal": 1, "fuse": 1}])
+                                  {"bvh_orders": 8, "compact_nodes": 2}, {"deal": 9}, {"deal": 9, "fuse": 0},
+                                  {"deal": 9, "lds": 127 & ~2}, {"deal": 9, "wf_paths": 4096},
+                                  {"deal": 0}, {"deal": 0, "fuse": 0}, {"deal": 0, "lds": 127 & ~2, "fuse": 5},
+                                  {"deal": 9, "wf_iters": 1}, {"deal": 9, "fuse": 0, "wf_iters": 2},
+                                  {"deal": 9, "lds": 127 & ~2, "fuse": 5}, {"deal": 9, "fuse": 1},
+                                  {"deal": 13}, {"deal": 13, "fuse": 0}, {"deal": 13, "lds": 127 & ~2, "fuse": 5},
+                                  {"deal": 10}, {"deal": 11, "wf_iters": 1}, {"deal": 11}, {"deal": 11, "fuse": 0},
+                                  {"deal": 11, "wf_paths": 4096}, {"deal": 13, "wf_paths": 65536, "fuse": 0}])
 def test_wavefront_knobs_invariant(rtw, book1, knob):
     """Wavefront tuning (rtw_tuning: bounces before the tail kernel, batch size ->
     many batches, FMA vs reference slab test, LDS-staged nodes, SAH leaf runs of up

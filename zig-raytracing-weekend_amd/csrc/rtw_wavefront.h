@@ -66,10 +66,11 @@ struct rtw_wf {
     uint32_t sort_mask;   // the bucket key bits they use ((1 << rtw_tuning.sort_bits) - 1)
     uint32_t run_log2;    // iteration 0's tile runs: 2^run_log2 samples of one tile per run (wf_coherence)
     uint32_t packed;      // this render's queues hold the packed path state (wf_packed; set by wf_run*)
-    uint32_t* deal;       // dynamic dealing (rtw_tuning.deal): this launch's run and single-chunk counters (two,
-                          // zeroed per batch), or null for the static round-robin deal
+    uint32_t* deal;       // dynamic dealing (rtw_tuning.deal): this launch's counters (zeroed per batch), or null
+    uint32_t deal_mode;   // rtw_tuning.deal bits: 1 iteration 0, 2 the tail (one counter), 4 the tail (per stripe)
 };
-#define RTW_WF_DEAL_COUNTERS 64  // run counters per batch (one per launch that deals iteration 0)
+#define RTW_WF_DEAL_LAUNCH (2 * RTW_WF_STRIPES)  // counters of one launch dealing iteration 0 (runs, singles per group)
+#define RTW_WF_DEAL_COUNTERS (2 * RTW_WF_DEAL_LAUNCH + RTW_WF_STRIPES)  // per batch: split trace's, shade's, the tail's
 
 // bytes of device state per path (two slot sets + hit + ls; the batch's counters aside)
 #define RTW_WF_PATH_BYTES (2 * (4 * 16 + 8) + 8 + 12)

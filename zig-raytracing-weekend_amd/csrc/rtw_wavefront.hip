@@ -76,12 +76,16 @@ __device__ __forceinline__ void wf_path(const rtw_wf& W, uint32_t p, uint32_t& s
     q = (t << 6) | (p & 63u);
 }
 
-// Dynamic dealing of iteration 0 (W.deal, rtw_tuning.deal): a wave claims whole runs (RUN chunks of one tile,
-// tile-major) from the launch's counter W.deal[0] -- one atomic per run, issued a run ahead so its latency is
-// hidden -- until the runs run out.  Waves that draw cheap tiles (sky) take more runs, so the launch drains
-// evenly however few runs each wave gets: the runs keep their full 16 samples on small batches (a shard of a
-// multi-GPU render), where the static deal must shorten them to keep every wave's share even.  The last
-// 4 x (waves) chunks go one at a time (counter W.deal[1]), so the drain waits for a chunk, not a run.
+// Dynamic dealing of iteration 0 (W.deal, rtw_tuning.deal).  The waves of stripe group g (the waves w with
+// w % RTW_WF_STRIPES == g, whose survivors all go to stripe g) share the runs r = g + 256 k (RUN chunks of one
+// tile, tile-major): a wave claims the group's next k from W.deal[g] -- one atomic per run, issued a run ahead
+// so its latency is hidden -- until the group's runs run out.  Within the group the waves that draw cheap tiles
+// (sky) take more runs, so its 16-odd waves drain together however few runs each gets, and the runs keep their
+// full 16 samples on small batches (a shard of a multi-GPU render), where the static deal must shorten them to
+// keep every wave's share even.  Each group still takes exactly every 256th run, so a stripe receives the
+// survivors of the same share of the batch as under the static deal and its capacity holds (rtw_host.hip
+// stripe_cap; a global deal let one stripe's waves take more than their share and overflow it).  The last
+// 4 x (waves) chunks go one at a time, the group's every 256th (W.deal[256 + g]): the drain waits for a chunk.
 __device__ __forceinline__ uint32_t wf_claim(uint32_t* c) {  // lane 0 holds the claimed run
     uint32_t v = 0;
     if (__lane_id() == 0) v = atomicAdd(c, 1u);
@@ -103,14 +107,14 @@ struct WfIter {
         if (it == 0) {
             j = 0;
             step = 1;
-            if (W.deal) {
+            if (W.deal && (W.deal_mode & 1u)) {
                 const uint32_t nc = W.n_paths >> 6, tail = 4u * nw;
                 runs = nc > tail ? (nc - tail) >> W.run_log2 : 0u;
                 single = false;
-                run = __builtin_amdgcn_readfirstlane(wf_claim(W.deal));
-                next_run = wf_claim(W.deal);
+                run = __builtin_amdgcn_readfirstlane(wf_claim(W.deal + w % RTW_WF_STRIPES));
+                next_run = wf_claim(W.deal + w % RTW_WF_STRIPES);
                 kk = 0;
-                if (run >= runs) to_single(W);
+                if (grp(run) >= runs) to_single(W);
                 live0 = dyn_chunk(W);
             } else {
                 live0 = wf_chunk0(W, w, nw, 0, slot0);
@@ -126,13 +130,15 @@ struct WfIter {
         W_ = &W;
     }
     const rtw_wf* W_;
+    // the group's k-th run / single chunk (k claimed from the group's counter)
+    __device__ uint32_t grp(uint32_t k) const { return k * RTW_WF_STRIPES + w % RTW_WF_STRIPES; }
     __device__ void to_single(const rtw_wf& W) {
         single = true;
-        run = __builtin_amdgcn_readfirstlane(wf_claim(W.deal + 1));
-        next_run = wf_claim(W.deal + 1);
+        run = __builtin_amdgcn_readfirstlane(wf_claim(W.deal + RTW_WF_STRIPES + w % RTW_WF_STRIPES));
+        next_run = wf_claim(W.deal + RTW_WF_STRIPES + w % RTW_WF_STRIPES);
     }
     __device__ bool dyn_chunk(const rtw_wf& W) {
-        const uint32_t c = single ? (runs << W.run_log2) + run : (run << W.run_log2) + kk;
+        const uint32_t c = single ? (runs << W.run_log2) + grp(run) : (grp(run) << W.run_log2) + kk;
         slot0 = c << 6;
         return c < (W.n_paths >> 6);
     }
@@ -140,15 +146,15 @@ struct WfIter {
     __device__ void next() {
         j += step;
         if (it == 0) {
-            if (W_->deal) {
+            if (W_->deal && (W_->deal_mode & 1u)) {
                 if (single) {
                     run = __builtin_amdgcn_readfirstlane(next_run);
-                    next_run = wf_claim(W_->deal + 1);
+                    next_run = wf_claim(W_->deal + RTW_WF_STRIPES + w % RTW_WF_STRIPES);
                 } else if (++kk == (1u << W_->run_log2)) {
                     run = __builtin_amdgcn_readfirstlane(next_run);
-                    next_run = wf_claim(W_->deal);
+                    next_run = wf_claim(W_->deal + w % RTW_WF_STRIPES);
                     kk = 0;
-                    if (run >= runs) to_single(*W_);
+                    if (grp(run) >= runs) to_single(*W_);
                 }
                 live0 = dyn_chunk(*W_);
             } else {
@@ -1131,30 +1137,41 @@ __device__ __forceinline__ void wf_tail_body(const rtw_launch& L, const rtw_wf& 
     f3 thr = mk(0, 0, 0), acc = mk(0, 0, 0);
     rtw_rng rng;
     rng.s = 0;
-    // Dynamic input (W.deal, rtw_tuning.deal): the wave claims 64-slot chunks of the input stripes from the
-    // launch's counter as its lanes run dry -- chunk g is chunk g / 256 of stripe g % 256 -- one claim issued a
-    // chunk ahead.  The tail's end is then set by its longest paths, not by a wave whose static share held more
-    // of them (C2 at 8 ranks: the tail was 1.3-1.5x its share of the 1-GPU tail).
+    // Dynamic input (W.deal, rtw_tuning.deal): the wave claims 64-slot chunks of the input stripes from a
+    // counter as its lanes run dry, one claim issued a chunk ahead, so the tail's end is set by its longest
+    // paths, not by a wave whose static share held more of them (C4: tail 56.7 -> 45.3 ms).  Global (deal bit 1):
+    // chunk g of one counter is chunk g / 256 of stripe g % 256.  Per stripe (bit 2): the waves of stripe group
+    // s claim chunks of stripe s -- the stripe its own group's waves wrote, in the same XCD's L2 -- balancing
+    // within the group only.
     const uint32_t* lens = W.len[it % 3u];
     uint32_t gcur = 0, gnext = 0, limit = 0;  // wave-uniform; gnext lane 0's
-    if (W.deal) {
-        uint32_t mx = 0;
-        for (uint32_t k = lane; k < RTW_WF_STRIPES; k += 64u) mx = max(mx, lens[k * RTW_WF_LEN_STRIDE]);
-        for (int o = 32; o > 0; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
-        limit = ((mx + 63u) >> 6) * RTW_WF_STRIPES;
-        gcur = __builtin_amdgcn_readfirstlane(wf_claim(W.deal));
-        gnext = wf_claim(W.deal);
+    const bool dyn = W.deal && (W.deal_mode & 6u);
+    const bool per_stripe = (W.deal_mode & 4u) != 0;
+    const uint32_t own = wf_wave() % RTW_WF_STRIPES;
+    uint32_t* ctr = W.deal ? W.deal + (per_stripe ? own : 0u) : nullptr;
+    if (dyn) {
+        if (per_stripe) {
+            limit = (lens[own * RTW_WF_LEN_STRIDE] + 63u) >> 6;
+        } else {
+            uint32_t mx = 0;
+            for (uint32_t k = lane; k < RTW_WF_STRIPES; k += 64u) mx = max(mx, lens[k * RTW_WF_LEN_STRIDE]);
+            for (int o = 32; o > 0; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
+            limit = ((mx + 63u) >> 6) * RTW_WF_STRIPES;
+        }
+        gcur = __builtin_amdgcn_readfirstlane(wf_claim(ctr));
+        gnext = wf_claim(ctr);
         exhausted = gcur >= limit;
     }
     for (;;) {
         const uint64_t need = __ballot(!active);
-        if (need && !exhausted && W.deal) {
+        if (need && !exhausted && dyn) {
             const uint32_t m = cursor + (uint32_t)__popcll(need & lt);  // element m of the wave's claimed chunks
             const uint32_t n_need = (uint32_t)__popcll(need);
             const uint32_t gn = __builtin_amdgcn_readfirstlane(gnext);
             if (!active) {
                 const uint32_t g = (m >> 6) == (cursor >> 6) ? gcur : gn;
-                const uint32_t s = g % RTW_WF_STRIPES, e = ((g / RTW_WF_STRIPES) << 6) | (m & 63u);
+                const uint32_t s = per_stripe ? own : g % RTW_WF_STRIPES;
+                const uint32_t e = ((per_stripe ? g : g / RTW_WF_STRIPES) << 6) | (m & 63u);
                 if (g < limit && e < lens[s * RTW_WF_LEN_STRIDE]) {
                     float2 txy;
                     const uint32_t slot = s * W.stripe_cap + e;
@@ -1167,7 +1184,7 @@ __device__ __forceinline__ void wf_tail_body(const rtw_launch& L, const rtw_wf& 
             }
             if (((cursor + n_need) >> 6) != (cursor >> 6)) {  // the current chunk is used up: the next one
                 gcur = gn;
-                gnext = wf_claim(W.deal);
+                gnext = wf_claim(ctr);
             }
             cursor += n_need;
             exhausted = gcur >= limit;
@@ -1734,7 +1751,10 @@ rtw_wf wf_coherence(const rtw_wf& W, uint32_t nw, uint32_t sort_iters) {
     const uint32_t per_wave = nw ? (W.n_paths >> 6) / nw : 0u;
     uint32_t lg = 0;
     while (lg < 4 && (per_wave >> (lg + 1)) >= 64u) lg++;
-    if (W.deal) lg = 4;  // dynamic deal: the waves balance themselves, runs keep 16 samples of a tile
+    // the dynamic deal only where the waves have enough work to share: a small batch (simple_light, 137 chunks per
+    // wave) ran 6 % slower with it -- its tail's claims cost more than they balance (profiles/r5_deal/)
+    if (per_wave < RTW_WF_SORT_MIN_CHUNKS && !(C.deal_mode & 8u)) C.deal = nullptr;  // (bit 8: tests force it)
+    if (C.deal && (C.deal_mode & 1u)) lg = 4;  // dynamic deal: the waves balance themselves, runs keep 16 samples
     C.run_log2 = lg;
     C.sort_iters = per_wave >= RTW_WF_SORT_MIN_CHUNKS ? sort_iters : 0u;
     return C;
@@ -1844,7 +1864,7 @@ void wf_run_fused(const rtw_launch& L, const rtw_wf& W0, hipStream_t st, int n_c
     if (iters == 0) (void)hipMemsetAsync(W.ls, 0, (size_t)W.n_paths * sizeof(rtw_rgb), st);
     for (uint32_t it = 0; it < iters; it++) {
         RTW_TIME_BEGIN(T, RTW_K_TRACE)
-        Wt.deal = W.deal;  // (only iteration 0 deals from it: counters 0-1)
+        Wt.deal = W.deal;  // (only iteration 0 deals from it: counters 0 .. 511)
         if constexpr ((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING)) == 0) {
             if (clds) {
                 rtw_launch Lc = L;  // the materials are staged only when they fit
@@ -1876,8 +1896,8 @@ void wf_run_fused(const rtw_launch& L, const rtw_wf& W0, hipStream_t st, int n_c
         bool done = false;
         if constexpr ((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING)) == 0) {
             if (clds && (L.wf_fuse & 2u)) {
-                rtw_wf Wd = W;  // the tail's input claims: counter 2 (iteration 0 took 0-1)
-                if (W.deal) Wd.deal = W.deal + 2;
+                rtw_wf Wd = W;  // the tail's input claims: counter 512 (iteration 0 took 0 .. 511)
+                if (W.deal) Wd.deal = W.deal + RTW_WF_DEAL_LAUNCH;
                 const rtw_wf& W = Wd;
                 if (shape == 2)
                     hipLaunchKernelGGL((wf_tail_clds2<FEAT, 512>), dim3(tgrid[0]), dim3(512), clds, st, L, W, iters);
@@ -1894,8 +1914,8 @@ void wf_run_fused(const rtw_launch& L, const rtw_wf& W0, hipStream_t st, int n_c
                 done = true;
             }
         }
-        rtw_wf Wd = W;  // the tail's input claims: counter 2 (iteration 0 took 0-1)
-        if (W.deal) Wd.deal = W.deal + 2;
+        rtw_wf Wd = W;  // the tail's input claims: counter 512 (iteration 0 took 0 .. 511)
+        if (W.deal) Wd.deal = W.deal + RTW_WF_DEAL_LAUNCH;
         if (!done && lds && (L.wf_fuse & 2u)) {  // the node array in LDS for the tail too
             thread_local uint32_t tl[2] = {0, 0};
             if (tl[1] != tdyn) {
@@ -1936,7 +1956,7 @@ void wf_run(const rtw_launch& L, const rtw_wf& W0, hipStream_t st, int n_cu, rtw
     }
     rtw_wf W = wf_coherence(W0, g.shade * 4u, W0.sort_iters_split);  // the split kernels' queues
     W.packed = wf_packed<FEAT>() ? 1u : 0u;  // the split kernels (and their tail) use the packed state too
-    // dynamic deal: iteration 0's trace deals from counters 0-1, its shade from counters 2-3
+    // dynamic deal: iteration 0's trace deals from counters 0 .. 511, its shade from 512 .. 1023
     if (W0.deal) (void)hipMemsetAsync(W0.deal, 0, RTW_WF_DEAL_COUNTERS * 4, st);
     const uint32_t iters = L.max_depth < W.iters ? L.max_depth : W.iters;
     // iteration 0's trace and shade generate the camera rays themselves (wf_camera); with no
@@ -1944,7 +1964,7 @@ void wf_run(const rtw_launch& L, const rtw_wf& W0, hipStream_t st, int n_cu, rtw
     if (iters == 0) (void)hipMemsetAsync(W.ls, 0, (size_t)W.n_paths * sizeof(rtw_rgb), st);
     const rtw_wf Wt = iters ? wf_lists<FEAT>(L, W, st) : W;  // camera rays: iteration 0 of wf_trace (L1/L2)
     rtw_wf Ws0 = W;  // iteration 0's shade: its own counters
-    if (W.deal) Ws0.deal = W.deal + 2;
+    if (W.deal) Ws0.deal = W.deal + RTW_WF_DEAL_LAUNCH;
     const size_t w2l = wf_w2_lds<FEAT>(L);  // the two-wide walk's stacks (trace / tail through L1/L2)
     thread_local uint32_t wtrace[2] = {0, 0}, wtrace0[2] = {0, 0}, wtail[2] = {0, 0};
     const size_t lds_need = (size_t)L.n_nodes * L.n_orders * 32u;
@@ -2010,8 +2030,8 @@ void wf_run(const rtw_launch& L, const rtw_wf& W0, hipStream_t st, int n_cu, rtw
     }
     if (iters < L.max_depth) {
         RTW_TIME_BEGIN(T, RTW_K_TAIL)
-        rtw_wf Wd = W;  // the tail's input claims: counter 4 (iteration 0's trace and shade took 0-3)
-        if (W.deal) Wd.deal = W.deal + 4;
+        rtw_wf Wd = W;  // the tail's input claims: counter 1024 (iteration 0's trace and shade took 0 .. 1023)
+        if (W.deal) Wd.deal = W.deal + 2 * RTW_WF_DEAL_LAUNCH;
         if (lds && (L.wf_fuse & 2u)) {  // the node array (+ geometry) in LDS for the tail (smoke +5 %)
             thread_local uint32_t tl[2] = {0, 0};
             const size_t tdyn = tlds + L.shade_lds;  // wf_tail_lds stages the materials too
