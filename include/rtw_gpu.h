@@ -311,7 +311,8 @@ enum {  /* rtw_tuning.fuse */
 #define RTW_OTREE_NO_CULL 0x100u  /* rtw_tuning.object_tree */
 typedef struct rtw_tuning {
     uint32_t kernel;           /* rtw_kernel_kind (default WAVEFRONT) */
-    uint32_t bvh_orders;       /* 0 = auto (8 octant-ordered copies for SAH sphere scenes, else 1), 1, 4 or 8
+    uint32_t bvh_orders;       /* 0 = auto (SAH sphere scenes: 4 for small static untextured trees whose 4-copy
+                                  compact stage fits half the LDS -- Book-1 --, else 8; other scenes 1), 1, 4 or 8
                                   (4: copies ordered by the x and z signs, the walk takes y's near/far per ray;
                                   half the compact-LDS stage; ABI 7) */
     uint32_t sah_max_leaf;     /* spheres per SAH leaf (default 1) */
@@ -346,7 +347,7 @@ typedef struct rtw_tuning {
                                   SAH tree, default 90; | RTW_OTREE_NO_CULL: instance and medium leaves do not
                                   test the instance's world box before its transforms and members (ABI 5,
                                   formerly padding) */
-    uint32_t clds_shape;       /* compact-LDS kernels (fused step, tail) of a 4-copy tree: 0 = auto, 1 = one
+    uint32_t clds_shape;       /* compact-LDS kernels (fused step, tail) of a 4-copy tree: 0 = auto (= 4), 1 = one
                                   1024-thread block per CU, 2 / 3 / 4 = two blocks of 512 / 640 / 768 threads
                                   (4 / 5 / 6 waves per SIMD) when the stage fits half the LDS; the 8-copy stage
                                   always runs one block (ABI 7) */

@@ -226,6 +226,15 @@ int rtw_scene_create_ex(const rtw_scene_desc* d, int device, const rtw_tuning* t
     // lanes walking different orders stop executing them together (Cornell: -31 % with 8 orders).
     const bool objects = d->n_quads || d->n_instances || d->n_media;
     uint32_t orders = (d->bvh_mode == RTW_BVH_SAH && !objects) ? 8u : 1u;
+    // Round 5: small static untextured sphere trees (Book-1, C2 / C3) take 4 copies (x, z signs): their compact
+    // stage (+ materials) then fits half the LDS and the fused step and tail run two 768-thread blocks per CU, 6
+    // waves per SIMD (C2 +4.6 %, profiles/r5_stage/).  (A tree of ~2 nodes per sphere; the check is redone on the
+    // built tree by the launcher, which falls back to one block.)
+    const uint32_t sfeat = scene_features(d);
+    const size_t mat_b = (size_t)d->n_materials * sizeof(rtw_dev_material);
+    if (orders == 8 && !tu.bvh_orders && tu.compact_nodes == 1 && tu.fast_box && !(sfeat & ~RTW_F_CHECKER) &&
+        (2 * (size_t)d->n_spheres + 8) * 4 * 16 + mat_b <= RTW_WF_CLDS2_MAX)
+        orders = 4;
     // (object scenes keep one ordering: their hit ids carry an instance member where sphere scenes carry the copy)
     if (tu.bvh_orders) orders = (d->bvh_mode == RTW_BVH_SAH && !objects && tu.bvh_orders > 1) ? tu.bvh_orders : 1u;
     uint32_t n_hoisted = 0;
@@ -396,7 +405,7 @@ int rtw_scene_create_ex(const rtw_scene_desc* d, int device, const rtw_tuning* t
     L.images = dev + o_imgs;
     L.n_nodes = (uint32_t)n_nodes;
     L.n_orders = orders;
-    L.clds_shape = tu.clds_shape;
+    L.clds_shape = tu.clds_shape ? tu.clds_shape : 4u;  // auto: two 768-thread blocks where the stage fits
     ctx->wf_deal = tu.deal;
     L.cnode32 = cnode32 ? 1u : 0u;
     L.n_perlin = d->n_perlins;
