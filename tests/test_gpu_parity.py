@@ -330,7 +330,7 @@ def test_v1_knobs_invariant(rtw, book1, knob):
     assert np.array_equal(ref, got)
 
 
-@pytest.mark.parametrize("knob", [{"wf_iters": 1}, {"wf_iters": 50}, {"wf_paths": 4096}, {"fast_box": 0},
+@pytest.mark.parametrize("knob", [{"wf_iters": 1}, {"wf_iters": 9}, {"wf_iters": 50}, {"wf_paths": 4096}, {"fast_box": 0},
                                   {"lds": 127 & ~1}, {"sah_max_leaf": 4}, {"compact_nodes": 0}, {"lds": 127 & ~2},
                                   {"fuse": 0}, {"fuse": 1}, {"lds": 127 & ~4}, {"bvh_orders": 1}, {"tile_lists": 0}, {"tile_lists": 2}, {"tile_lists": 64},
                                   {"lds": 127 & ~2, "wide_walk": 0}, {"fuse": 5}, {"lds": 127 & ~2, "fuse": 5},

@@ -12,7 +12,8 @@ G2="SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_S
 G3="SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU2 SQ_ACTIVE_INST_FLAT SQ_INSTS_BRANCH SQ_WAVES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE GRBM_COUNT"
 G4="SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_INT64 SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_CVT SQ_IFETCH"
 i=0
-for grp in "${GROUPS_PMC_1:-$G1}" "${GROUPS_PMC_2:-$G2}" "${GROUPS_PMC_3:-$G3}" "${GROUPS_PMC_4:-$G4}"; do
+# GROUPS_PMC_<k> unset: the default group; set but empty: the group is skipped
+for grp in "${GROUPS_PMC_1-$G1}" "${GROUPS_PMC_2-$G2}" "${GROUPS_PMC_3-$G3}" "${GROUPS_PMC_4-$G4}"; do
   i=$((i + 1))
   [ -n "$grp" ] || continue
   echo "== g$i: $grp"

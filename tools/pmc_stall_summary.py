@@ -117,6 +117,19 @@ def main():
         e = derive(tot)
         print("  all:      " + "  ".join(f"{n} {v:.3f}" if abs(v) < 1e4 else f"{n} {v:.4g}" for n, v in e.items()))
         out[k] = {"kernels": sorted(kernels[k]), "launches": rows, "total": {"counters": dict(tot), "derived": e}}
+    # the build and workload the passes ran (bench.py's line in each group's log): every group must agree
+    builds = set()
+    for g in sorted(glob.glob(os.path.join(d, "g*.log"))):
+        for line in open(g, errors="replace"):
+            if line.startswith("{"):
+                try:
+                    x = json.loads(line)
+                    builds.add((x["roofline"]["valu"]["build_id"], x["config"]["config_id"]))
+                except (ValueError, KeyError):
+                    pass
+    out["_build"] = {"build_id": sorted(b for b, _ in builds), "workload": sorted(w for _, w in builds),
+                     "consistent": len(builds) == 1}
+    print("build", out["_build"])
     json.dump(out, open(os.path.join(d, "pmc_stall.json"), "w"), indent=1, sort_keys=True)
 
 

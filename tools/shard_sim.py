@@ -17,7 +17,8 @@ import torch  # noqa: E402
 pkg = importlib.import_module("zig-raytracing-weekend_amd")
 cfg_name = sys.argv[1] if len(sys.argv) > 1 else "c2"
 spp_override = int(sys.argv[2]) if len(sys.argv) > 2 else 0
-rpb = int(sys.argv[3]) if len(sys.argv) > 3 else 16
+# default: bench.py's split (8-row blocks, balanced residual rows, RTW_ROWS_BALANCED); 0x80000008 = the same explicitly
+rpb = int(sys.argv[3], 0) if len(sys.argv) > 3 else 8 | pkg._abi.RTW_ROWS_BALANCED
 ns = [int(v) for v in sys.argv[4].split(",")] if len(sys.argv) > 4 else [1, 2, 4, 8]
 cfg = pkg.configs.CONFIGS[cfg_name]
 # RTW_SHARD_TUNING='{"wf_iters": 16}': the rtw_tuning fields to override (every setting renders the same image)
@@ -49,7 +50,8 @@ for n in ns:
     slow = max(times)
     if base is None:
         base = slow
-    print(json.dumps({"config": cfg_name, "n": n, "rows_per_block": rpb, "rank_ms": [round(t * 1e3, 2) for t in times],
+    print(json.dumps({"config": cfg_name, "n": n, "rows_per_block": rpb & 0xFFFF,
+                      "balanced": bool(rpb & pkg._abi.RTW_ROWS_BALANCED), "build_id": pkg.lib().rtw_build_id().decode(), "rank_ms": [round(t * 1e3, 2) for t in times],
                       "max_ms": round(slow * 1e3, 2), "pred_speedup": round(base / slow, 3),
                       "pred_Msamples_s": round(W * H * spp / slow / 1e6, 1)}), flush=True)
 world.close()

@@ -149,7 +149,7 @@ void rtw_tuning_defaults(rtw_tuning* t) {
     t->fast_reject = 1;
     t->lds = RTW_LDS_ALL;
     t->fuse = RTW_FUSE_STEP | RTW_FUSE_TAIL_LDS;
-    t->wf_iters = 9;  // C2 at 9/12/16/24 iterations: 7.02/7.00/6.92/6.78x at 8 ranks; 1 GPU flat
+    t->wf_iters = 0;  // auto: 4, or 9 for image-textured scenes (profiles/r5_iters/)
     t->mega_shade_min = 48;  // tuned on C2: 8..64 -> 48 best
     t->mega_waves = 1;
     t->mega_tile_order = 1;
@@ -179,7 +179,7 @@ int rtw_scene_create_ex(const rtw_scene_desc* d, int device, const rtw_tuning* t
         return fail(RTW_E_INVALID, "tuning.bvh_orders must be 0, 1, 4 or 8");
     if (tu.clds_shape > 4) return fail(RTW_E_INVALID, "tuning.clds_shape must be 0..4");
     if (tu.deal > 15 || (tu.deal & 6u) == 6u) return fail(RTW_E_INVALID, "tuning.deal: bits 1 | 2 or 4 | 8");
-    if (tu.wf_iters < 1 || tu.wf_iters > RTW_WF_MAX_ITERS) return fail(RTW_E_INVALID, "tuning.wf_iters out of range");
+    if (tu.wf_iters > RTW_WF_MAX_ITERS) return fail(RTW_E_INVALID, "tuning.wf_iters out of range");
     if ((tu.object_tree & 0xFFu) > 100 || (tu.object_tree & ~(0xFFu | RTW_OTREE_NO_CULL)))
         return fail(RTW_E_INVALID, "tuning.object_tree: 0..100 [| RTW_OTREE_NO_CULL]");
     if (tu.sort_bits > RTW_WF_BUCKET_BITS) return fail(RTW_E_INVALID, "tuning.sort_bits out of range");
@@ -263,9 +263,15 @@ int rtw_scene_create_ex(const rtw_scene_desc* d, int device, const rtw_tuning* t
     std::vector<rtw_cnode> w2;
     std::vector<uint32_t> w2leaf;
     uint32_t w2_stack = 0;
+#ifdef RTW_WIDE4
+    if (!cnodes.empty() && !cnode32 && tu.wide_walk && tu.sah_max_leaf <= 1 &&
+        !rtw_wide4_nodes(ctx->nodes_host, (uint32_t)(ctx->nodes_host.size() / orders), w2, w2leaf, &w2_stack))
+        w2.clear();
+#else
     if (!cnodes.empty() && !cnode32 && tu.wide_walk && tu.sah_max_leaf <= 1 &&
         !rtw_wide2_nodes(ctx->nodes_host, (uint32_t)(ctx->nodes_host.size() / orders), w2, w2leaf, &w2_stack))
         w2.clear();
+#endif
     if (w2_stack > RTW_W2_STACK_MAX) w2.clear();
 
     // Blob layout (each section 256-B aligned): nodes | cvec | spheres | quads | members | instances | media |
@@ -424,7 +430,10 @@ int rtw_scene_create_ex(const rtw_scene_desc* d, int device, const rtw_tuning* t
             cap = std::min<uint64_t>(cap, (uint64_t)(0.35 * (double)free_b) / RTW_WF_PATH_BYTES);
         ctx->wf_max_paths = tu.wf_paths ? tu.wf_paths : std::max<uint64_t>(cap, 1u << 20);
     }
-    ctx->wf_iters = tu.wf_iters;
+    // Round 5, with the dynamic tail (deal bit 2): fewer iterations before the tail pay everywhere but on
+    // image-textured scenes -- same-box A/B, 9 -> 4 iterations: C2 +3.7 %, C4 +3.3 %, Cornell +6.8 %, smoke
+    // +1.2 %, simple_light +1.9 %; C5 -3.5 % (profiles/r5_iters/).
+    ctx->wf_iters = tu.wf_iters ? tu.wf_iters : (sfeat & RTW_F_IMAGE) ? 9u : 4u;
     ctx->wf_sort_iters = tu.sort_iters;
     ctx->wf_sort_iters_split = tu.sort_iters_split;
     ctx->wf_sort_mask = (1u << tu.sort_bits) - 1u;

@@ -193,6 +193,8 @@ bool rtw_compact_nodes(const std::vector<rtw_node>& nodes, uint32_t orders, std:
 // sphere SAH trees (rtw_bvh.hip rtw_wide2_nodes); false: not encodable (leaf runs, fp16 range)
 bool rtw_wide2_nodes(const std::vector<rtw_node>& nodes, uint32_t n_per, std::vector<rtw_cnode>& out,
                      std::vector<uint32_t>& leaf_id, uint32_t* max_stack);
+bool rtw_wide4_nodes(const std::vector<rtw_node>& nodes, uint32_t n_per, std::vector<rtw_cnode>& out,
+                     std::vector<uint32_t>& leaf_id, uint32_t* max_stack);
 
 // hoist (SAH sphere scenes): emit spheres whose box dwarfs the rest ahead of the tree (*n_hoisted of them)
 // flatten_pct (SAH trees): inner nodes with >= that % of the area of the node above are not emitted

@@ -656,6 +656,108 @@ __device__ __forceinline__ int traverse_wide2(const rtw_launch& L, const Ray& r,
     return hit < 0 ? hit : (int)L.w2leaf[hit];
 }
 
+#ifdef RTW_WIDE4
+// The four-wide form of the stack walk (rtw_bvh.hip rtw_wide4_nodes, -DRTW_WIDE4 builds): one 64-B record
+// per step, its leaf slots first (the wave runs the sphere test as often as its lanes' most leaves), then
+// up to 4 boxes; the nearest entered child is walked next and the others pushed.  Same superset argument
+// as traverse_wide2.
+template <bool COUNT>
+__device__ __forceinline__ int traverse_wide4(const rtw_launch& L, const Ray& r, float& t_out, Counters& cnt) {
+    extern __shared__ uint32_t wf_w2_stack[];
+    uint32_t* __restrict__ stk = wf_w2_stack + threadIdx.x;
+    const RayTrav rt = ray_trav(r, true);
+    constexpr uint32_t KEEP = 0x03020100u, SWAP = 0x01000302u;
+    const uint32_t sx = rt.inv.x < 0.0f ? SWAP : KEEP, sy = rt.inv.y < 0.0f ? SWAP : KEEP,
+                   sz = rt.inv.z < 0.0f ? SWAP : KEEP;
+    const uint4* __restrict__ wn = L.w2nodes;
+    float closest = kInf;
+    int hit = -1;
+    uint32_t node = 0, sp = 0;
+    for (;;) {
+        uint4 s[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) s[k] = wn[4u * node + k];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            if (s[k].w & RTW_LEAF_BIT) {
+                if constexpr (COUNT) cnt.leaves++;
+                sphere_leaf(L, r, rt, mk(ubits(s[k].x), ubits(s[k].y), ubits(s[k].z)), ubits(s[k].w & ~RTW_LEAF_BIT),
+                            4u * node + k, closest, hit);
+            }
+        }
+#ifdef RTW_WIDE4_SORT
+        // entered children sorted by entry distance, farthest first (a 5-exchange network; others key -inf):
+        // the far ones are pushed, so the stack pops them nearest first
+        float key[4];
+        uint32_t w[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            float lo, hi;
+            w2_box(s[k], rt, sx, sy, sz, closest, lo, hi);
+            const bool e = (s[k].w >> 30) == 0u && !(hi <= lo);
+            if constexpr (COUNT) cnt.nodes += (s[k].w >> 30) == 0u ? 1u : 0u;
+            key[k] = e ? lo : -kInf;
+            w[k] = s[k].w;
+        }
+        auto xchg = [&](int a, int b) {
+            const bool sw = key[a] < key[b];
+            const float ka = key[a];
+            const uint32_t wa = w[a];
+            key[a] = sw ? key[b] : ka;
+            key[b] = sw ? ka : key[b];
+            w[a] = sw ? w[b] : wa;
+            w[b] = sw ? wa : w[b];
+        };
+        xchg(0, 1);
+        xchg(2, 3);
+        xchg(0, 2);
+        xchg(1, 3);
+        xchg(1, 2);
+        const uint32_t n_in = (key[0] > -kInf ? 1u : 0u) + (key[1] > -kInf ? 1u : 0u) + (key[2] > -kInf ? 1u : 0u) +
+                              (key[3] > -kInf ? 1u : 0u);
+        const bool any = n_in != 0u;
+        uint32_t nxt = n_in == 4u ? w[3] : n_in == 3u ? w[2] : n_in == 2u ? w[1] : w[0];
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+            const bool push = (uint32_t)k + 1u < n_in;
+            if (push) stk[sp * 256u] = w[k];
+            sp += push ? 1u : 0u;
+        }
+#else
+        float best = kInf;
+        uint32_t nxt = 0;
+        bool in[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            float lo, hi;
+            w2_box(s[k], rt, sx, sy, sz, closest, lo, hi);
+            in[k] = (s[k].w >> 30) == 0u && !(hi <= lo);
+            if constexpr (COUNT) cnt.nodes += (s[k].w >> 30) == 0u ? 1u : 0u;
+            const bool nearer = in[k] && lo < best;
+            best = nearer ? lo : best;
+            nxt = nearer ? s[k].w : nxt;
+        }
+        const bool any = in[0] || in[1] || in[2] || in[3];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const bool push = in[k] && s[k].w != nxt;
+            if (push) stk[sp * 256u] = s[k].w;
+            sp += push ? 1u : 0u;
+        }
+#endif
+        const bool done = !any && sp == 0;
+        if (!any && !done) {
+            sp--;
+            nxt = stk[sp * 256u];
+        }
+        if (done) break;
+        node = nxt;
+    }
+    t_out = closest;
+    return hit < 0 ? hit : (int)L.w2leaf[hit];
+}
+#endif
+
 // the walk of a static sphere scene through L1/L2: two-wide when the records exist and the FMA slab
 // test is allowed (its fp16 boxes are supersets only of boxes padded for |o| <= 7 * extent: make_launch
 // clears fast_box for a farther camera, and tuning.fast_box = 0 asks for the exact aabb.zig walk)
@@ -664,7 +766,11 @@ __device__ __forceinline__ int wf_traverse_global(const rtw_launch& L, const Ray
                                                   uint64_t mkey) {
     if constexpr ((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING)) == 0) {
         if (L.w2nodes && L.fast_box)
+#ifdef RTW_WIDE4
+            return L.counters ? traverse_wide4<true>(L, r, t, cnt) : traverse_wide4<false>(L, r, t, cnt);
+#else
             return L.counters ? traverse_wide2<true>(L, r, t, cnt) : traverse_wide2<false>(L, r, t, cnt);
+#endif
     }
     return traverse<FEAT>(L.nodes, L, r, t, cnt, mkey);
 }
