@@ -355,8 +355,11 @@ typedef struct rtw_tuning {
                                   (the last chunks singly) claimed from a counter per stripe group as its waves
                                   finish, instead of dealt round-robin; 2 = the tail's input chunks claimed from one
                                   counter, or 4 = from a counter per stripe (its own group's waves), instead of
-                                  each wave's own list; 0 = all static.  Default 3.  A batch with fewer than 192
-                                  chunks of 64 paths per wave keeps the static shares unless bit 8 is set. */
+                                  each wave's own list; 16 = the fused step's iterations >= 1 claim their stripe's
+                                  chunks from a counter per stripe group; 32 = iteration 0's last 16 x (waves)
+                                  chunks go singly (else the last 4 x); 0 = all static.  A batch with fewer than
+                                  192 chunks of 64 paths per wave keeps the static shares unless bit 8 is set.
+                                  Default 59 = 1 | 2 | 8 | 16 | 32. */
 } rtw_tuning;
 
 void rtw_tuning_defaults(rtw_tuning* out);

@@ -56,7 +56,7 @@ def test_tuning_defaults_and_no_environment_knobs(rtw):
     assert (t.kernel, t.bvh_orders, t.sah_max_leaf, t.compact_nodes, t.fast_box, t.fast_reject) == (0, 0, 1, 1, 1, 1)
     assert t.lds == A.RTW_LDS_ALL and t.fuse == A.RTW_FUSE_STEP | A.RTW_FUSE_TAIL_LDS and t.wf_iters == 0
     assert t.wf_paths == 0 and (t.hoist, t.sort_iters, t.sort_bits, t.sort_iters_split) == (1, 3, 4, 1)
-    assert t.object_tree == 90 and (t.clds_shape, t.deal) == (0, 3)
+    assert t.object_tree == 90 and (t.clds_shape, t.deal) == (0, 59)
     syms = subprocess.check_output(["nm", "-D", "--undefined-only", rtw._abi.LIB_PATH], text=True)
     assert "getenv" not in syms, "the product library reads the environment"
 

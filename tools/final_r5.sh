@@ -19,7 +19,7 @@ if [ "$PART" = pmc ]; then
     cp "$O/pmc_$c/valu/pmc_valu.json" "$O/pmc_valu_${c}_sah.json" && cp "$O/pmc_$c/traffic/pmc_traffic.json" "$O/pmc_traffic_${c}_sah.json" || exit 1
     echo "pmc $c: $(grep '^build' "$O/pmc_$c/valu/summary.txt") / $(grep '^build' "$O/pmc_$c/traffic/summary.txt")"
   done
-  for n in ${SHARD_NS:-2 4 8}; do
+  for n in ${SHARD_NS-2 4 8}; do
     bash tools/pmc_shard.sh c2 $n 0 > "$O/pmc_shard_n$n.txt" 2>&1 || { tail "$O/pmc_shard_n$n.txt"; exit 1; }
     cp profiles/pmc_valu_c2_sah_n${n}_r0.json profiles/pmc_traffic_c2_sah_n${n}_r0.json "$O/" || exit 1
     echo "shard pass n$n done"

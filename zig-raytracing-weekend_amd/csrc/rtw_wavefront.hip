@@ -85,7 +85,10 @@ __device__ __forceinline__ void wf_path(const rtw_wf& W, uint32_t p, uint32_t& s
 // keep every wave's share even.  Each group still takes exactly every 256th run, so a stripe receives the
 // survivors of the same share of the batch as under the static deal and its capacity holds (rtw_host.hip
 // stripe_cap; a global deal let one stripe's waves take more than their share and overflow it).  The last
-// 4 x (waves) chunks go one at a time, the group's every 256th (W.deal[256 + g]): the drain waits for a chunk.
+// 4 x (waves) chunks -- 16 x with deal bit 32, as long as a run, so that a wave that took the last run does not
+// leave the others idle -- go one at a time, the group's every 256th (W.deal[256 + g]).  Deal bit 16: iteration
+// it >= 1's waves of group g claim the chunks of stripe g from one counter (W.deal_it[g]) instead of a fixed
+// stride; their survivors still go to stripe g, so the capacities hold as before.
 __device__ __forceinline__ uint32_t wf_claim(uint32_t* c) {  // lane 0 holds the claimed run
     uint32_t v = 0;
     if (__lane_id() == 0) v = atomicAdd(c, 1u);
@@ -108,7 +111,7 @@ struct WfIter {
             j = 0;
             step = 1;
             if (W.deal && (W.deal_mode & 1u)) {
-                const uint32_t nc = W.n_paths >> 6, tail = 4u * nw;
+                const uint32_t nc = W.n_paths >> 6, tail = (W.deal_mode & 32u) ? nw << W.run_log2 : 4u * nw;
                 runs = nc > tail ? (nc - tail) >> W.run_log2 : 0u;
                 single = false;
                 run = __builtin_amdgcn_readfirstlane(wf_claim(W.deal + w % RTW_WF_STRIPES));
@@ -126,6 +129,10 @@ struct WfIter {
             base = W.len[it % 3u][s * RTW_WF_LEN_STRIDE];  // slots used in the stripe
             n = (base + 63u) >> 6;
             off = s * W.stripe_cap;
+            if (W.deal_it) {  // deal bit 16: the group's waves claim stripe s's chunks, one claim issued ahead
+                j = __builtin_amdgcn_readfirstlane(wf_claim(W.deal_it + s));
+                next_run = wf_claim(W.deal_it + s);
+            }
         }
         W_ = &W;
     }
@@ -144,6 +151,11 @@ struct WfIter {
     }
     __device__ bool more() const { return it == 0 ? live0 : j < n; }
     __device__ void next() {
+        if (it != 0 && W_->deal_it) {
+            j = __builtin_amdgcn_readfirstlane(next_run);
+            next_run = wf_claim(W_->deal_it + w % RTW_WF_STRIPES);
+            return;
+        }
         j += step;
         if (it == 0) {
             if (W_->deal && (W_->deal_mode & 1u)) {
@@ -1971,6 +1983,9 @@ void wf_run_fused(const rtw_launch& L, const rtw_wf& W0, hipStream_t st, int n_c
     for (uint32_t it = 0; it < iters; it++) {
         RTW_TIME_BEGIN(T, RTW_K_TRACE)
         Wt.deal = W.deal;  // (only iteration 0 deals from it: counters 0 .. 511)
+        // deal bit 16: iteration it >= 1 claims its stripes' chunks from counters of its own
+        Wt.deal_it = (W.deal && (W.deal_mode & 16u) && it) ? W.deal + RTW_WF_DEAL_COUNTERS0 + it * RTW_WF_STRIPES
+                                                           : nullptr;
         if constexpr ((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING)) == 0) {
             if (clds) {
                 rtw_launch Lc = L;  // the materials are staged only when they fit
@@ -2062,6 +2077,7 @@ void wf_run(const rtw_launch& L, const rtw_wf& W0, hipStream_t st, int n_cu, rtw
     }
     rtw_wf W = wf_coherence(W0, g.shade * 4u, W0.sort_iters_split);  // the split kernels' queues
     W.packed = wf_packed<FEAT>() ? 1u : 0u;  // the split kernels (and their tail) use the packed state too
+    const rtw_wf W1 = W;
     // dynamic deal: iteration 0's trace deals from counters 0 .. 511, its shade from 512 .. 1023
     if (W0.deal) (void)hipMemsetAsync(W0.deal, 0, RTW_WF_DEAL_COUNTERS * 4, st);
     const uint32_t iters = L.max_depth < W.iters ? L.max_depth : W.iters;
@@ -2098,6 +2114,13 @@ void wf_run(const rtw_launch& L, const rtw_wf& W0, hipStream_t st, int n_cu, rtw
     }
     for (uint32_t it = 0; it < iters; it++) {
         RTW_TIME_BEGIN(T, RTW_K_TRACE)
+        // deal bit 16: iteration it >= 1's trace and shade claim their stripes' chunks from counters of their own
+        rtw_wf W = W1;
+        rtw_wf Ws = W1;
+        if (W1.deal && (W1.deal_mode & 16u) && it) {
+            W.deal_it = W1.deal + RTW_WF_DEAL_COUNTERS0 + it * RTW_WF_STRIPES;
+            Ws.deal_it = W1.deal + RTW_WF_DEAL_SHADE + it * RTW_WF_STRIPES;
+        }
         if constexpr ((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING)) == 0) {
             if (clds_grid) {
                 const int cn = L.cnode32 ? CN_F32_4 : L.n_orders == 4 ? CN_F16_4 : CN_F16_8;
@@ -2131,7 +2154,7 @@ void wf_run(const rtw_launch& L, const rtw_wf& W0, hipStream_t st, int n_cu, rtw
                                st, L, Ws0, it);
         else
             hipLaunchKernelGGL(wf_shade<FEAT>, dim3(g.shade), dim3(256), (FEAT & RTW_F_GEOM) ? L.geom_lds : 0u, st, L,
-                               W, it);
+                               Ws, it);
         RTW_TIME_END(T)
     }
     if (iters < L.max_depth) {
