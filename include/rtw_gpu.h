@@ -357,9 +357,10 @@ typedef struct rtw_tuning {
                                   counter, or 4 = from a counter per stripe (its own group's waves), instead of
                                   each wave's own list; 16 = the fused step's iterations >= 1 claim their stripe's
                                   chunks from a counter per stripe group; 32 = iteration 0's last 16 x (waves)
-                                  chunks go singly (else the last 4 x); 0 = all static.  A batch with fewer than
-                                  192 chunks of 64 paths per wave keeps the static shares unless bit 8 is set.
-                                  Default 59 = 1 | 2 | 8 | 16 | 32. */
+                                  chunks go singly (else the last 4 x); 64 = the tail in two launches (7 bounces
+                                  per path, the live paths requeued, then the rest: measured slower, an A/B knob);
+                                  0 = all static.  A batch with fewer than 192 chunks of 64 paths per wave keeps
+                                  the static shares unless bit 8 is set.  Default 59 = 1 | 2 | 8 | 16 | 32. */
 } rtw_tuning;
 
 void rtw_tuning_defaults(rtw_tuning* out);

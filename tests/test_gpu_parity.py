@@ -353,7 +353,10 @@ def test_v1_knobs_invariant(rtw, book1, knob):
                                   {"deal": 10}, {"deal": 11, "wf_iters": 1}, {"deal": 11}, {"deal": 11, "fuse": 0},
                                   {"deal": 11, "wf_paths": 4096}, {"deal": 13, "wf_paths": 65536, "fuse": 0},
                                   {"deal": 59}, {"deal": 27, "lds": 127 & ~2, "fuse": 5}, {"deal": 57, "wf_iters": 9}, {"deal": 51},
-                                  {"deal": 59, "fuse": 0}, {"deal": 59, "lds": 127 & ~2, "fuse": 0}, {"deal": 51, "fuse": 0, "wf_iters": 3}])
+                                  {"deal": 59, "fuse": 0}, {"deal": 59, "lds": 127 & ~2, "fuse": 0}, {"deal": 51, "fuse": 0, "wf_iters": 3},
+                                  {"deal": 123}, {"deal": 123, "fuse": 0}, {"deal": 123, "lds": 127 & ~2, "fuse": 0},
+                                  {"deal": 123, "wf_paths": 4096}, {"deal": 64}, {"deal": 64, "fuse": 0}, {"deal": 69, "wf_iters": 2},
+                                  {"deal": 123, "wf_iters": 1}, {"deal": 123, "lds": 127 & ~2, "fuse": 5}])
 def test_wavefront_knobs_invariant(rtw, book1, knob):
     """Wavefront tuning (rtw_tuning: bounces before the tail kernel, batch size ->
     many batches, FMA vs reference slab test, LDS-staged nodes, SAH leaf runs of up

@@ -180,7 +180,8 @@ int rtw_scene_create_ex(const rtw_scene_desc* d, int device, const rtw_tuning* t
     if (tu.bvh_orders != 0 && tu.bvh_orders != 1 && tu.bvh_orders != 4 && tu.bvh_orders != 8)
         return fail(RTW_E_INVALID, "tuning.bvh_orders must be 0, 1, 4 or 8");
     if (tu.clds_shape > 4) return fail(RTW_E_INVALID, "tuning.clds_shape must be 0..4");
-    if (tu.deal > 63 || (tu.deal & 6u) == 6u) return fail(RTW_E_INVALID, "tuning.deal: bits 1 | 2 or 4 | 8 | 16 | 32");
+    if (tu.deal > 127 || (tu.deal & 6u) == 6u)
+        return fail(RTW_E_INVALID, "tuning.deal: bits 1 | 2 or 4 | 8 | 16 | 32 | 64");
     if (tu.wf_iters > RTW_WF_MAX_ITERS) return fail(RTW_E_INVALID, "tuning.wf_iters out of range");
     if ((tu.object_tree & 0xFFu) > 100 || (tu.object_tree & ~(0xFFu | RTW_OTREE_NO_CULL)))
         return fail(RTW_E_INVALID, "tuning.object_tree: 0..100 [| RTW_OTREE_NO_CULL]");
@@ -677,7 +678,8 @@ int run_wavefront(rtw_ctx* ctx, rtw_launch L, hipStream_t stream, rtw_timer* T) 
     uint32_t* deal = reinterpret_cast<uint32_t*>(take(RTW_WF_DEAL_COUNTERS * 4));
     W.deal = ctx->wf_deal ? deal : nullptr;
     W.deal_mode = ctx->wf_deal;
-    W.deal_it = nullptr;  // set per fused-step launch (deal bit 16)
+    W.deal_it = nullptr;  // set per launch (deal bit 16)
+    W.tail_budget = 0;    // set per tail launch (deal bit 64)
     W.n_pix = (uint32_t)n_pix;
     W.iters = ctx->wf_iters;
     W.sort_iters = ctx->wf_sort_iters;

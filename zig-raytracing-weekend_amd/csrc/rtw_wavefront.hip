@@ -1250,6 +1250,7 @@ __device__ __forceinline__ void wf_tail_body(const rtw_launch& L, const rtw_wf& 
     const rtw_wf_set& S = W.set[it & 1u];
     Counters cnt;
     uint32_t cursor = 0, pid = 0, depth = 0;
+    uint32_t nb = 0, src = 0;  // deal bit 64: bounces of this path in this launch, the stripe it came from
     bool active = false, exhausted = false;
     Ray r;
     f3 thr = mk(0, 0, 0), acc = mk(0, 0, 0);
@@ -1298,6 +1299,8 @@ __device__ __forceinline__ void wf_tail_body(const rtw_launch& L, const rtw_wf& 
                     if (depth) wf_load_rest<FEAT>(L, S, slot, depth, txy, thr, acc, rs, pid, W.packed != 0u);
                     rng.s = rs;
                     active = depth != 0;
+                    nb = 0;
+                    src = s;
                 }
             }
             if (((cursor + n_need) >> 6) != (cursor >> 6)) {  // the current chunk is used up: the next one
@@ -1320,6 +1323,8 @@ __device__ __forceinline__ void wf_tail_body(const rtw_launch& L, const rtw_wf& 
                 if (depth) wf_load_rest<FEAT>(L, S, slot, depth, txy, thr, acc, rs, pid, W.packed != 0u);
                 rng.s = rs;
                 active = depth != 0;
+                nb = 0;
+                src = slot / W.stripe_cap;
             }
         }
         if (!__ballot(active)) {
@@ -1402,6 +1407,15 @@ __device__ __forceinline__ void wf_tail_body(const rtw_launch& L, const rtw_wf& 
         }
         if (active && done) {
             W.ls[pid] = rtw_rgb{acc.x, acc.y, acc.z};
+            active = false;
+        }
+        // deal bit 64, first tail launch: a path alive after W.tail_budget bounces here goes back to the stripe it
+        // came from (its outputs never outnumber its inputs), in the other set, for the second launch -- the
+        // state the fused shade stores after a bounce: the next ray, its remaining depth, throughput, RNG, id
+        if (W.tail_budget && active && !done && ++nb == W.tail_budget) {
+            const uint32_t e = atomicAdd(&W.len[(it + 1u) % 3u][src * RTW_WF_LEN_STRIDE], 1u);
+            wf_store_path<FEAT>(W.set[(it + 1u) & 1u], src * W.stripe_cap + e, r, depth, thr, rng.s, pid, acc,
+                                W.packed != 0u);
             active = false;
         }
     }
@@ -1832,6 +1846,27 @@ void wf_launch_tail(const rtw_launch& L, const rtw_wf& W, hipStream_t st, int n_
                            W, it);
 }
 
+// The tail of a batch: one launch over iteration iters' queue, or (deal bit 64) two -- RTW_WF_TAIL_BUDGET bounces
+// per path with the live paths requeued into the stripes they came from, then the rest to completion.  In the
+// second launch the longest paths start with the GPU nearly idle: the drain that sets the end of a small batch
+// (a shard of a multi-GPU render) is shorter.  `tail(Wd, it)` launches the configuration's tail kernel.
+template <uint32_t FEAT, class F>
+void wf_tail_launches(const rtw_launch& L, const rtw_wf& W, rtw_wf Wd, uint32_t iters, hipStream_t st, F&& tail) {
+    const bool two = W.deal && (W.deal_mode & 64u) && iters >= 1u && iters + RTW_WF_TAIL_BUDGET < L.max_depth;
+    if (!two) {
+        tail(Wd, iters);
+        return;
+    }
+    // the first launch appends to len[(iters + 1) % 3] (the split kernels leave it holding an older count)
+    (void)hipMemsetAsync(W.len[(iters + 1u) % 3u], 0, RTW_WF_STRIPES * RTW_WF_LEN_STRIDE * 4, st);
+    Wd.tail_budget = RTW_WF_TAIL_BUDGET;
+    tail(Wd, iters);
+    rtw_wf W2 = W;
+    W2.deal = W.deal + RTW_WF_DEAL_TAIL2;
+    W2.tail_budget = 0;
+    tail(W2, iters + RTW_WF_TAIL_BUDGET);
+}
+
 // dynamic LDS of the kernels that walk through L1/L2: the two-wide walk's per-lane stacks
 template <uint32_t FEAT>
 size_t wf_w2_lds(const rtw_launch& L) {
@@ -2014,39 +2049,40 @@ void wf_run_fused(const rtw_launch& L, const rtw_wf& W0, hipStream_t st, int n_c
     }
     if (iters < L.max_depth) {
         RTW_TIME_BEGIN(T, RTW_K_TAIL)
-        bool done = false;
-        if constexpr ((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING)) == 0) {
-            if (clds && (L.wf_fuse & 2u)) {
-                rtw_wf Wd = W;  // the tail's input claims: counter 512 (iteration 0 took 0 .. 511)
-                if (W.deal) Wd.deal = W.deal + RTW_WF_DEAL_LAUNCH;
-                const rtw_wf& W = Wd;
-                if (shape == 2)
-                    hipLaunchKernelGGL((wf_tail_clds2<FEAT, 512>), dim3(tgrid[0]), dim3(512), clds, st, L, W, iters);
-                else if (shape == 3)
-                    hipLaunchKernelGGL((wf_tail_clds2<FEAT, 640>), dim3(tgrid[0]), dim3(640), clds, st, L, W, iters);
-                else if (shape == 4)
-                    hipLaunchKernelGGL((wf_tail_clds2<FEAT, 768>), dim3(tgrid[0]), dim3(768), clds, st, L, W, iters);
-                else if (cn == CN_F32_4)
-                    hipLaunchKernelGGL((wf_tail_clds<FEAT, CN_F32_4>), dim3(tgrid[0]), dim3(1024), clds, st, L, W, iters);
-                else if (cn == CN_F16_4)
-                    hipLaunchKernelGGL((wf_tail_clds<FEAT, CN_F16_4>), dim3(tgrid[0]), dim3(1024), clds, st, L, W, iters);
-                else
-                    hipLaunchKernelGGL((wf_tail_clds<FEAT, CN_F16_8>), dim3(tgrid[0]), dim3(1024), clds, st, L, W, iters);
-                done = true;
+        // one tail launch over iteration itx's queue (W's counters: the launch's own)
+        auto tail = [&](const rtw_wf& Wd, uint32_t itx) {
+            if constexpr ((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING)) == 0) {
+                if (clds && (L.wf_fuse & 2u)) {
+                    const rtw_wf& W = Wd;
+                    if (shape == 2)
+                        hipLaunchKernelGGL((wf_tail_clds2<FEAT, 512>), dim3(tgrid[0]), dim3(512), clds, st, L, W, itx);
+                    else if (shape == 3)
+                        hipLaunchKernelGGL((wf_tail_clds2<FEAT, 640>), dim3(tgrid[0]), dim3(640), clds, st, L, W, itx);
+                    else if (shape == 4)
+                        hipLaunchKernelGGL((wf_tail_clds2<FEAT, 768>), dim3(tgrid[0]), dim3(768), clds, st, L, W, itx);
+                    else if (cn == CN_F32_4)
+                        hipLaunchKernelGGL((wf_tail_clds<FEAT, CN_F32_4>), dim3(tgrid[0]), dim3(1024), clds, st, L, W, itx);
+                    else if (cn == CN_F16_4)
+                        hipLaunchKernelGGL((wf_tail_clds<FEAT, CN_F16_4>), dim3(tgrid[0]), dim3(1024), clds, st, L, W, itx);
+                    else
+                        hipLaunchKernelGGL((wf_tail_clds<FEAT, CN_F16_8>), dim3(tgrid[0]), dim3(1024), clds, st, L, W, itx);
+                    return;
+                }
             }
-        }
+            if (lds && (L.wf_fuse & 2u)) {  // the node array in LDS for the tail too
+                thread_local uint32_t tl[2] = {0, 0};
+                if (tl[1] != tdyn) {
+                    tl[0] = wf_grid(wf_tail_lds<FEAT>, n_cu, tdyn);
+                    tl[1] = (uint32_t)tdyn;
+                }
+                hipLaunchKernelGGL(wf_tail_lds<FEAT>, dim3(tl[0]), dim3(256), tdyn, st, L, Wd, itx);
+                return;
+            }
+            wf_launch_tail<FEAT>(L, Wd, st, n_cu, gdyn, wtail, itx);
+        };
         rtw_wf Wd = W;  // the tail's input claims: counter 512 (iteration 0 took 0 .. 511)
         if (W.deal) Wd.deal = W.deal + RTW_WF_DEAL_LAUNCH;
-        if (!done && lds && (L.wf_fuse & 2u)) {  // the node array in LDS for the tail too
-            thread_local uint32_t tl[2] = {0, 0};
-            if (tl[1] != tdyn) {
-                tl[0] = wf_grid(wf_tail_lds<FEAT>, n_cu, tdyn);
-                tl[1] = (uint32_t)tdyn;
-            }
-            hipLaunchKernelGGL(wf_tail_lds<FEAT>, dim3(tl[0]), dim3(256), tdyn, st, L, Wd, iters);
-            done = true;
-        }
-        if (!done) wf_launch_tail<FEAT>(L, Wd, st, n_cu, gdyn, wtail, iters);
+        wf_tail_launches<FEAT>(L, W, Wd, iters, st, tail);
         RTW_TIME_END(T)
     }
     RTW_TIME_BEGIN(T, RTW_K_REDUCE)
@@ -2161,17 +2197,20 @@ void wf_run(const rtw_launch& L, const rtw_wf& W0, hipStream_t st, int n_cu, rtw
         RTW_TIME_BEGIN(T, RTW_K_TAIL)
         rtw_wf Wd = W;  // the tail's input claims: counter 1024 (iteration 0's trace and shade took 0 .. 1023)
         if (W.deal) Wd.deal = W.deal + 2 * RTW_WF_DEAL_LAUNCH;
-        if (lds && (L.wf_fuse & 2u)) {  // the node array (+ geometry) in LDS for the tail (smoke +5 %)
-            thread_local uint32_t tl[2] = {0, 0};
-            const size_t tdyn = tlds + L.shade_lds;  // wf_tail_lds stages the materials too
-            if (tl[1] != tdyn) {
-                tl[0] = wf_grid(wf_tail_lds<FEAT>, n_cu, tdyn);
-                tl[1] = (uint32_t)tdyn;
+        auto tail = [&](const rtw_wf& Wx, uint32_t itx) {
+            if (lds && (L.wf_fuse & 2u)) {  // the node array (+ geometry) in LDS for the tail (smoke +5 %)
+                thread_local uint32_t tl[2] = {0, 0};
+                const size_t tdyn = tlds + L.shade_lds;  // wf_tail_lds stages the materials too
+                if (tl[1] != tdyn) {
+                    tl[0] = wf_grid(wf_tail_lds<FEAT>, n_cu, tdyn);
+                    tl[1] = (uint32_t)tdyn;
+                }
+                hipLaunchKernelGGL(wf_tail_lds<FEAT>, dim3(tl[0]), dim3(256), tdyn, st, L, Wx, itx);
+            } else {
+                wf_launch_tail<FEAT>(L, Wx, st, n_cu, w2l, wtail, itx);
             }
-            hipLaunchKernelGGL(wf_tail_lds<FEAT>, dim3(tl[0]), dim3(256), tdyn, st, L, Wd, iters);
-        } else {
-            wf_launch_tail<FEAT>(L, Wd, st, n_cu, w2l, wtail, iters);
-        }
+        };
+        wf_tail_launches<FEAT>(L, W, Wd, iters, st, tail);
         RTW_TIME_END(T)
     }
     RTW_TIME_BEGIN(T, RTW_K_REDUCE)
