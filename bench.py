@@ -344,7 +344,7 @@ def main():
         "note": "device walk steps (inner boxes + sphere tests, one lane's own walk each) of a whole render per "
                 "second of render, over the compact LDS walk's rate alone on the config's rays (the ceiling)"}
     # a fraction above 1 is not evidence (a pass of another shard or launch shape): never published
-    for sec in (roofline, roofline["hbm"]):
+    for sec in (roofline, roofline["hbm"], roofline["walk"]):
         if sec["frac"] is not None and sec["frac"] > 1.0:
             sec["guard"] = f"frac {sec['frac']} > 1 from {sec.get('source') or roofline['valu']['source']}: nulled"
             sec["frac"] = sec["achieved"] = None

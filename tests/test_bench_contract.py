@@ -1,4 +1,4 @@
-"""The committed bench line (profiles/r4_c2_bench.json, written by bench.py on an
+"""The committed bench line (profiles/r5_c2_bench.json, written by bench.py on an
 MI355X) carries every field of the driver's contract: the headline metric of
 BASELINE.json on config 2, the dominant kernel's roofline and the CPU baseline.
 Its roofline fractions are physical (<= 1) and recomputable from profiles/
@@ -11,7 +11,7 @@ import sys
 import pytest
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-ROUND = "r4"
+ROUND = "r5"
 BENCH = f"{ROUND}_c2_bench.json"
 SUMMARY = f"{ROUND}_c2_timed_summary.txt"
 
@@ -40,6 +40,13 @@ def test_c2_bench_line_contract():
     assert 0 < r["frac"] <= 1 and 0 < r["hbm"]["frac"] <= 1 and r["hbm"]["peak"] == 8000.0
     assert 0 < r["valu"]["lane_util"] <= 1
     assert r["traffic"] and r["traffic"] > 0
+    # the work-normalised walk roofline (round 5): device node visits per second against the walk ceiling of
+    # the same build (diag/trav_bench.hip -> profiles/walk_ceiling_c2.json)
+    w = r["walk"]
+    assert w["frac"] is not None and 0 < w["frac"] <= 1 and w["ceiling"] > 0
+    ceil = json.load(open(os.path.join(REPO, "profiles", "walk_ceiling_c2.json")))
+    assert ceil["build_id"] == d["build_id"] and abs(ceil["ceiling"] - w["ceiling"]) <= 1e-6 * w["ceiling"]
+    assert abs(w["frac"] - w["achieved"] / w["ceiling"]) < 1e-3
     c = d["cpu_baseline"]
     for k in ("value", "unit", "cores", "kind", "sample"):
         assert k in c, k
@@ -51,7 +58,7 @@ def test_c2_bench_line_contract():
 
 @pytest.mark.parametrize("config", ["c2", "c3", "c4", "c5", "cornell", "cornell_smoke", "simple_light"])
 def test_roofline_recomputes_from_profiles(config):
-    """Every committed round-4 bench line: VALU and HBM fractions <= 1 and recomputable from
+    """Every committed round-5 bench line: VALU and HBM fractions <= 1 and recomputable from
     the PMC passes in profiles/ (taken on the same build: the line's build_id) and its HIP-event launch time."""
     line = os.path.join(REPO, "profiles", f"{ROUND}_{config}_bench.json")
     rc = subprocess.run([sys.executable, os.path.join(REPO, "tools", "roofline_check.py"), line],
@@ -67,7 +74,7 @@ def test_roofline_recomputes_from_profiles(config):
 
 
 def test_rocprof_summary_agrees_with_bench_events():
-    """profiles/r4_c2_timed_summary.txt (rocprofv3 --kernel-trace --stats of the bench
+    """profiles/r5_c2_timed_summary.txt (rocprofv3 --kernel-trace --stats of the bench
     command) and the bench's HIP-event average of the dominant kernel agree."""
     d = load(BENCH)
     kernel = d["roofline"]["kernel"].split("<")[0]
