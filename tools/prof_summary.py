@@ -1,12 +1,13 @@
 """Per-kernel duration summary of a rocprofv3 kernel trace, restricted to the
 timed region of bench.py.
 
-bench.py runs 2 counted renders (reference + SAH topology) and `warmup`
-renders before the timed steps; rocprofv3 --stats averages over all of them.
-This script drops the first `--skip` dispatches of every kernel name (the
-untimed ones) and reports count / total / mean / min / max of the rest, so the
-mean of the dominant kernel can be compared with bench.py's HIP-event
-`roofline.avg_launch_ms`.
+bench.py runs counted renders (reference + SAH topology, which may use other
+kernel instantiations) and `warmup` renders before the timed steps; rocprofv3
+--stats averages over all of them.  With the bench line (--json), this script
+keeps the timed region only: the last steps x launches_per_step calls of the
+dominant kernel and every call from the end of the render before them, and
+reports count / total / mean / min / max per kernel, so the mean of the
+dominant kernel can be compared with bench.py's HIP-event `roofline.avg_launch_ms`.
 
 Usage: python tools/prof_summary.py gpurun_out/prof/run_kernel_trace.csv --skip-renders 2 [--json bench.json]
 """
@@ -22,28 +23,38 @@ def main():
     ap.add_argument("--skip-renders", type=int, default=2, help="untimed renders before the timed steps")
     ap.add_argument("--json", help="bench JSON line (file) to compare against")
     args = ap.parse_args()
-    per = defaultdict(list)
+    rows = []
     for r in csv.DictReader(open(args.trace_csv)):
-        per[r["Kernel_Name"]].append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]) - int(r["Start_Timestamp"])))
-    n_renders = None
+        rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]) - int(r["Start_Timestamp"]), r["Kernel_Name"]))
+    rows.sort()
     bench = None
     if args.json:
         for line in open(args.json):
             line = line.strip()
             if line.startswith("{"):
                 bench = json.loads(line)
-        if bench:
-            n_renders = bench["steps"] + bench["warmup"] + args.skip_renders
+    t0 = None
+    if bench:
+        # the timed region: the last steps x launches_per_step calls of the dominant kernel, back to the end of the
+        # render before them (the wf_reduce preceding the first of those calls).  The untimed renders before it
+        # (counted passes, warm-up) may run other instantiations, so counting calls per name is not enough.
+        rf = bench["roofline"]
+        n_dom = int(round(bench["steps"] * rf["launches_per_step"]))
+        dom = [i for i, (_, _, n) in enumerate(rows) if n.split("(")[0].endswith(rf["kernel"]) or rf["kernel"] in n]
+        if len(dom) >= n_dom > 0:
+            first = dom[-n_dom]
+            j = first
+            while j > 0 and "wf_reduce" not in rows[j - 1][2]:
+                j -= 1
+            t0 = rows[j][0]
+    per = defaultdict(list)
+    for t, d, n in rows:
+        if t0 is None or t >= t0:
+            per[n].append(d)
+    if t0 is None and bench:
+        print("(timed region not found: every call)")
     print(f"{'kernel':70s} {'calls':>6s} {'total_ms':>10s} {'mean_us':>10s} {'min_us':>9s} {'max_us':>9s}")
-    for name, recs in sorted(per.items(), key=lambda kv: -sum(d for _, d in kv[1])):
-        recs.sort()
-        skip = 0
-        if n_renders and len(recs) % n_renders == 0:
-            per_render = len(recs) // n_renders
-            skip = per_render * (args.skip_renders + bench["warmup"])
-        d = [x for _, x in recs[skip:]]
-        if not d:
-            continue
+    for name, d in sorted(per.items(), key=lambda kv: -sum(kv[1])):
         print(f"{name[:70]:70s} {len(d):6d} {sum(d) / 1e6:10.3f} {sum(d) / len(d) / 1e3:10.1f} "
               f"{min(d) / 1e3:9.1f} {max(d) / 1e3:9.1f}")
     if bench:
