@@ -81,6 +81,15 @@ def derive(c):
         e["valu_issue2"] = 2.0 * c["SQ_INSTS_VALU"] / (1024.0 * c["GRBM_GUI_ACTIVE"] / 8.0)
     if c.get("SQ_LDS_IDX_ACTIVE") and "SQ_LDS_BANK_CONFLICT" in c:
         e["lds_conflict"] = c["SQ_LDS_BANK_CONFLICT"] / c["SQ_LDS_IDX_ACTIVE"]
+    hit, miss = c.get("TCC_HIT_sum"), c.get("TCC_MISS_sum")
+    if hit is not None and miss is not None and hit + miss > 0:
+        e["l2_hit"] = hit / (hit + miss)
+    for n in ("TCP_TOTAL_CACHE_ACCESSES_sum", "TCP_TCC_READ_REQ_sum", "TA_FLAT_READ_WAVEFRONTS_sum", "SQ_INSTS_VMEM_RD",
+              "SQ_INSTS_VMEM_WR", "TA_BUSY_avr"):
+        if n in c:
+            e[n.lower().replace("_sum", "").replace("_avr", "")] = c[n]
+    if c.get("TCP_TOTAL_CACHE_ACCESSES_sum") and "TCP_TCC_READ_REQ_sum" in c:
+        e["l1_miss_to_l2"] = c["TCP_TCC_READ_REQ_sum"] / c["TCP_TOTAL_CACHE_ACCESSES_sum"]
     if c.get("SQ_WAVES"):
         for n in ("SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_INSTS_SALU", "SQ_INSTS_SMEM", "SQ_INSTS_VMEM",
                   "SQ_INSTS_BRANCH"):
