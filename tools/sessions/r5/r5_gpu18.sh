@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 5: auto wf_iters (4 / 9 on image textures) -- whole GPU suite, bench lines, C2 8-rank shard breakdown
 set -u
-bash tools/r5_gpu9.sh || exit 1
+bash tools/sessions/r5/r5_gpu9.sh || exit 1
 TAG=iters_auto bash tools/r5_shard_breakdown.sh c2 8
 # four-wide records: same hits, then C4 A/B against the in-tree (two-wide) library
 RTW_LIB=build/rtw_wide4.so timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_boundary.py -m gpu -x -q \
