@@ -208,3 +208,47 @@ def test_bench_torchrun_line_never_carries_a_whole_frame_roofline(tmp_path, worl
     assert r["valu"]["lane_ops_per_launch"] is None and r["traffic"] is None
     assert "no pass of this rank's shard" in r["valu"]["source"]
     assert "no pass of this rank's shard" in r["hbm"]["source"]
+
+
+def test_prof_summary_keeps_only_the_timed_region(tmp_path):
+    """tools/prof_summary.py: with the bench line, only the last steps x launches_per_step calls of the dominant
+    kernel and the calls after the render before them count -- the counted passes before them may run other
+    instantiations of the same kernels, so counting calls per name would misplace the region."""
+    rows = []
+    t = 0
+
+    def call(name, dur):
+        nonlocal t
+        rows.append((name, t, t + dur))
+        t += dur + 10
+
+    call("wf_step<0u, true>(rtw_launch)", 5000)           # counted pass: another instantiation
+    call("wf_reduce(rtw_launch, rtw_wf)", 100)
+    for dur in (900, 800):                                # SAH counted pass: the dominant kernel, untimed
+        call("wf_step_clds2<0u, 768u>(rtw_launch)", dur)
+    call("wf_reduce(rtw_launch, rtw_wf)", 100)
+    for _ in range(2):                                    # two timed steps, 2 launches each
+        call("wf_tile_lists(rtw_launch, rtw_wf)", 5)
+        for dur in (1000, 3000):
+            call("wf_step_clds2<0u, 768u>(rtw_launch)", dur)
+        call("wf_reduce(rtw_launch, rtw_wf)", 100)
+    trace = tmp_path / "kt.csv"
+    with open(trace, "w") as f:
+        f.write("Kernel_Name,Start_Timestamp,End_Timestamp\n")
+        for n, a, b in rows:
+            f.write(f'"{n}",{a * 1000},{b * 1000}\n')
+    line = {"steps": 2, "warmup": 0, "roofline": {"kernel": "wf_step_clds2<0u, 768u>", "launches_per_step": 2,
+                                                  "avg_launch_ms": 2.0}}
+    bench = tmp_path / "bench.json"
+    bench.write_text(json.dumps(line) + "\n")
+    rc = subprocess.run([sys.executable, os.path.join(REPO, "tools", "prof_summary.py"), str(trace), "--json", str(bench)],
+                        capture_output=True, text=True)
+    assert rc.returncode == 0, rc.stderr
+    got = {}
+    for ln in rc.stdout.splitlines()[1:]:  # kernel (70 columns), calls, total_ms, mean_us, min_us, max_us
+        nums = ln[70:].split()
+        if not ln.startswith("bench.py") and len(nums) == 5 and nums[0].isdigit():
+            got[ln[:70].strip().split("(")[0]] = (int(nums[0]), float(nums[2]))
+    assert got["wf_step_clds2<0u, 768u>"] == (4, 2000.0)  # 4 timed calls, mean 2000 us
+    assert got["wf_reduce"][0] == 2 and got["wf_tile_lists"][0] == 2
+    assert "wf_step<0u, true>" not in got
