@@ -322,7 +322,7 @@ typedef struct rtw_tuning {
     uint32_t fast_reject;      /* 1 = exact sphere fast-reject filter (default) */
     uint32_t lds;              /* RTW_LDS_* (default RTW_LDS_ALL) */
     uint32_t fuse;             /* RTW_FUSE_* (default STEP | TAIL_LDS) */
-    uint32_t wf_iters;         /* wavefront iterations before the tail kernel (1..100; default 0 = auto: 4, 9 on image-textured scenes) */
+    uint32_t wf_iters;         /* wavefront iterations before the tail kernel (1..100; default 0 = auto: 4, or 100 -- every bounce, no tail -- on image-textured scenes) */
     uint32_t mega_shade_min;   /* persistent kernel: lanes ready before a shading pass (default 48; 1..64) */
     uint32_t mega_waves;       /* persistent kernel: launch-bound variant (default 1; 1, 6 or 8) */
     uint32_t mega_tile_order;  /* persistent kernel: 1 = last tile row first (default) */

@@ -149,7 +149,7 @@ void rtw_tuning_defaults(rtw_tuning* t) {
     t->fast_reject = 1;
     t->lds = RTW_LDS_ALL;
     t->fuse = RTW_FUSE_STEP | RTW_FUSE_TAIL_LDS;
-    t->wf_iters = 0;  // auto: 4, or 9 for image-textured scenes (profiles/r5_iters/)
+    t->wf_iters = 0;  // auto: 4, or every bounce (no tail) on image-textured scenes (profiles/r5_iters/)
     t->mega_shade_min = 48;  // tuned on C2: 8..64 -> 48 best
     t->mega_waves = 1;
     t->mega_tile_order = 1;
@@ -435,8 +435,10 @@ int rtw_scene_create_ex(const rtw_scene_desc* d, int device, const rtw_tuning* t
     }
     // Round 5, with the dynamic tail (deal bit 2): fewer iterations before the tail pay everywhere but on
     // image-textured scenes -- same-box A/B, 9 -> 4 iterations: C2 +3.7 %, C4 +3.3 %, Cornell +6.8 %, smoke
-    // +1.2 %, simple_light +1.9 %; C5 -3.5 % (profiles/r5_iters/).
-    ctx->wf_iters = tu.wf_iters ? tu.wf_iters : (sfeat & RTW_F_IMAGE) ? 9u : 4u;
+    // +1.2 %, simple_light +1.9 %.  Image-textured scenes run no tail at all (every bounce a wavefront
+    // iteration: the launcher clamps to max_depth): C5 9 / 24 / 32 / 50 iterations 9425 / 9750 / 9816 / 9990
+    // Msamples/s (profiles/r5_iters/).
+    ctx->wf_iters = tu.wf_iters ? tu.wf_iters : (sfeat & RTW_F_IMAGE) ? (uint32_t)RTW_WF_MAX_ITERS : 4u;
     ctx->wf_sort_iters = tu.sort_iters;
     ctx->wf_sort_iters_split = tu.sort_iters_split;
     ctx->wf_sort_mask = (1u << tu.sort_bits) - 1u;
