@@ -343,11 +343,16 @@ def main():
         "device_steps_per_render": dev_steps, "render_ms": round(render_s * 1e3, 3), "source": ceil_src,
         "note": "device walk steps (inner boxes + sphere tests, one lane's own walk each) of a whole render per "
                 "second of render, over the compact LDS walk's rate alone on the config's rays (the ceiling)"}
-    # a fraction above 1 is not evidence (a pass of another shard or launch shape): never published
-    for sec in (roofline, roofline["hbm"], roofline["walk"]):
+    # A VALU or HBM fraction above 1 is physically impossible: pmc_pass only prices this build's own shard, so it
+    # means a wrong PMC pass, peak or launch time -- a measurement bug.  The raw value stays in the line, the
+    # section carries "error", and the run exits non-zero after printing it (tests/test_bench_contract.py).  The
+    # walk ceiling is a measured rate, not a hardware peak: a walk fraction above 1 is reported as it is.
+    frac_errors = []
+    for name, sec in (("valu", roofline), ("hbm", roofline["hbm"])):
         if sec["frac"] is not None and sec["frac"] > 1.0:
-            sec["guard"] = f"frac {sec['frac']} > 1 from {sec.get('source') or roofline['valu']['source']}: nulled"
-            sec["frac"] = sec["achieved"] = None
+            sec["error"] = (f"{name} frac {sec['frac']} > 1 from {sec.get('source') or roofline['valu']['source']}: "
+                            "a measurement bug")
+            frac_errors.append(sec["error"])
 
     cpu = None
     if rank == 0 and world_size == 1 and not args.no_cpu_baseline:
@@ -391,6 +396,9 @@ def main():
     world.close()
     if distributed:
         dist.destroy_process_group()
+    if frac_errors:
+        print("bench.py: " + "; ".join(frac_errors), file=sys.stderr, flush=True)
+        sys.exit(3)
 
 
 def pmc_build_id(data):
@@ -451,9 +459,10 @@ def pmc_valu(args, kind, build_id, n_shards=1, rank=0, single=False):
 
 def walk_ceiling(args, build_id):
     """The walk ceiling of this config measured on this build (diag/run_walk_ceiling.py ->
-    profiles/walk_ceiling_<config>.json), or (None, reason).  Only the product defaults on the whole frame
-    (an A/B build or tuning, a shard at N > 1 -- whose per-rank render time prices fewer visits -- still
-    compare: the rate is per second, not per launch), but never a measurement of another build."""
+    profiles/walk_ceiling_<config>.json), or (None, reason).  The ceiling belongs to one build: a file of
+    another build is unused, and A/B runs (--spp, --tuning, --bvh other than sah, RTW_LIB builds) get none.
+    Shards at N > 1 do get it: the walk rate is node-steps per second of render, which a shard's shorter
+    render does not change, unlike the per-launch PMC counts of pmc_pass."""
     if args.spp or args.tuning or args.bvh != "sah" or os.environ.get("RTW_LIB"):
         return None, None
     f = os.path.join(args.profiles_dir, f"walk_ceiling_{args.config}.json")

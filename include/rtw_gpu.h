@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define RTW_ABI_VERSION 7
+#define RTW_ABI_VERSION 8
 
 enum rtw_status {
     RTW_OK = 0,
@@ -351,17 +351,24 @@ typedef struct rtw_tuning {
                                   1024-thread block per CU, 2 / 3 / 4 = two blocks of 512 / 640 / 768 threads
                                   (4 / 5 / 6 waves per SIMD) when the stage fits half the LDS; the 8-copy stage
                                   always runs one block (ABI 7) */
-    uint32_t deal;             /* how the wavefront's waves share work (ABI 7), bits: 1 = iteration 0's runs of 16
-                                  (the last chunks singly) claimed from a counter per stripe group as its waves
-                                  finish, instead of dealt round-robin; 2 = the tail's input chunks claimed from one
-                                  counter, or 4 = from a counter per stripe (its own group's waves), instead of
-                                  each wave's own list; 16 = the fused step's iterations >= 1 claim their stripe's
-                                  chunks from a counter per stripe group; 32 = iteration 0's last 16 x (waves)
-                                  chunks go singly (else the last 4 x); 64 = the tail in two launches (7 bounces
-                                  per path, the live paths requeued, then the rest: measured slower, an A/B knob);
-                                  0 = all static.  A batch with fewer than 192 chunks of 64 paths per wave keeps
-                                  the static shares unless bit 8 is set.  Default 59 = 1 | 2 | 8 | 16 | 32. */
+    uint32_t deal;             /* how the wavefront's waves share work (ABI 8), RTW_DEAL_* bits; 0 = all static,
+                                  default 59 = RUNS | TAIL | SMALL | ITERS | SINGLES16 */
 } rtw_tuning;
+enum {  /* rtw_tuning.deal (ABI 8: the per-stripe tail claims, bit 4, and the two-launch tail, bit 64, lost their
+           A/Bs and were removed -- diag/deal_tail_modes.patch; both bits are now refused) */
+    RTW_DEAL_RUNS = 1u,        /* iteration 0's runs of 16 samples of a tile (the last chunks singly) claimed from a
+                                  counter per stripe group as its waves finish, instead of dealt round-robin */
+    RTW_DEAL_TAIL = 2u,        /* the tail's input chunks claimed from one counter instead of each wave's own list */
+    RTW_DEAL_SMALL = 8u,       /* the dynamic deal also on batches with fewer than 192 chunks of 64 paths per wave
+                                  (which otherwise keep the static shares) */
+    RTW_DEAL_ITERS = 16u,      /* the fused step's iterations >= 1 claim their stripe's chunks from a counter per
+                                  stripe group */
+    RTW_DEAL_SINGLES16 = 32u,  /* iteration 0's last 16 x (waves) chunks go singly (else the last 4 x) */
+    RTW_DEAL_SMALL_SORT = 128u,/* direction bucketing (sort_iters / sort_iters_split) also on batches with fewer
+                                  than 192 chunks per wave, which otherwise append in order: a test knob that runs
+                                  the queues of the large benched batches on small images (same image) */
+    RTW_DEAL_ALL = 187u
+};
 
 void rtw_tuning_defaults(rtw_tuning* out);
 /* rtw_scene_create with explicit tuning (NULL = defaults). */

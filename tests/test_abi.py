@@ -29,7 +29,7 @@ def test_exports_every_header_symbol(rtw):
     for n in names:
         assert hasattr(lib, n), n
     assert set(names) == set(rtw._abi.SIGNATURES), set(names) ^ set(rtw._abi.SIGNATURES)
-    assert lib.rtw_version() == 7
+    assert lib.rtw_version() == 8
 
 
 def test_struct_sizes_match_header(rtw, tmp_path):
@@ -194,3 +194,21 @@ def test_box_pad_extent_covers_hoisted_spheres(rtw):
         assert st["n_hoisted"] == hoist
         assert st["extent"] >= 2000.0, st        # the ground's box: (-1000, -2000, -1000) .. (1000, 0, 1000)
         assert st["box_pad"] == np.float32(st["extent"]) * np.float32(2.0 ** -19)
+
+
+def test_deal_bits_header_and_validation(rtw):
+    """rtw_tuning.deal (ABI 8): the header's RTW_DEAL_* values are the binding's, the live bits are accepted and
+    the removed modes (4: per-stripe tail claims, 64: the two-launch tail; diag/deal_tail_modes.patch) refused."""
+    src = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
+    hdr = {k: int(v) for k, v in re.findall(r"(RTW_DEAL_[A-Z_0-9]+)\s*=\s*(\d+)u", src)}
+    A = rtw._abi
+    assert hdr and all(getattr(A, k) == v for k, v in hdr.items()), hdr
+    live = [v for k, v in hdr.items() if k != "RTW_DEAL_ALL"]
+    assert sum(live) == hdr["RTW_DEAL_ALL"] == A.RTW_DEAL_ALL
+    arr = rtw.flatten(rtw.worlds.two_spheres_world())
+    for deal in (0, 59, A.RTW_DEAL_ALL, A.RTW_DEAL_SMALL_SORT):
+        rtw.World(arr, device=A.RTW_DEVICE_CPU, tuning={"deal": deal}).close()
+    for deal in (4, 64, 63, 123, 256):
+        with pytest.raises(rtw.RtwError) as e:
+            rtw.World(arr, device=A.RTW_DEVICE_CPU, tuning={"deal": deal})
+        assert e.value.code == A.RTW_E_INVALID

@@ -121,19 +121,21 @@ def test_fused_step_bit_identical(rtw, name):
         kw = SCENES[name][1]
     cam = rtw.Camera(image_width=80, samples_per_pixel=6, max_depth=50, **kw).init()
     outs = {}
-    for v in ("0111", "3111", "7111", "3011", "3101", "3110", "3111d", "0111d", "7111d", "3111p", "0111p", "3111i",
-              "7111i", "3111t", "0111t"):
+    for v in ("0111", "3111", "7111", "3011", "3101", "3110", "3111d", "0111d", "7111d", "3111i", "7111i", "3111s",
+              "0111s", "7111s", "3011s", "3111n"):
         # fuse, Perlin / geometry / material LDS; d: the static deal of iteration 0 and the tail (tuning.deal 0),
-        # p: the tail's per-stripe claims (deal 5); i: iterations >= 1 claimed per stripe group, long singles phase;
-        # t: and the tail in two launches (deal 123)
+        # i: iterations >= 1 claimed per stripe group, long singles phase (deal 59); s: and the direction-bucketed
+        # queues of the benched batches forced on at this size (deal 187 = 59 | RTW_DEAL_SMALL_SORT), every
+        # iteration bucketed; n: bucketed with the static deal (deal 128)
         lds = 127 & ~((32 if v[1] == "0" else 0) | (16 if v[2] == "0" else 0) | (8 if v[3] == "0" else 0))
-        world = rtw.World(arr, tuning={"fuse": int(v[0]), "lds": lds,
-                                       "deal": 0 if v.endswith("d") else 13 if v.endswith("p") else 59 if v.endswith("i") else
-                                       123 if v.endswith("t") else 11})
+        deal = {"d": 0, "i": 59, "s": 187, "n": 128}.get(v[-1], 11)
+        tu = {"fuse": int(v[0]), "lds": lds, "deal": deal}
+        if v[-1] in "sn":
+            tu.update(sort_iters=50, sort_iters_split=50)
+        world = rtw.World(arr, tuning=tu)
         outs[v] = render_all(rtw, world, cam, 6, 5)
         world.close()
-    for k in ("3111", "7111", "3011", "3101", "3110", "3111d", "0111d", "7111d", "3111p", "0111p", "3111i", "7111i",
-              "3111t", "0111t"):
+    for k in outs:
         assert np.array_equal(outs["0111"], outs[k]), k
 
 

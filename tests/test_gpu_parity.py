@@ -349,14 +349,22 @@ def test_v1_knobs_invariant(rtw, book1, knob):
                                   {"deal": 0}, {"deal": 0, "fuse": 0}, {"deal": 0, "lds": 127 & ~2, "fuse": 5},
                                   {"deal": 9, "wf_iters": 1}, {"deal": 9, "fuse": 0, "wf_iters": 2},
                                   {"deal": 9, "lds": 127 & ~2, "fuse": 5}, {"deal": 9, "fuse": 1},
-                                  {"deal": 13}, {"deal": 13, "fuse": 0}, {"deal": 13, "lds": 127 & ~2, "fuse": 5},
                                   {"deal": 10}, {"deal": 11, "wf_iters": 1}, {"deal": 11}, {"deal": 11, "fuse": 0},
-                                  {"deal": 11, "wf_paths": 4096}, {"deal": 13, "wf_paths": 65536, "fuse": 0},
+                                  {"deal": 11, "wf_paths": 4096}, {"deal": 11, "wf_paths": 65536, "fuse": 0},
                                   {"deal": 59}, {"deal": 27, "lds": 127 & ~2, "fuse": 5}, {"deal": 57, "wf_iters": 9}, {"deal": 51},
                                   {"deal": 59, "fuse": 0}, {"deal": 59, "lds": 127 & ~2, "fuse": 0}, {"deal": 51, "fuse": 0, "wf_iters": 3},
-                                  {"deal": 123}, {"deal": 123, "fuse": 0}, {"deal": 123, "lds": 127 & ~2, "fuse": 0},
-                                  {"deal": 123, "wf_paths": 4096}, {"deal": 64}, {"deal": 64, "fuse": 0}, {"deal": 69, "wf_iters": 2},
-                                  {"deal": 123, "wf_iters": 1}, {"deal": 123, "lds": 127 & ~2, "fuse": 5}])
+                                  # deal 128 (RTW_DEAL_SMALL_SORT): the direction-bucketed queues of the large benched
+                                  # batches on this small image -- fused compact-LDS step (4- and 8-copy stages, one and
+                                  # two blocks per CU, fp32 nodes), fused step through L1/L2, split trace / shade, all
+                                  # iterations bucketed, fewer key bits, many batches, the static deal
+                                  {"deal": 187}, {"deal": 187, "sort_iters": 50}, {"deal": 187, "sort_iters": 50, "wf_iters": 9},
+                                  {"deal": 187, "bvh_orders": 8}, {"deal": 187, "clds_shape": 1}, {"deal": 187, "compact_nodes": 2},
+                                  {"deal": 187, "lds": 127 & ~2, "fuse": 5}, {"deal": 187, "lds": 127 & ~2, "fuse": 5, "sort_iters": 50},
+                                  {"deal": 187, "fuse": 0}, {"deal": 187, "fuse": 0, "sort_iters_split": 50},
+                                  {"deal": 187, "fuse": 0, "sort_iters_split": 3, "wf_iters": 9}, {"deal": 187, "sort_bits": 2},
+                                  {"deal": 187, "fuse": 0, "sort_bits": 1}, {"deal": 187, "wf_paths": 65536},
+                                  {"deal": 187, "fuse": 0, "wf_paths": 65536}, {"deal": 128}, {"deal": 128, "fuse": 0},
+                                  {"deal": 187, "lds": 127 & ~2, "fuse": 0, "wide_walk": 0}])
 def test_wavefront_knobs_invariant(rtw, book1, knob):
     """Wavefront tuning (rtw_tuning: bounces before the tail kernel, batch size ->
     many batches, FMA vs reference slab test, LDS-staged nodes, SAH leaf runs of up
@@ -365,7 +373,8 @@ def test_wavefront_knobs_invariant(rtw, book1, knob):
     one node ordering instead of 8, camera rays against per-tile candidate lists vs
     the walk, the two-wide stack walk through L1/L2 vs the
     octant-ordered compact walk, the fused step through L1/L2, dominant spheres hoisted ahead of the
-    tree or not, survivors filed into direction-bucketed blocks or appended; the fused path's packed 48-B path
+    tree or not, survivors filed into direction-bucketed blocks or appended -- forced on at this size by deal bit
+    128, as the benched batches run them --; the dynamic and static deals; the fused path's packed 48-B path
     state and the split path's 60-B one, each with its tail) never changes a pixel."""
     arr, world = book1
     cam = rtw.book1_camera(image_width=300, aspect_ratio=1.5, spp=5).init()

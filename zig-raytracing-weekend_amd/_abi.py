@@ -31,6 +31,8 @@ RTW_KERNEL_WAVEFRONT, RTW_KERNEL_PERSISTENT, RTW_KERNEL_SIMPLE = 0, 1, 2
 RTW_LDS_NODES, RTW_LDS_CNODES, RTW_LDS_MATERIALS, RTW_LDS_SHADE = 1, 2, 4, 8
 RTW_LDS_GEOMETRY, RTW_LDS_PERLIN, RTW_LDS_MEGA_NODES, RTW_LDS_ALL = 16, 32, 64, 127
 RTW_FUSE_STEP, RTW_FUSE_TAIL_LDS, RTW_FUSE_GLOBAL = 1, 2, 4
+RTW_DEAL_RUNS, RTW_DEAL_TAIL, RTW_DEAL_SMALL, RTW_DEAL_ITERS, RTW_DEAL_SINGLES16 = 1, 2, 8, 16, 32
+RTW_DEAL_SMALL_SORT, RTW_DEAL_ALL = 128, 187
 RTW_DEVICE_CPU = -1
 
 # numpy record layouts == the C structs (asserted against sizeof in tests)

@@ -180,8 +180,8 @@ int rtw_scene_create_ex(const rtw_scene_desc* d, int device, const rtw_tuning* t
     if (tu.bvh_orders != 0 && tu.bvh_orders != 1 && tu.bvh_orders != 4 && tu.bvh_orders != 8)
         return fail(RTW_E_INVALID, "tuning.bvh_orders must be 0, 1, 4 or 8");
     if (tu.clds_shape > 4) return fail(RTW_E_INVALID, "tuning.clds_shape must be 0..4");
-    if (tu.deal > 127 || (tu.deal & 6u) == 6u)
-        return fail(RTW_E_INVALID, "tuning.deal: bits 1 | 2 or 4 | 8 | 16 | 32 | 64");
+    if (tu.deal & ~(uint32_t)RTW_DEAL_ALL)
+        return fail(RTW_E_INVALID, "tuning.deal: bits 1 | 2 | 8 | 16 | 32 | 128 (RTW_DEAL_*)");
     if (tu.wf_iters > RTW_WF_MAX_ITERS) return fail(RTW_E_INVALID, "tuning.wf_iters out of range");
     if ((tu.object_tree & 0xFFu) > 100 || (tu.object_tree & ~(0xFFu | RTW_OTREE_NO_CULL)))
         return fail(RTW_E_INVALID, "tuning.object_tree: 0..100 [| RTW_OTREE_NO_CULL]");
@@ -633,8 +633,12 @@ int run_wavefront(rtw_ctx* ctx, rtw_launch L, hipStream_t stream, rtw_timer* T) 
     // + direction-bucketed iterations: every wave of a stripe may leave one partly filled 64-slot block per
     //   bucket (wf_push_bucketed)
     const uint64_t bucket_blocks = (ctx->wf_sort_iters || ctx->wf_sort_iters_split) ? (max_waves / RTW_WF_STRIPES + 1) * RTW_WF_BUCKETS : 0;
+    // + the dynamic deal of iteration 0 (rtw_tuning.deal bit 1): a stripe group claims whole runs of 16 chunks
+    //   and then singles, so it may end up to one run and one single chunk above its even share (RUN + 1), whatever
+    //   the grid's waves per stripe (a device or partition with few CUs)
+    const uint64_t deal_slack = ctx->wf_deal ? (1u << 4) + 1u : 0u;
     auto stripe_cap = [&](uint64_t paths) {
-        return ((paths + 63) / 64 / RTW_WF_STRIPES + 1 + max_waves / RTW_WF_STRIPES + bucket_blocks) * 64;
+        return ((paths + 63) / 64 / RTW_WF_STRIPES + 1 + max_waves / RTW_WF_STRIPES + bucket_blocks + deal_slack) * 64;
     };
     // slots per set: every path (iteration 0: slot = path id) or every stripe's capacity
     auto slots = [&](uint64_t paths) { return std::max<uint64_t>(paths, stripe_cap(paths) * RTW_WF_STRIPES); };
@@ -681,7 +685,6 @@ int run_wavefront(rtw_ctx* ctx, rtw_launch L, hipStream_t stream, rtw_timer* T) 
     W.deal = ctx->wf_deal ? deal : nullptr;
     W.deal_mode = ctx->wf_deal;
     W.deal_it = nullptr;  // set per launch (deal bit 16)
-    W.tail_budget = 0;    // set per tail launch (deal bit 64)
     W.n_pix = (uint32_t)n_pix;
     W.iters = ctx->wf_iters;
     W.sort_iters = ctx->wf_sort_iters;
@@ -1032,8 +1035,7 @@ uint32_t rtw_shard_image_row(uint32_t rpb, uint32_t n_shards, uint32_t shard, ui
 }
 
 uint32_t rtw_shard_image_row_h(uint32_t H, uint32_t rpb, uint32_t n_shards, uint32_t shard, uint32_t tile_row) {
-    if (!(rpb & ~RTW_ROWS_FLAGS) || (rpb & RTW_ROWS_FLAGS & ~RTW_ROWS_BALANCED) || !n_shards || shard >= n_shards)
-        return 0xFFFFFFFFu;
+    if (!(rpb & ~RTW_ROWS_FLAGS) || !n_shards || shard >= n_shards) return 0xFFFFFFFFu;
     return rtw_shard_row(H, rpb, n_shards, shard, tile_row);
 }
 

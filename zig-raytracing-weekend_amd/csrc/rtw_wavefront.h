@@ -67,22 +67,17 @@ struct rtw_wf {
     uint32_t run_log2;    // iteration 0's tile runs: 2^run_log2 samples of one tile per run (wf_coherence)
     uint32_t packed;      // this render's queues hold the packed path state (wf_packed; set by wf_run*)
     uint32_t* deal;       // dynamic dealing (rtw_tuning.deal): this launch's counters (zeroed per batch), or null
-    uint32_t deal_mode;   // rtw_tuning.deal bits: 1 iteration 0, 2 the tail (one counter), 4 the tail (per stripe),
-                          // 8 dynamic even on small batches, 16 iterations >= 1 (per stripe group), 32 long singles
+    uint32_t deal_mode;   // rtw_tuning.deal bits (RTW_DEAL_*): 1 iteration 0, 2 the tail, 8 dynamic even on small
+                          // batches, 16 iterations >= 1 (per stripe group), 32 long singles, 128 bucketing on small
+                          // batches
     uint32_t* deal_it;    // this launch's per-stripe counters for iteration it >= 1 (deal bit 16), or null
-    uint32_t tail_budget; // this tail launch's bounces per path before it requeues a live path (deal bit 64), 0 = off
 };
-// deal bit 64: the tail runs in two launches -- RTW_WF_TAIL_BUDGET bounces per path, the paths still alive requeued
-// into the stripe they came from, then the rest to completion as "iteration" it + RTW_WF_TAIL_BUDGET, which reads
-// the set and the stripe lengths the first launch wrote (it + 7 = it + 1 mod 2 and mod 3)
-#define RTW_WF_TAIL_BUDGET 7u
 #define RTW_WF_DEAL_LAUNCH (2 * RTW_WF_STRIPES)  // counters of one launch dealing iteration 0 (runs, singles per group)
 #define RTW_WF_DEAL_COUNTERS0 (2 * RTW_WF_DEAL_LAUNCH + RTW_WF_STRIPES)  // split trace's, shade's, the tail's
 // per batch: those, then RTW_WF_STRIPES per iteration it >= 1 (deal bit 16): the fused step's or the split trace's at
 // RTW_WF_DEAL_COUNTERS0 + it * 256, the split shade's at RTW_WF_DEAL_SHADE + it * 256
 #define RTW_WF_DEAL_SHADE (RTW_WF_DEAL_COUNTERS0 + (RTW_WF_MAX_ITERS + 1) * RTW_WF_STRIPES)
-#define RTW_WF_DEAL_TAIL2 (RTW_WF_DEAL_SHADE + (RTW_WF_MAX_ITERS + 1) * RTW_WF_STRIPES)  // the second tail launch's
-#define RTW_WF_DEAL_COUNTERS (RTW_WF_DEAL_TAIL2 + RTW_WF_STRIPES)
+#define RTW_WF_DEAL_COUNTERS (RTW_WF_DEAL_SHADE + (RTW_WF_MAX_ITERS + 1) * RTW_WF_STRIPES)
 
 // bytes of device state per path (two slot sets + hit + ls; the batch's counters aside)
 #define RTW_WF_PATH_BYTES (2 * (4 * 16 + 8) + 8 + 12)

@@ -1250,33 +1250,25 @@ __device__ __forceinline__ void wf_tail_body(const rtw_launch& L, const rtw_wf& 
     const rtw_wf_set& S = W.set[it & 1u];
     Counters cnt;
     uint32_t cursor = 0, pid = 0, depth = 0;
-    uint32_t nb = 0, src = 0;  // deal bit 64: bounces of this path in this launch, the stripe it came from
     bool active = false, exhausted = false;
     Ray r;
     f3 thr = mk(0, 0, 0), acc = mk(0, 0, 0);
     rtw_rng rng;
     rng.s = 0;
-    // Dynamic input (W.deal, rtw_tuning.deal): the wave claims 64-slot chunks of the input stripes from a
+    // Dynamic input (W.deal, rtw_tuning.deal bit 2): the wave claims 64-slot chunks of the input stripes from one
     // counter as its lanes run dry, one claim issued a chunk ahead, so the tail's end is set by its longest
-    // paths, not by a wave whose static share held more of them (C4: tail 56.7 -> 45.3 ms).  Global (deal bit 1):
-    // chunk g of one counter is chunk g / 256 of stripe g % 256.  Per stripe (bit 2): the waves of stripe group
-    // s claim chunks of stripe s -- the stripe its own group's waves wrote, in the same XCD's L2 -- balancing
-    // within the group only.
+    // paths, not by a wave whose static share held more of them (C4: tail 56.7 -> 45.3 ms): chunk g of the
+    // counter is chunk g / 256 of stripe g % 256.  (Claims per stripe group and a two-launch tail lost their
+    // A/Bs: diag/deal_tail_modes.patch.)
     const uint32_t* lens = W.len[it % 3u];
     uint32_t gcur = 0, gnext = 0, limit = 0;  // wave-uniform; gnext lane 0's
-    const bool dyn = W.deal && (W.deal_mode & 6u);
-    const bool per_stripe = (W.deal_mode & 4u) != 0;
-    const uint32_t own = wf_wave() % RTW_WF_STRIPES;
-    uint32_t* ctr = W.deal ? W.deal + (per_stripe ? own : 0u) : nullptr;
+    const bool dyn = W.deal && (W.deal_mode & 2u);
+    uint32_t* ctr = W.deal;
     if (dyn) {
-        if (per_stripe) {
-            limit = (lens[own * RTW_WF_LEN_STRIDE] + 63u) >> 6;
-        } else {
-            uint32_t mx = 0;
-            for (uint32_t k = lane; k < RTW_WF_STRIPES; k += 64u) mx = max(mx, lens[k * RTW_WF_LEN_STRIDE]);
-            for (int o = 32; o > 0; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
-            limit = ((mx + 63u) >> 6) * RTW_WF_STRIPES;
-        }
+        uint32_t mx = 0;
+        for (uint32_t k = lane; k < RTW_WF_STRIPES; k += 64u) mx = max(mx, lens[k * RTW_WF_LEN_STRIDE]);
+        for (int o = 32; o > 0; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
+        limit = ((mx + 63u) >> 6) * RTW_WF_STRIPES;
         gcur = __builtin_amdgcn_readfirstlane(wf_claim(ctr));
         gnext = wf_claim(ctr);
         exhausted = gcur >= limit;
@@ -1289,8 +1281,8 @@ __device__ __forceinline__ void wf_tail_body(const rtw_launch& L, const rtw_wf& 
             const uint32_t gn = __builtin_amdgcn_readfirstlane(gnext);
             if (!active) {
                 const uint32_t g = (m >> 6) == (cursor >> 6) ? gcur : gn;
-                const uint32_t s = per_stripe ? own : g % RTW_WF_STRIPES;
-                const uint32_t e = ((per_stripe ? g : g / RTW_WF_STRIPES) << 6) | (m & 63u);
+                const uint32_t s = g % RTW_WF_STRIPES;
+                const uint32_t e = ((g / RTW_WF_STRIPES) << 6) | (m & 63u);
                 if (g < limit && e < lens[s * RTW_WF_LEN_STRIDE]) {
                     float2 txy;
                     const uint32_t slot = s * W.stripe_cap + e;
@@ -1299,8 +1291,6 @@ __device__ __forceinline__ void wf_tail_body(const rtw_launch& L, const rtw_wf& 
                     if (depth) wf_load_rest<FEAT>(L, S, slot, depth, txy, thr, acc, rs, pid, W.packed != 0u);
                     rng.s = rs;
                     active = depth != 0;
-                    nb = 0;
-                    src = s;
                 }
             }
             if (((cursor + n_need) >> 6) != (cursor >> 6)) {  // the current chunk is used up: the next one
@@ -1323,8 +1313,6 @@ __device__ __forceinline__ void wf_tail_body(const rtw_launch& L, const rtw_wf& 
                 if (depth) wf_load_rest<FEAT>(L, S, slot, depth, txy, thr, acc, rs, pid, W.packed != 0u);
                 rng.s = rs;
                 active = depth != 0;
-                nb = 0;
-                src = slot / W.stripe_cap;
             }
         }
         if (!__ballot(active)) {
@@ -1407,15 +1395,6 @@ __device__ __forceinline__ void wf_tail_body(const rtw_launch& L, const rtw_wf& 
         }
         if (active && done) {
             W.ls[pid] = rtw_rgb{acc.x, acc.y, acc.z};
-            active = false;
-        }
-        // deal bit 64, first tail launch: a path alive after W.tail_budget bounces here goes back to the stripe it
-        // came from (its outputs never outnumber its inputs), in the other set, for the second launch -- the
-        // state the fused shade stores after a bounce: the next ray, its remaining depth, throughput, RNG, id
-        if (W.tail_budget && active && !done && ++nb == W.tail_budget) {
-            const uint32_t e = atomicAdd(&W.len[(it + 1u) % 3u][src * RTW_WF_LEN_STRIDE], 1u);
-            wf_store_path<FEAT>(W.set[(it + 1u) & 1u], src * W.stripe_cap + e, r, depth, thr, rng.s, pid, acc,
-                                W.packed != 0u);
             active = false;
         }
     }
@@ -1824,19 +1803,24 @@ uint32_t wf_grid(K kernel, int n_cu, size_t lds = 0, uint32_t threads = 256) {
     return g ? g : per;
 }
 
-// the same, cached per host thread for one dynamic LDS size (c = {grid, lds + 1})
+// grid-cache key of a launch shape on a device of n_cu CUs (never 0: an empty cache misses).  Every cache is
+// per host thread and keyed by the CU count too: a grid larger than the device's would overflow the stripes
+// that rtw_wavefront_max_waves(n_cu) sized.
+inline uint64_t wf_key(int n_cu, uint64_t shape) { return ((uint64_t)(uint32_t)n_cu << 40) | (shape + 1u); }
+
+// the same, cached per host thread for one dynamic LDS size (c = {grid, key})
 template <typename K>
-uint32_t wf_grid_cached(K kernel, int n_cu, size_t lds, uint32_t (&c)[2]) {
-    if (c[1] != lds + 1) {
+uint32_t wf_grid_cached(K kernel, int n_cu, size_t lds, uint64_t (&c)[2]) {
+    if (c[1] != wf_key(n_cu, lds)) {
         c[0] = wf_grid(kernel, n_cu, lds);
-        c[1] = (uint32_t)(lds + 1);
+        c[1] = wf_key(n_cu, lds);
     }
-    return c[0];
+    return (uint32_t)c[0];
 }
 
 // the global tail launch of either form
 template <uint32_t FEAT>
-void wf_launch_tail(const rtw_launch& L, const rtw_wf& W, hipStream_t st, int n_cu, size_t lds, uint32_t (&cache)[2],
+void wf_launch_tail(const rtw_launch& L, const rtw_wf& W, hipStream_t st, int n_cu, size_t lds, uint64_t (&cache)[2],
                     uint32_t it) {
     if constexpr ((FEAT & ~RTW_F_CHECKER) == 0)
         hipLaunchKernelGGL(wf_tail_w5<FEAT>, dim3(wf_grid_cached(wf_tail_w5<FEAT>, n_cu, lds, cache)), dim3(256), lds, st,
@@ -1844,27 +1828,6 @@ void wf_launch_tail(const rtw_launch& L, const rtw_wf& W, hipStream_t st, int n_
     else
         hipLaunchKernelGGL(wf_tail<FEAT>, dim3(wf_grid_cached(wf_tail<FEAT>, n_cu, lds, cache)), dim3(256), lds, st, L,
                            W, it);
-}
-
-// The tail of a batch: one launch over iteration iters' queue, or (deal bit 64) two -- RTW_WF_TAIL_BUDGET bounces
-// per path with the live paths requeued into the stripes they came from, then the rest to completion.  In the
-// second launch the longest paths start with the GPU nearly idle: the drain that sets the end of a small batch
-// (a shard of a multi-GPU render) is shorter.  `tail(Wd, it)` launches the configuration's tail kernel.
-template <uint32_t FEAT, class F>
-void wf_tail_launches(const rtw_launch& L, const rtw_wf& W, rtw_wf Wd, uint32_t iters, hipStream_t st, F&& tail) {
-    const bool two = W.deal && (W.deal_mode & 64u) && iters >= 1u && iters + RTW_WF_TAIL_BUDGET < L.max_depth;
-    if (!two) {
-        tail(Wd, iters);
-        return;
-    }
-    // the first launch appends to len[(iters + 1) % 3] (the split kernels leave it holding an older count)
-    (void)hipMemsetAsync(W.len[(iters + 1u) % 3u], 0, RTW_WF_STRIPES * RTW_WF_LEN_STRIDE * 4, st);
-    Wd.tail_budget = RTW_WF_TAIL_BUDGET;
-    tail(Wd, iters);
-    rtw_wf W2 = W;
-    W2.deal = W.deal + RTW_WF_DEAL_TAIL2;
-    W2.tail_budget = 0;
-    tail(W2, iters + RTW_WF_TAIL_BUDGET);
 }
 
 // dynamic LDS of the kernels that walk through L1/L2: the two-wide walk's per-lane stacks
@@ -1897,7 +1860,9 @@ rtw_wf wf_lists(const rtw_launch& L, const rtw_wf& W, hipStream_t st) {
 // up to 16 samples per tile, shorter when a wave would get fewer than 64 runs (a small batch: whole runs
 // would leave the waves' shares of work uneven); direction bucketing only when a wave's iteration 0 has at
 // least RTW_WF_SORT_MIN_CHUNKS chunks -- each open block ends its iteration partly dead, which only a large
-// share of survivors per wave amortises (simple_light, 137 chunks per wave: -10 % with bucketing).
+// share of survivors per wave amortises (simple_light, 137 chunks per wave: -10 % with bucketing).  Deal bit 128
+// (RTW_DEAL_SMALL_SORT) lifts that gate, so the tests run the bucketed queues of the large benched batches on small
+// images (tests/test_gpu_parity.py, test_gpu_objects.py).
 #define RTW_WF_SORT_MIN_CHUNKS 192u
 rtw_wf wf_coherence(const rtw_wf& W, uint32_t nw, uint32_t sort_iters) {
     rtw_wf C = W;
@@ -1909,13 +1874,14 @@ rtw_wf wf_coherence(const rtw_wf& W, uint32_t nw, uint32_t sort_iters) {
     if (per_wave < RTW_WF_SORT_MIN_CHUNKS && !(C.deal_mode & 8u)) C.deal = nullptr;  // (bit 8: tests force it)
     if (C.deal && (C.deal_mode & 1u)) lg = 4;  // dynamic deal: the waves balance themselves, runs keep 16 samples
     C.run_log2 = lg;
-    C.sort_iters = per_wave >= RTW_WF_SORT_MIN_CHUNKS ? sort_iters : 0u;
+    C.sort_iters = (per_wave >= RTW_WF_SORT_MIN_CHUNKS || (C.deal_mode & 128u)) ? sort_iters : 0u;
     return C;
 }
 
 template <uint32_t FEAT>
 struct WfGrids {
-    uint32_t shade, shade0;  // shade0: iteration 0's instantiation (wf_camera)
+    uint32_t shade = 0, shade0 = 0;  // shade0: iteration 0's instantiation (wf_camera)
+    WfGrids() = default;
     explicit WfGrids(int n_cu)
         : shade(wf_grid(wf_shade<FEAT>, n_cu)), shade0(wf_grid(wf_shade<FEAT, true>, n_cu)) {}
 };
@@ -1927,14 +1893,26 @@ struct WfGrids {
 template <uint32_t FEAT, bool CAM>
 uint32_t wf_lds_grid(int n_cu, size_t lds) {
     thread_local uint32_t cache[(RTW_WF_LDS_MAX + 16384) / 512 + 1] = {0};  // + geometry (L.geom_lds)
+    thread_local int cache_cu = 0;
+    if (cache_cu != n_cu) {
+        for (uint32_t& c : cache) c = 0;
+        cache_cu = n_cu;
+    }
     uint32_t& g = cache[lds / 512];
     if (!g) g = wf_grid(wf_trace<FEAT, true, CAM>, n_cu, lds);
     return g;
 }
 
+// (per CU count: a process may render on devices or partitions of different sizes; per host thread, as the
+// other grid caches)
 template <uint32_t FEAT>
 const WfGrids<FEAT>& wf_grids(int n_cu) {
-    static const WfGrids<FEAT> g(n_cu);
+    thread_local int key = 0;
+    thread_local WfGrids<FEAT> g{};
+    if (key != n_cu) {
+        g = WfGrids<FEAT>(n_cu);
+        key = n_cu;
+    }
     return g;
 }
 
@@ -1955,7 +1933,7 @@ void wf_run_fused(const rtw_launch& L, const rtw_wf& W0, hipStream_t st, int n_c
                         ((FEAT & RTW_F_GEOM) ? L.geom_lds : 0u) + L.shade_lds,
                  tdyn = lds + ((FEAT & RTW_F_GEOM) ? L.geom_lds : 0u) + L.shade_lds,
                  gdyn = wf_w2_lds<FEAT>(L);
-    thread_local uint32_t cgrid[2] = {0, 0}, tgrid[2] = {0, 0}, lgrid[2] = {0, 0}, ggrid[2] = {0, 0}, wtail[2] = {0, 0};
+    thread_local uint64_t cgrid[2] = {0, 0}, tgrid[2] = {0, 0}, lgrid[2] = {0, 0}, ggrid[2] = {0, 0}, wtail[2] = {0, 0};
     uint32_t grid = 0;
     // The compact stage's block shape: the 8-copy stage (C2: 124 KB) leaves room for one 1024-thread block
     // per CU; the 4-copy stage (L.n_orders == 4, 62 KB) for two blocks (rtw_tuning.clds_shape 2..4: of 512,
@@ -1967,7 +1945,7 @@ void wf_run_fused(const rtw_launch& L, const rtw_wf& W0, hipStream_t st, int n_c
     const size_t cdyn2 = two && cdyn > RTW_WF_CLDS2_MAX ? cdyn0 : cdyn;  // materials only if they fit too
     const uint32_t cthreads = shape == 2 ? 512u : shape == 3 ? 640u : shape == 4 ? 768u : 1024u;
     if constexpr ((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING)) == 0) {
-        const uint32_t key = (uint32_t)cdyn2 | (shape << 24) | ((uint32_t)cn << 28);
+        const uint64_t key = wf_key(n_cu, (uint32_t)cdyn2 | (shape << 24) | ((uint32_t)cn << 28));
         if (clds && cgrid[1] != key) {
             if (shape == 2) {
                 cgrid[0] = wf_grid(wf_step_clds2<FEAT, 512>, n_cu, cdyn2, 512);
@@ -1992,13 +1970,13 @@ void wf_run_fused(const rtw_launch& L, const rtw_wf& W0, hipStream_t st, int n_c
         }
     }
     if (clds) {
-        grid = cgrid[0];
+        grid = (uint32_t)cgrid[0];
     } else if (lds) {
-        if (lgrid[1] != ldyn) {
+        if (lgrid[1] != wf_key(n_cu, ldyn)) {
             lgrid[0] = wf_grid(wf_step<FEAT, true>, n_cu, ldyn);
-            lgrid[1] = (uint32_t)ldyn;
+            lgrid[1] = wf_key(n_cu, ldyn);
         }
-        grid = lgrid[0];
+        grid = (uint32_t)lgrid[0];
     } else {
         grid = wf_grid_cached(wf_step<FEAT, false>, n_cu, gdyn, ggrid);
     }
@@ -2055,34 +2033,34 @@ void wf_run_fused(const rtw_launch& L, const rtw_wf& W0, hipStream_t st, int n_c
                 if (clds && (L.wf_fuse & 2u)) {
                     const rtw_wf& W = Wd;
                     if (shape == 2)
-                        hipLaunchKernelGGL((wf_tail_clds2<FEAT, 512>), dim3(tgrid[0]), dim3(512), clds, st, L, W, itx);
+                        hipLaunchKernelGGL((wf_tail_clds2<FEAT, 512>), dim3((uint32_t)tgrid[0]), dim3(512), clds, st, L, W, itx);
                     else if (shape == 3)
-                        hipLaunchKernelGGL((wf_tail_clds2<FEAT, 640>), dim3(tgrid[0]), dim3(640), clds, st, L, W, itx);
+                        hipLaunchKernelGGL((wf_tail_clds2<FEAT, 640>), dim3((uint32_t)tgrid[0]), dim3(640), clds, st, L, W, itx);
                     else if (shape == 4)
-                        hipLaunchKernelGGL((wf_tail_clds2<FEAT, 768>), dim3(tgrid[0]), dim3(768), clds, st, L, W, itx);
+                        hipLaunchKernelGGL((wf_tail_clds2<FEAT, 768>), dim3((uint32_t)tgrid[0]), dim3(768), clds, st, L, W, itx);
                     else if (cn == CN_F32_4)
-                        hipLaunchKernelGGL((wf_tail_clds<FEAT, CN_F32_4>), dim3(tgrid[0]), dim3(1024), clds, st, L, W, itx);
+                        hipLaunchKernelGGL((wf_tail_clds<FEAT, CN_F32_4>), dim3((uint32_t)tgrid[0]), dim3(1024), clds, st, L, W, itx);
                     else if (cn == CN_F16_4)
-                        hipLaunchKernelGGL((wf_tail_clds<FEAT, CN_F16_4>), dim3(tgrid[0]), dim3(1024), clds, st, L, W, itx);
+                        hipLaunchKernelGGL((wf_tail_clds<FEAT, CN_F16_4>), dim3((uint32_t)tgrid[0]), dim3(1024), clds, st, L, W, itx);
                     else
-                        hipLaunchKernelGGL((wf_tail_clds<FEAT, CN_F16_8>), dim3(tgrid[0]), dim3(1024), clds, st, L, W, itx);
+                        hipLaunchKernelGGL((wf_tail_clds<FEAT, CN_F16_8>), dim3((uint32_t)tgrid[0]), dim3(1024), clds, st, L, W, itx);
                     return;
                 }
             }
             if (lds && (L.wf_fuse & 2u)) {  // the node array in LDS for the tail too
-                thread_local uint32_t tl[2] = {0, 0};
-                if (tl[1] != tdyn) {
+                thread_local uint64_t tl[2] = {0, 0};
+                if (tl[1] != wf_key(n_cu, tdyn)) {
                     tl[0] = wf_grid(wf_tail_lds<FEAT>, n_cu, tdyn);
-                    tl[1] = (uint32_t)tdyn;
+                    tl[1] = wf_key(n_cu, tdyn);
                 }
-                hipLaunchKernelGGL(wf_tail_lds<FEAT>, dim3(tl[0]), dim3(256), tdyn, st, L, Wd, itx);
+                hipLaunchKernelGGL(wf_tail_lds<FEAT>, dim3((uint32_t)tl[0]), dim3(256), tdyn, st, L, Wd, itx);
                 return;
             }
             wf_launch_tail<FEAT>(L, Wd, st, n_cu, gdyn, wtail, itx);
         };
         rtw_wf Wd = W;  // the tail's input claims: counter 512 (iteration 0 took 0 .. 511)
         if (W.deal) Wd.deal = W.deal + RTW_WF_DEAL_LAUNCH;
-        wf_tail_launches<FEAT>(L, W, Wd, iters, st, tail);
+        tail(Wd, iters);
         RTW_TIME_END(T)
     }
     RTW_TIME_BEGIN(T, RTW_K_REDUCE)
@@ -2124,7 +2102,7 @@ void wf_run(const rtw_launch& L, const rtw_wf& W0, hipStream_t st, int n_cu, rtw
     rtw_wf Ws0 = W;  // iteration 0's shade: its own counters
     if (W.deal) Ws0.deal = W.deal + RTW_WF_DEAL_LAUNCH;
     const size_t w2l = wf_w2_lds<FEAT>(L);  // the two-wide walk's stacks (trace / tail through L1/L2)
-    thread_local uint32_t wtrace[2] = {0, 0}, wtrace0[2] = {0, 0}, wtail[2] = {0, 0};
+    thread_local uint64_t wtrace[2] = {0, 0}, wtrace0[2] = {0, 0}, wtail[2] = {0, 0};
     const size_t lds_need = (size_t)L.n_nodes * L.n_orders * 32u;
     const size_t lds = (L.wf_lds && lds_need <= RTW_WF_LDS_MAX)
                            ? (lds_need + 511u) / 512u * 512u : 0;
@@ -2134,18 +2112,18 @@ void wf_run(const rtw_launch& L, const rtw_wf& W0, hipStream_t st, int n_cu, rtw
     // compact nodes of every octant copy in LDS (small static sphere trees)
     const size_t clds = (L.cnodes && L.fast_box && L.wf_clds)
                             ? (size_t)L.n_nodes * L.n_orders * (L.cnode32 ? 32u : 16u) : 0;
-    thread_local uint32_t clds_grid_cache[3] = {0, 0, 0};
+    thread_local uint64_t clds_grid_cache[3] = {0, 0, 0};
     uint32_t clds_grid = 0, clds_grid0 = 0;
     constexpr uint32_t clds_threads = 1024;  // one block per CU shares the stage (256 / 512: slower)
     if constexpr ((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING)) == 0) {
         if (clds && clds <= RTW_WF_CLDS_MAX) {
-            if (!clds_grid_cache[0] || clds_grid_cache[1] != clds) {  // (the Y4 forms: the same registers)
+            if (clds_grid_cache[1] != wf_key(n_cu, clds)) {  // (the Y4 forms: the same registers)
                 clds_grid_cache[0] = wf_grid(wf_trace_clds<FEAT>, n_cu, clds, clds_threads);
                 clds_grid_cache[2] = wf_grid(wf_trace_clds<FEAT, true>, n_cu, clds, clds_threads);
-                clds_grid_cache[1] = (uint32_t)clds;
+                clds_grid_cache[1] = wf_key(n_cu, clds);
             }
-            clds_grid = clds_grid_cache[0];
-            clds_grid0 = clds_grid_cache[2];
+            clds_grid = (uint32_t)clds_grid_cache[0];
+            clds_grid0 = (uint32_t)clds_grid_cache[2];
         }
     }
     for (uint32_t it = 0; it < iters; it++) {
@@ -2199,18 +2177,18 @@ void wf_run(const rtw_launch& L, const rtw_wf& W0, hipStream_t st, int n_cu, rtw
         if (W.deal) Wd.deal = W.deal + 2 * RTW_WF_DEAL_LAUNCH;
         auto tail = [&](const rtw_wf& Wx, uint32_t itx) {
             if (lds && (L.wf_fuse & 2u)) {  // the node array (+ geometry) in LDS for the tail (smoke +5 %)
-                thread_local uint32_t tl[2] = {0, 0};
+                thread_local uint64_t tl[2] = {0, 0};
                 const size_t tdyn = tlds + L.shade_lds;  // wf_tail_lds stages the materials too
-                if (tl[1] != tdyn) {
+                if (tl[1] != wf_key(n_cu, tdyn)) {
                     tl[0] = wf_grid(wf_tail_lds<FEAT>, n_cu, tdyn);
-                    tl[1] = (uint32_t)tdyn;
+                    tl[1] = wf_key(n_cu, tdyn);
                 }
-                hipLaunchKernelGGL(wf_tail_lds<FEAT>, dim3(tl[0]), dim3(256), tdyn, st, L, Wx, itx);
+                hipLaunchKernelGGL(wf_tail_lds<FEAT>, dim3((uint32_t)tl[0]), dim3(256), tdyn, st, L, Wx, itx);
             } else {
                 wf_launch_tail<FEAT>(L, Wx, st, n_cu, w2l, wtail, itx);
             }
         };
-        wf_tail_launches<FEAT>(L, W, Wd, iters, st, tail);
+        tail(Wd, iters);
         RTW_TIME_END(T)
     }
     RTW_TIME_BEGIN(T, RTW_K_REDUCE)
@@ -2272,18 +2250,24 @@ void rtw_wf_run_spheres(const rtw_launch& L, const rtw_wf& W, hipStream_t st, in
     else wf_run<0u>(L, W, st, n_cu, T);
 }
 
-// (waves: the 256-thread shade grids and the compact-LDS kernels' grids, whichever launches more)
+// (waves: the 256-thread shade grids and the compact-LDS kernels' grids, whichever launches more; computed per
+// CU count -- it sizes the stripes, which the kernels do not bound-check)
 uint32_t rtw_wf_spheres_max_waves(int n_cu) {
+    thread_local int key = 0;
+    thread_local uint32_t val = 0;
+    if (key == n_cu) return val;
     const uint32_t b = std::max({wf_grids<0u>(n_cu).shade, wf_grids<0u>(n_cu).shade0, wf_grids<RTW_F_CHECKER>(n_cu).shade,
                                  wf_grids<RTW_F_CHECKER>(n_cu).shade0});
-    static const uint32_t c2 = std::max({wf_grid(wf_step_clds2<0u, 512>, n_cu, 0, 512) * 8u,
+    const uint32_t c2 = std::max({wf_grid(wf_step_clds2<0u, 512>, n_cu, 0, 512) * 8u,
                                          wf_grid(wf_step_clds2<0u, 640>, n_cu, 0, 640) * 10u,
                                          wf_grid(wf_step_clds2<0u, 768>, n_cu, 0, 768) * 12u,
                                          wf_grid(wf_step_clds2<RTW_F_CHECKER, 512>, n_cu, 0, 512) * 8u,
                                          wf_grid(wf_step_clds2<RTW_F_CHECKER, 640>, n_cu, 0, 640) * 10u,
                                          wf_grid(wf_step_clds2<RTW_F_CHECKER, 768>, n_cu, 0, 768) * 12u});
-    static const uint32_t c1 = std::max(wf_grid(wf_step_clds<0u>, n_cu, 0, 1024), wf_grid(wf_step_clds<RTW_F_CHECKER>, n_cu, 0, 1024)) * 16u;
-    return std::max({4u * b, c2, c1});
+    const uint32_t c1 = std::max(wf_grid(wf_step_clds<0u>, n_cu, 0, 1024), wf_grid(wf_step_clds<RTW_F_CHECKER>, n_cu, 0, 1024)) * 16u;
+    val = std::max({4u * b, c2, c1});
+    key = n_cu;
+    return val;
 }
 
 #if defined(RTW_DIAG_WALK)  // (the sphere-scene kernels' records and counters: this translation unit's)
