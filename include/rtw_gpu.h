@@ -348,9 +348,9 @@ typedef struct rtw_tuning {
                                   test the instance's world box before its transforms and members (ABI 5,
                                   formerly padding) */
     uint32_t clds_shape;       /* compact-LDS kernels (fused step, tail) of a 4-copy tree: 0 = auto (= 4), 1 = one
-                                  1024-thread block per CU, 2 / 3 / 4 = two blocks of 512 / 640 / 768 threads
-                                  (4 / 5 / 6 waves per SIMD) when the stage fits half the LDS; the 8-copy stage
-                                  always runs one block (ABI 7) */
+                                  1024-thread block per CU, 4 = two blocks of 768 threads (6 waves per SIMD) when
+                                  the stage fits half the LDS; the 8-copy stage always runs one block (ABI 7; ABI 8
+                                  refuses the former 2 / 3, two blocks of 512 / 640 threads, which lost their A/Bs) */
     uint32_t deal;             /* how the wavefront's waves share work (ABI 8), RTW_DEAL_* bits; 0 = all static,
                                   default 59 = RUNS | TAIL | SMALL | ITERS | SINGLES16 */
 } rtw_tuning;

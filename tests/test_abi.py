@@ -212,3 +212,26 @@ def test_deal_bits_header_and_validation(rtw):
         with pytest.raises(rtw.RtwError) as e:
             rtw.World(arr, device=A.RTW_DEVICE_CPU, tuning={"deal": deal})
         assert e.value.code == A.RTW_E_INVALID
+    # (ABI 8: clds_shape 2 / 3, the 512- / 640-thread two-block shapes, were removed with the losing modes)
+    for shape in (0, 1, 4):
+        rtw.World(arr, device=A.RTW_DEVICE_CPU, tuning={"clds_shape": shape}).close()
+    for shape in (2, 3, 5):
+        with pytest.raises(rtw.RtwError):
+            rtw.World(arr, device=A.RTW_DEVICE_CPU, tuning={"clds_shape": shape})
+
+
+def test_resource_report_is_this_build(rtw):
+    """profiles/isa_resources.json (make -C zig-raytracing-weekend_amd/csrc resources): VGPR / SGPR / scratch /
+    occupancy of every wavefront kernel, read from the gfx950 assembly of these sources -- stamped with the build id
+    of the in-tree library, so a source change without a regenerated table fails here."""
+    import json
+    path = os.path.join(REPO, "profiles", "isa_resources.json")
+    rep = json.load(open(path))
+    assert rep["build_id"] == rtw.lib().rtw_build_id().decode(), "stale: run make -C zig-raytracing-weekend_amd/csrc resources"
+    k = rep["kernels"]
+    for name in ("wf_step_clds2<0u, 768u>", "wf_tail_clds2<0u, 768u>", "wf_tail_w5<0u>", "wf_trace<0u, false, false>",
+                 "wf_shade<0u, false>", "wf_step<49u, true>", "wf_tail_lds<49u>", "wf_step<7u, true>", "wf_reduce"):
+        assert name in k, name
+        assert k[name]["vgpr"] and k[name]["occupancy"], (name, k[name])
+    # the 6-wave shapes fit 80 VGPRs (MI355X_MICROARCH.md: 80 allocated -> 6 waves / SIMD)
+    assert k["wf_step_clds2<0u, 768u>"]["vgpr"] <= 80 and k["wf_step_clds2<0u, 768u>"]["occupancy"] == 6

@@ -160,7 +160,7 @@ def test_four_copy_stage_full_c2(rtw, book1):
     arr, world = book1
     cam = rtw.book1_camera().init()
     ref = render_rows(rtw, world, cam, 0, 800, 0, 6, 2)
-    for tu in ({"bvh_orders": 4}, {"bvh_orders": 4, "clds_shape": 2}, {"bvh_orders": 4, "clds_shape": 3},
+    for tu in ({"bvh_orders": 4}, {"bvh_orders": 4, "clds_shape": 1},
                {"bvh_orders": 4, "clds_shape": 4}, {"bvh_orders": 4, "fuse": 0}, {"bvh_orders": 4, "compact_nodes": 2},
                {"bvh_orders": 4, "compact_nodes": 2, "fuse": 0}):
         w = rtw.World(arr, tuning=tu)
@@ -337,7 +337,7 @@ def test_v1_knobs_invariant(rtw, book1, knob):
                                   {"lds": 127 & ~2, "fuse": 5, "wide_walk": 0}, {"hoist": 0}, {"hoist": 0, "fuse": 0},
                                   {"sort_iters": 0}, {"sort_iters": 50}, {"sort_iters_split": 50, "fuse": 0}, {"sort_iters_split": 0, "fuse": 0},
                                   {"sort_iters": 2, "wf_iters": 1}, {"sort_bits": 0}, {"sort_bits": 2, "fuse": 0}, {"wf_iters": 3, "fuse": 0},
-                                  {"bvh_orders": 4}, {"bvh_orders": 4, "clds_shape": 3}, {"bvh_orders": 4, "fuse": 0},
+                                  {"bvh_orders": 4}, {"bvh_orders": 4, "clds_shape": 1}, {"bvh_orders": 4, "fuse": 0},
                                   {"bvh_orders": 4, "lds": 127 & ~2}, {"bvh_orders": 4, "wide_walk": 0, "lds": 127 & ~2},
                                   {"bvh_orders": 4, "compact_nodes": 0}, {"bvh_orders": 4, "kernel": 1},
                                   {"bvh_orders": 4, "kernel": 2}, {"bvh_orders": 4, "compact_nodes": 2},

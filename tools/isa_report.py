@@ -8,6 +8,10 @@ loop is the one that loads BVH nodes (ds_read_b128 from the LDS stage, or global
 
 Usage: python tools/isa_report.py build/isa/rtw_wavefront_all.s wf_step_cldsILj0E wf_traceILj0ELb0E wf_tail_cldsILj0E
        [--json out.json]
+       python tools/isa_report.py build/isa/rtw_wavefront_all.s --resources profiles/isa_resources.json
+         the build-stamped resource table of every wavefront kernel (VGPR / SGPR / scratch / occupancy / code
+         bytes), stamped with the in-tree library's rtw_build_id() (tests/test_abi.py checks the stamp);
+         `make -C zig-raytracing-weekend_amd/csrc resources` runs both steps
 """
 from __future__ import annotations
 
@@ -108,13 +112,52 @@ def hist(seq):
     return dict(sorted(c.items(), key=lambda kv: -kv[1]))
 
 
+def demangle(sym):
+    """_ZN12_GLOBAL__N_113wf_step_clds2ILj0ELj768EEEv... -> wf_step_clds2<0u, 768u> (template ints / bools only)."""
+    pre = "_ZN12_GLOBAL__N_1"
+    if not sym.startswith(pre):
+        return sym
+    m = re.match(r"(\d+)", sym[len(pre):])
+    if not m:
+        return sym
+    n = int(m.group(1))
+    k = len(pre) + len(m.group(1))
+    name, rest = sym[k:k + n], sym[k + n:]
+    if not rest.startswith("I"):
+        return name
+    args = re.findall(r"L([jib])(\d+)E", rest[:rest.index("EE") + 1] if "EE" in rest else rest)
+    pretty = [("true" if v == "1" else "false") if t == "b" else (v + "u" if t == "j" else v) for t, v in args]
+    return f"{name}<{', '.join(pretty)}>"
+
+
+def write_resources(text, path):
+    import ctypes
+    import os
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    lib = ctypes.CDLL(os.path.join(repo, "zig-raytracing-weekend_amd", "librtw_gpu.so"))
+    lib.rtw_build_id.restype = ctypes.c_char_p
+    table = {}
+    for sym, body, meta in kernels(text):
+        table[demangle(sym)] = {k: meta.get(k) for k in ("vgpr", "agpr", "sgpr", "scratch", "occupancy", "code_bytes")}
+    out = {"build_id": lib.rtw_build_id().decode(), "source": "tools/isa_report.py --resources over "
+           "`make isa` (both wavefront translation units, product flags)", "kernels": table}
+    with open(path, "w") as f:
+        json.dump(out, f, indent=1, sort_keys=True)
+    spill = {k: v["scratch"] for k, v in table.items() if v.get("scratch")}
+    print(f"{len(table)} kernels, build {out['build_id']}; with scratch: {spill}")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("asm")
-    ap.add_argument("names", nargs="+")
+    ap.add_argument("names", nargs="*")
     ap.add_argument("--json")
+    ap.add_argument("--resources", help="write the build-stamped resource table of every kernel to this file")
     a = ap.parse_args()
     text = open(a.asm).read()
+    if a.resources:
+        write_resources(text, a.resources)
+        return
     report = {}
     for sym, body, meta in kernels(text):
         if not any(n in sym for n in a.names):

@@ -962,128 +962,3 @@ bool rtw_wide2_nodes(const std::vector<rtw_node>& nodes, uint32_t n_per, std::ve
     if (max_stack) *max_stack = dmax;
     return true;
 }
-
-// ---------------------------------------------------------------------------
-// Four-wide records (round 5 experiment; built with -DRTW_WIDE4): the binary tree of
-// rtw_wide2_nodes collapsed to up to 4 children per record (an inner child with the largest box area is
-// replaced by its two children until 4 slots are used), 64 B per record = one cache line, leaves first.
-// Slots as rtw_wide2_nodes; an unused slot is RTW_W4_EMPTY (no leaf bit, never entered).
-// leaf_id[4 * record + k] = the leaf's ordering-0 index.  *max_stack = the deepest the walk can push
-// (per record path, the sum of (inner slots - 1) of its ancestors, + its own).
-bool rtw_wide4_nodes(const std::vector<rtw_node>& nodes, uint32_t n_per, std::vector<rtw_cnode>& out,
-                     std::vector<uint32_t>& leaf_id, uint32_t* max_stack) {
-    auto word = [&](uint32_t i) {
-        uint32_t w;
-        std::memcpy(&w, &nodes[i].a[3], 4);
-        return w;
-    };
-    uint32_t h = 0;
-    while (h < n_per && (word(h) & RTW_LEAF_BIT)) h++;
-    if (n_per < h + 3 || nodes.size() < n_per) return false;
-    auto next = [&](uint32_t j) { return (word(j) & RTW_LEAF_BIT) ? j + 1 : (word(j) & RTW_SKIP_MASK); };
-    // binary view: real nodes 0..n_per-1, virtual node n_per + k (k < h): children (hoisted sphere k, the rest)
-    std::vector<float> vbox(6 * (size_t)h);
-    {
-        float mn[3], mx[3];
-        for (int a = 0; a < 3; a++) {
-            mn[a] = nodes[h].a[a];
-            mx[a] = nodes[h].b[a];
-        }
-        for (uint32_t k = h; k-- > 0;) {
-            const float r = std::fabs(nodes[k].b[0]), pad = 1e-3f * (r + 1.0f);
-            for (int a = 0; a < 3; a++) {
-                mn[a] = std::min(mn[a], nodes[k].a[a] - r - pad);
-                mx[a] = std::max(mx[a], nodes[k].a[a] + r + pad);
-                vbox[6 * k + a] = mn[a];
-                vbox[6 * k + 3 + a] = mx[a];
-            }
-        }
-    }
-    auto is_leaf = [&](uint32_t x) { return x < n_per && (word(x) & RTW_LEAF_BIT); };
-    auto children = [&](uint32_t x, uint32_t c[2]) {
-        if (x >= n_per) {
-            const uint32_t k = x - n_per;
-            c[0] = k;
-            c[1] = k + 1 < h ? n_per + k + 1 : h;
-            return true;
-        }
-        c[0] = x + 1;
-        c[1] = next(x + 1);
-        return c[1] < n_per && next(c[1]) == (word(x) & RTW_SKIP_MASK);
-    };
-    auto bmin = [&](uint32_t x) { return x >= n_per ? &vbox[6 * (size_t)(x - n_per)] : nodes[x].a; };
-    auto bmax = [&](uint32_t x) { return x >= n_per ? &vbox[6 * (size_t)(x - n_per) + 3] : nodes[x].b; };
-    auto area = [&](uint32_t x) {
-        const float *a = bmin(x), *b = bmax(x);
-        const float dx = b[0] - a[0], dy = b[1] - a[1], dz = b[2] - a[2];
-        return dx * dy + dy * dz + dz * dx;
-    };
-    out.clear();
-    leaf_id.clear();
-    uint32_t deepest = 0;
-    // records in DFS pre-order: (binary inner node, record index, stack depth of its ancestors)
-    struct Job { uint32_t x, rec, acc; };
-    std::vector<Job> todo;
-    auto new_record = [&]() {
-        const uint32_t r = (uint32_t)(out.size() / 4);
-        out.resize(out.size() + 4, rtw_cnode{});
-        leaf_id.resize(leaf_id.size() + 4, 0u);
-        for (int k = 0; k < 4; k++) out[4 * (size_t)r + k].v[3] = RTW_W4_EMPTY;
-        return r;
-    };
-    todo.push_back({h > 0 ? n_per : h, new_record(), 0u});
-    while (!todo.empty()) {
-        const Job jb = todo.back();
-        todo.pop_back();
-        std::vector<uint32_t> list;
-        uint32_t c[2];
-        if (!children(jb.x, c)) return false;
-        list.assign(c, c + 2);
-        while (list.size() < 4) {
-            int best = -1;
-            float ba = -1.0f;
-            for (size_t i = 0; i < list.size(); i++)
-                if (!is_leaf(list[i]) && area(list[i]) > ba) {
-                    ba = area(list[i]);
-                    best = (int)i;
-                }
-            if (best < 0) break;
-            if (!children(list[best], c)) return false;
-            list[best] = c[0];
-            list.insert(list.begin() + best + 1, c[1]);
-        }
-        std::stable_partition(list.begin(), list.end(), [&](uint32_t x) { return is_leaf(x); });
-        uint32_t n_inner = 0;
-        for (uint32_t x : list) n_inner += is_leaf(x) ? 0u : 1u;
-        const uint32_t acc = jb.acc + (n_inner ? n_inner - 1u : 0u);
-        deepest = std::max(deepest, acc);
-        for (size_t k = 0; k < list.size(); k++) {
-            const uint32_t x = list[k];
-            const size_t slot = 4 * (size_t)jb.rec + k;
-            if (is_leaf(x)) {
-                const rtw_node& n = nodes[x];
-                uint32_t mv;
-                std::memcpy(&mv, &n.b[3], 4);
-                const float rr = n.b[0] * n.b[0];
-                uint32_t rb;
-                std::memcpy(&rb, &rr, 4);
-                if (mv || !(rr >= 0) || !std::isfinite(rr) || (rb & RTW_LEAF_BIT)) return false;
-                std::memcpy(&out[slot].v[0], &n.a[0], 12);
-                out[slot].v[3] = rb | RTW_LEAF_BIT;
-                leaf_id[slot] = x;
-                continue;
-            }
-            const float *mn = bmin(x), *mx = bmax(x);
-            for (int a = 0; a < 3; a++) {
-                if (!(std::fabs(mn[a]) <= 60000.0f) || !(std::fabs(mx[a]) <= 60000.0f)) return false;
-                out[slot].v[a] = (uint32_t)h_down(mn[a]) | ((uint32_t)h_up(mx[a]) << 16);
-            }
-            const uint32_t rec = new_record();
-            if (rec >= RTW_W4_EMPTY) return false;
-            out[slot].v[3] = rec;
-            todo.push_back({x, rec, acc});
-        }
-    }
-    if (max_stack) *max_stack = deepest;
-    return true;
-}

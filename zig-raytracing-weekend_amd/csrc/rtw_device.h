@@ -26,8 +26,9 @@
 #pragma clang fp contract(off)
 
 #ifndef RTW_STEPS
-#define RTW_STEPS 1
+#define RTW_STEPS 1  // the persistent megakernel's node steps per readiness check (rtw_kernels.hip)
 #endif
+
 
 #if defined(RTW_ABLATE_MATH) && defined(__HIP_DEVICE_COMPILE__)
 // timing ablation only (not IEEE): hardware sqrt / reciprocal
@@ -998,76 +999,6 @@ RTW_DHD int traverse_compact(const rtw_launch& L, const uint4* base, const Ray& 
     WalkDiag dgv;
     WalkDiag* dg = &dgv;
     dgv.walks = 1;
-#endif
-#if defined(RTW_WALK_PREFETCH) && defined(__HIP_DEVICE_COMPILE__)
-    if constexpr (LDS && !Y4) {
-        // A/B variant: the pre-order successor i + 16 (a leaf's next node, an entered box's first child)
-        // is read while node i is tested; a lane whose next node is the skip target reads it then
-        uint4 c = *(lds_uint4*)(uintptr_t)i;
-        while (i < end) {
-            const uint32_t ip = i + 16u < end ? i + 16u : end - 16u;
-            const uint4 cn = *(lds_uint4*)(uintptr_t)ip;
-            uint32_t next;
-            if (c.w & RTW_LEAF_BIT) {
-                if constexpr (COUNT) cnt.leaves++;
-                sphere_leaf(L, r, rt, mk(ubits(c.x), ubits(c.y), ubits(c.z)), ubits(c.w & ~RTW_LEAF_BIT), i, closest,
-                            hit);
-                next = i + 16u;
-            } else {
-                if constexpr (COUNT) cnt.nodes++;
-                const float tnx = __builtin_fmaf(h_lo(c.x), rt.inv.x, rt.oinv.x);
-                const float tny = __builtin_fmaf(h_hi(c.x), rt.inv.y, rt.oinv.y);
-                const float tnz = __builtin_fmaf(h_lo(c.y), rt.inv.z, rt.oinv.z);
-                const float tfx = __builtin_fmaf(h_hi(c.y), rt.inv.x, rt.oinv.x);
-                const float tfy = __builtin_fmaf(h_lo(c.z), rt.inv.y, rt.oinv.y);
-                const float tfz = __builtin_fmaf(h_hi(c.z), rt.inv.z, rt.oinv.z);
-                const float lo = __builtin_fmaxf(__builtin_fmaxf(kTmin, tnx), __builtin_fmaxf(tny, tnz));
-                const float hi = __builtin_fminf(__builtin_fminf(closest, tfx), __builtin_fminf(tfy, tfz));
-                next = (hi <= lo) ? c.w : i + 16u;
-            }
-            if (next == i + 16u) c = cn;
-            else if (next < end) c = *(lds_uint4*)(uintptr_t)next;
-            i = next;
-        }
-        t_out = closest;
-        return hit_with_order(hit < 0 ? hit : (int)(((uint32_t)hit - a0) >> 4), oct);
-    }
-#endif
-#if defined(RTW_LEAF_POSTPONE) && defined(__HIP_DEVICE_COMPILE__)
-    if constexpr (LDS && !Y4) {
-        // A/B variant: a lane that reaches a leaf waits there (its walk is unchanged: every box test and
-        // sphere test of the lane happens in the same order with the same closest) until at least
-        // 1/RTW_LEAF_POSTPONE of the wave's walking lanes wait too, or no walking lane is at an inner node;
-        // the wave then runs the leaf code once for all of them
-        while (i < end) {
-            const uint4 c = *(lds_uint4*)(uintptr_t)i;
-            const bool leaf = (c.w & RTW_LEAF_BIT) != 0;
-            const uint64_t walking = __ballot(1), at_leaf = __ballot(leaf);
-            const bool run_leaves = at_leaf == walking ||
-                                    (uint32_t)__popcll(at_leaf) * (uint32_t)RTW_LEAF_POSTPONE >= (uint32_t)__popcll(walking);
-            if (leaf) {
-                if (run_leaves) {
-                    if constexpr (COUNT) cnt.leaves++;
-                    sphere_leaf(L, r, rt, mk(ubits(c.x), ubits(c.y), ubits(c.z)), ubits(c.w & ~RTW_LEAF_BIT), i,
-                                closest, hit);
-                    i += 16u;
-                }
-            } else {
-                if constexpr (COUNT) cnt.nodes++;
-                const float tnx = __builtin_fmaf(h_lo(c.x), rt.inv.x, rt.oinv.x);
-                const float tny = __builtin_fmaf(h_hi(c.x), rt.inv.y, rt.oinv.y);
-                const float tnz = __builtin_fmaf(h_lo(c.y), rt.inv.z, rt.oinv.z);
-                const float tfx = __builtin_fmaf(h_hi(c.y), rt.inv.x, rt.oinv.x);
-                const float tfy = __builtin_fmaf(h_lo(c.z), rt.inv.y, rt.oinv.y);
-                const float tfz = __builtin_fmaf(h_hi(c.z), rt.inv.z, rt.oinv.z);
-                const float lo = __builtin_fmaxf(__builtin_fmaxf(kTmin, tnx), __builtin_fmaxf(tny, tnz));
-                const float hi = __builtin_fminf(__builtin_fminf(closest, tfx), __builtin_fminf(tfy, tfz));
-                i = (hi <= lo) ? c.w : i + 16u;
-            }
-        }
-        t_out = closest;
-        return hit_with_order(hit < 0 ? hit : (int)(((uint32_t)hit - a0) >> 4), oct);
-    }
 #endif
     while (i < end) {
         uint4 c;

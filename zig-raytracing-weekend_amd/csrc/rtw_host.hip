@@ -179,7 +179,8 @@ int rtw_scene_create_ex(const rtw_scene_desc* d, int device, const rtw_tuning* t
     if (tu.kernel > RTW_KERNEL_SIMPLE) return fail(RTW_E_INVALID, "tuning.kernel out of range");
     if (tu.bvh_orders != 0 && tu.bvh_orders != 1 && tu.bvh_orders != 4 && tu.bvh_orders != 8)
         return fail(RTW_E_INVALID, "tuning.bvh_orders must be 0, 1, 4 or 8");
-    if (tu.clds_shape > 4) return fail(RTW_E_INVALID, "tuning.clds_shape must be 0..4");
+    if (tu.clds_shape != 0 && tu.clds_shape != 1 && tu.clds_shape != 4)
+        return fail(RTW_E_INVALID, "tuning.clds_shape must be 0, 1 or 4 (ABI 8)");
     if (tu.deal & ~(uint32_t)RTW_DEAL_ALL)
         return fail(RTW_E_INVALID, "tuning.deal: bits 1 | 2 | 8 | 16 | 32 | 128 (RTW_DEAL_*)");
     if (tu.wf_iters > RTW_WF_MAX_ITERS) return fail(RTW_E_INVALID, "tuning.wf_iters out of range");
@@ -266,15 +267,9 @@ int rtw_scene_create_ex(const rtw_scene_desc* d, int device, const rtw_tuning* t
     std::vector<rtw_cnode> w2;
     std::vector<uint32_t> w2leaf;
     uint32_t w2_stack = 0;
-#ifdef RTW_WIDE4
-    if (!cnodes.empty() && !cnode32 && tu.wide_walk && tu.sah_max_leaf <= 1 &&
-        !rtw_wide4_nodes(ctx->nodes_host, (uint32_t)(ctx->nodes_host.size() / orders), w2, w2leaf, &w2_stack))
-        w2.clear();
-#else
     if (!cnodes.empty() && !cnode32 && tu.wide_walk && tu.sah_max_leaf <= 1 &&
         !rtw_wide2_nodes(ctx->nodes_host, (uint32_t)(ctx->nodes_host.size() / orders), w2, w2leaf, &w2_stack))
         w2.clear();
-#endif
     if (w2_stack > RTW_W2_STACK_MAX) w2.clear();
 
     // Blob layout (each section 256-B aligned): nodes | cvec | spheres | quads | members | instances | media |

@@ -73,7 +73,7 @@ struct rtw_launch {
     uint32_t n_orders;           // 1, or 4 / 8 sign-ordered copies of the node array (SAH sphere scenes)
     uint32_t cnode32;            // 1: cnodes are the 32-B fp32-box nodes (rtw_tuning.compact_nodes 2)
     uint32_t clds_shape;         // compact-LDS kernels of a 4-copy tree: 0 / 1 = one 1024-thread block per CU,
-                                 // 2 / 3 / 4 = two blocks of 512 / 640 / 768 threads (rtw_tuning.clds_shape)
+                                 // 4 = two blocks of 768 threads (rtw_tuning.clds_shape)
     uint32_t wf_lds;             // wavefront trace: stage the node array(s) in LDS when they fit
     uint32_t wf_clds;            // wavefront trace: stage the compact nodes (all orders) in LDS when they fit
     uint32_t wf_fuse;            // with the compact LDS stage: one gen+trace+shade kernel per iteration,
@@ -192,8 +192,6 @@ bool rtw_compact_nodes(const std::vector<rtw_node>& nodes, uint32_t orders, std:
 // two-wide 32-B records (2 x rtw_cnode per inner node) of ordering 0 for the stack walk of large static
 // sphere SAH trees (rtw_bvh.hip rtw_wide2_nodes); false: not encodable (leaf runs, fp16 range)
 bool rtw_wide2_nodes(const std::vector<rtw_node>& nodes, uint32_t n_per, std::vector<rtw_cnode>& out,
-                     std::vector<uint32_t>& leaf_id, uint32_t* max_stack);
-bool rtw_wide4_nodes(const std::vector<rtw_node>& nodes, uint32_t n_per, std::vector<rtw_cnode>& out,
                      std::vector<uint32_t>& leaf_id, uint32_t* max_stack);
 
 // hoist (SAH sphere scenes): emit spheres whose box dwarfs the rest ahead of the tree (*n_hoisted of them)

@@ -19,7 +19,6 @@
 #include <stdint.h>
 
 #define RTW_LEAF_BIT 0x80000000u
-#define RTW_W4_EMPTY 0x40000000u  // an unused slot of a four-wide record (rtw_wide4_nodes)
 #define RTW_SKIP_MASK 0x7FFFFFFFu
 
 struct rtw_node {

@@ -24,6 +24,8 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <map>
+#include <mutex>
 
 namespace {
 
@@ -668,107 +670,6 @@ __device__ __forceinline__ int traverse_wide2(const rtw_launch& L, const Ray& r,
     return hit < 0 ? hit : (int)L.w2leaf[hit];
 }
 
-#ifdef RTW_WIDE4
-// The four-wide form of the stack walk (rtw_bvh.hip rtw_wide4_nodes, -DRTW_WIDE4 builds): one 64-B record
-// per step, its leaf slots first (the wave runs the sphere test as often as its lanes' most leaves), then
-// up to 4 boxes; the nearest entered child is walked next and the others pushed.  Same superset argument
-// as traverse_wide2.
-template <bool COUNT>
-__device__ __forceinline__ int traverse_wide4(const rtw_launch& L, const Ray& r, float& t_out, Counters& cnt) {
-    extern __shared__ uint32_t wf_w2_stack[];
-    uint32_t* __restrict__ stk = wf_w2_stack + threadIdx.x;
-    const RayTrav rt = ray_trav(r, true);
-    constexpr uint32_t KEEP = 0x03020100u, SWAP = 0x01000302u;
-    const uint32_t sx = rt.inv.x < 0.0f ? SWAP : KEEP, sy = rt.inv.y < 0.0f ? SWAP : KEEP,
-                   sz = rt.inv.z < 0.0f ? SWAP : KEEP;
-    const uint4* __restrict__ wn = L.w2nodes;
-    float closest = kInf;
-    int hit = -1;
-    uint32_t node = 0, sp = 0;
-    for (;;) {
-        uint4 s[4];
-#pragma unroll
-        for (int k = 0; k < 4; k++) s[k] = wn[4u * node + k];
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            if (s[k].w & RTW_LEAF_BIT) {
-                if constexpr (COUNT) cnt.leaves++;
-                sphere_leaf(L, r, rt, mk(ubits(s[k].x), ubits(s[k].y), ubits(s[k].z)), ubits(s[k].w & ~RTW_LEAF_BIT),
-                            4u * node + k, closest, hit);
-            }
-        }
-#ifdef RTW_WIDE4_SORT
-        // entered children sorted by entry distance, farthest first (a 5-exchange network; others key -inf):
-        // the far ones are pushed, so the stack pops them nearest first
-        float key[4];
-        uint32_t w[4];
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            float lo, hi;
-            w2_box(s[k], rt, sx, sy, sz, closest, lo, hi);
-            const bool e = (s[k].w >> 30) == 0u && !(hi <= lo);
-            if constexpr (COUNT) cnt.nodes += (s[k].w >> 30) == 0u ? 1u : 0u;
-            key[k] = e ? lo : -kInf;
-            w[k] = s[k].w;
-        }
-        auto xchg = [&](int a, int b) {
-            const bool sw = key[a] < key[b];
-            const float ka = key[a];
-            const uint32_t wa = w[a];
-            key[a] = sw ? key[b] : ka;
-            key[b] = sw ? ka : key[b];
-            w[a] = sw ? w[b] : wa;
-            w[b] = sw ? wa : w[b];
-        };
-        xchg(0, 1);
-        xchg(2, 3);
-        xchg(0, 2);
-        xchg(1, 3);
-        xchg(1, 2);
-        const uint32_t n_in = (key[0] > -kInf ? 1u : 0u) + (key[1] > -kInf ? 1u : 0u) + (key[2] > -kInf ? 1u : 0u) +
-                              (key[3] > -kInf ? 1u : 0u);
-        const bool any = n_in != 0u;
-        uint32_t nxt = n_in == 4u ? w[3] : n_in == 3u ? w[2] : n_in == 2u ? w[1] : w[0];
-#pragma unroll
-        for (int k = 0; k < 3; k++) {
-            const bool push = (uint32_t)k + 1u < n_in;
-            if (push) stk[sp * 256u] = w[k];
-            sp += push ? 1u : 0u;
-        }
-#else
-        float best = kInf;
-        uint32_t nxt = 0;
-        bool in[4];
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            float lo, hi;
-            w2_box(s[k], rt, sx, sy, sz, closest, lo, hi);
-            in[k] = (s[k].w >> 30) == 0u && !(hi <= lo);
-            if constexpr (COUNT) cnt.nodes += (s[k].w >> 30) == 0u ? 1u : 0u;
-            const bool nearer = in[k] && lo < best;
-            best = nearer ? lo : best;
-            nxt = nearer ? s[k].w : nxt;
-        }
-        const bool any = in[0] || in[1] || in[2] || in[3];
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const bool push = in[k] && s[k].w != nxt;
-            if (push) stk[sp * 256u] = s[k].w;
-            sp += push ? 1u : 0u;
-        }
-#endif
-        const bool done = !any && sp == 0;
-        if (!any && !done) {
-            sp--;
-            nxt = stk[sp * 256u];
-        }
-        if (done) break;
-        node = nxt;
-    }
-    t_out = closest;
-    return hit < 0 ? hit : (int)L.w2leaf[hit];
-}
-#endif
 
 // the walk of a static sphere scene through L1/L2: two-wide when the records exist and the FMA slab
 // test is allowed (its fp16 boxes are supersets only of boxes padded for |o| <= 7 * extent: make_launch
@@ -778,11 +679,7 @@ __device__ __forceinline__ int wf_traverse_global(const rtw_launch& L, const Ray
                                                   uint64_t mkey) {
     if constexpr ((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING)) == 0) {
         if (L.w2nodes && L.fast_box)
-#ifdef RTW_WIDE4
-            return L.counters ? traverse_wide4<true>(L, r, t, cnt) : traverse_wide4<false>(L, r, t, cnt);
-#else
             return L.counters ? traverse_wide2<true>(L, r, t, cnt) : traverse_wide2<false>(L, r, t, cnt);
-#endif
     }
     return traverse<FEAT>(L.nodes, L, r, t, cnt, mkey);
 }
@@ -1665,22 +1562,14 @@ __device__ __forceinline__ void wf_step_clds_body(const rtw_launch& L, const rtw
 template <uint32_t FEAT, int CN = CN_F16_8>
 __global__ __launch_bounds__(1024) void wf_step_clds(rtw_launch L, rtw_wf W, uint32_t it) {
     static_assert((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING)) == 0, "static sphere scenes");
-#if defined(RTW_SETPRIO)
-    {   // A/B variant: the 4 waves a SIMD holds get priorities 0..3 (waves of one block go to SIMDs cyclically)
-        const uint32_t pr = __builtin_amdgcn_readfirstlane(threadIdx.x >> 8) & 3u;
-        if (pr == 1u) __builtin_amdgcn_s_setprio(1);
-        else if (pr == 2u) __builtin_amdgcn_s_setprio(2);
-        else if (pr == 3u) __builtin_amdgcn_s_setprio(3);
-    }
-#endif
     wf_step_clds_body<FEAT, CN == CN_F32_4 ? WALK_CLDS32 : CN == CN_F16_4 ? WALK_CLDS4 : WALK_CLDS>(L, W, it);
 }
 
-// The 4-copy stage (C2: 62 KB + 15.5 KB of materials) at two blocks per CU (rtw_tuning.clds_shape): 2 x 512
-// threads (4 waves per SIMD, as one 1024-thread block), 2 x 640 (5 waves, <= 96 VGPRs) or 2 x 768 (6 waves,
-// <= 80 VGPRs; MI355X_MICROARCH.md: 88-96 allocated -> 5 waves, 80 -> 6).
-// The fused step waits on its dependent ds_read_b128 41 % of the cycles at 4 waves (profiles/r4_stall/):
-// a fifth wave per SIMD has more ready work to issue in those waits.
+// The 4-copy stage (C2: 62 KB + 15.5 KB of materials) at two blocks of T = 768 threads per CU (rtw_tuning.clds_shape
+// 4, the default): 6 waves per SIMD at <= 80 VGPRs (MI355X_MICROARCH.md: 80 allocated -> 6).  The fused step waits on
+// its dependent ds_read_b128 41 % of the cycles at 4 waves (profiles/r4_stall/): the fifth and sixth waves have
+// ready work to issue in those waits.  (Two blocks of 512 or 640 threads lost their A/Bs -- profiles/r5_occupancy/,
+// diag/walk_variants.patch -- and were removed in round 6.)
 template <uint32_t FEAT, uint32_t T>
 __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(2 * T / 256)))
 void wf_step_clds2(rtw_launch L, rtw_wf W, uint32_t it) {
@@ -1903,17 +1792,16 @@ uint32_t wf_lds_grid(int n_cu, size_t lds) {
     return g;
 }
 
-// (per CU count: a process may render on devices or partitions of different sizes; per host thread, as the
-// other grid caches)
+// per CU count (a process may render on devices or partitions of different sizes), process-wide: the 8
+// Tasks of a render (main.zig:314-326) share one set instead of each thread querying the occupancy API again
 template <uint32_t FEAT>
-const WfGrids<FEAT>& wf_grids(int n_cu) {
-    thread_local int key = 0;
-    thread_local WfGrids<FEAT> g{};
-    if (key != n_cu) {
-        g = WfGrids<FEAT>(n_cu);
-        key = n_cu;
-    }
-    return g;
+WfGrids<FEAT> wf_grids(int n_cu) {
+    static std::mutex mu;
+    static std::map<int, WfGrids<FEAT>> cache;
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = cache.find(n_cu);
+    if (it == cache.end()) it = cache.emplace(n_cu, WfGrids<FEAT>(n_cu)).first;
+    return it->second;
 }
 
 // (Grid sizes are cached per host thread: rtw_render may be called from several threads at once.)
@@ -1924,6 +1812,9 @@ const WfGrids<FEAT>& wf_grids(int n_cu) {
 //   else    : the tree through L1/L2 (wf_step<FEAT, false>)
 // dynamic LDS of the fused kernels: tree stage + what is staged after it
 
+// scene classes whose fused step never runs on the compact LDS stage (wf_run: textured scenes keep the 32-B
+// stage), so wf_run_fused instantiates no compact-LDS kernel for them
+#define RTW_WF_NO_CLDS (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING | RTW_F_IMAGE | RTW_F_NOISE)
 template <uint32_t FEAT>
 void wf_run_fused(const rtw_launch& L, const rtw_wf& W0, hipStream_t st, int n_cu, size_t clds, size_t lds,
                   rtw_timer* T) {
@@ -1936,24 +1827,18 @@ void wf_run_fused(const rtw_launch& L, const rtw_wf& W0, hipStream_t st, int n_c
     thread_local uint64_t cgrid[2] = {0, 0}, tgrid[2] = {0, 0}, lgrid[2] = {0, 0}, ggrid[2] = {0, 0}, wtail[2] = {0, 0};
     uint32_t grid = 0;
     // The compact stage's block shape: the 8-copy stage (C2: 124 KB) leaves room for one 1024-thread block
-    // per CU; the 4-copy stage (L.n_orders == 4, 62 KB) for two blocks (rtw_tuning.clds_shape 2..4: of 512,
-    // 640 or 768 threads) when it fits half the LDS
+    // per CU; the 4-copy stage (L.n_orders == 4, 62 KB) for two 768-thread blocks (rtw_tuning.clds_shape 4)
+    // when it fits half the LDS
     const bool y4 = L.n_orders == 4;
     const int cn = L.cnode32 ? CN_F32_4 : y4 ? CN_F16_4 : CN_F16_8;
-    const uint32_t shape = clds && cn == CN_F16_4 && cdyn0 <= RTW_WF_CLDS2_MAX && L.clds_shape >= 2 ? L.clds_shape : 1u;
-    const bool two = shape >= 2;
+    const uint32_t shape = clds && cn == CN_F16_4 && cdyn0 <= RTW_WF_CLDS2_MAX && L.clds_shape == 4u ? 4u : 1u;
+    const bool two = shape == 4u;
     const size_t cdyn2 = two && cdyn > RTW_WF_CLDS2_MAX ? cdyn0 : cdyn;  // materials only if they fit too
-    const uint32_t cthreads = shape == 2 ? 512u : shape == 3 ? 640u : shape == 4 ? 768u : 1024u;
-    if constexpr ((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING)) == 0) {
+    const uint32_t cthreads = two ? 768u : 1024u;
+    if constexpr ((FEAT & RTW_WF_NO_CLDS) == 0) {
         const uint64_t key = wf_key(n_cu, (uint32_t)cdyn2 | (shape << 24) | ((uint32_t)cn << 28));
         if (clds && cgrid[1] != key) {
-            if (shape == 2) {
-                cgrid[0] = wf_grid(wf_step_clds2<FEAT, 512>, n_cu, cdyn2, 512);
-                tgrid[0] = wf_grid(wf_tail_clds2<FEAT, 512>, n_cu, clds, 512);
-            } else if (shape == 3) {
-                cgrid[0] = wf_grid(wf_step_clds2<FEAT, 640>, n_cu, cdyn2, 640);
-                tgrid[0] = wf_grid(wf_tail_clds2<FEAT, 640>, n_cu, clds, 640);
-            } else if (shape == 4) {
+            if (two) {
                 cgrid[0] = wf_grid(wf_step_clds2<FEAT, 768>, n_cu, cdyn2, 768);
                 tgrid[0] = wf_grid(wf_tail_clds2<FEAT, 768>, n_cu, clds, 768);
             } else if (cn == CN_F32_4) {
@@ -1999,15 +1884,11 @@ void wf_run_fused(const rtw_launch& L, const rtw_wf& W0, hipStream_t st, int n_c
         // deal bit 16: iteration it >= 1 claims its stripes' chunks from counters of its own
         Wt.deal_it = (W.deal && (W.deal_mode & 16u) && it) ? W.deal + RTW_WF_DEAL_COUNTERS0 + it * RTW_WF_STRIPES
                                                            : nullptr;
-        if constexpr ((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING)) == 0) {
+        if constexpr ((FEAT & RTW_WF_NO_CLDS) == 0) {
             if (clds) {
                 rtw_launch Lc = L;  // the materials are staged only when they fit
                 if (cdyn2 == cdyn0) Lc.mat_lds = 0;
-                if (shape == 2)
-                    hipLaunchKernelGGL((wf_step_clds2<FEAT, 512>), dim3(grid), dim3(512), cdyn2, st, Lc, Wt, it);
-                else if (shape == 3)
-                    hipLaunchKernelGGL((wf_step_clds2<FEAT, 640>), dim3(grid), dim3(640), cdyn2, st, Lc, Wt, it);
-                else if (shape == 4)
+                if (two)
                     hipLaunchKernelGGL((wf_step_clds2<FEAT, 768>), dim3(grid), dim3(768), cdyn2, st, Lc, Wt, it);
                 else if (cn == CN_F32_4)
                     hipLaunchKernelGGL((wf_step_clds<FEAT, CN_F32_4>), dim3(grid), dim3(1024), cdyn2, st, Lc, Wt, it);
@@ -2029,14 +1910,10 @@ void wf_run_fused(const rtw_launch& L, const rtw_wf& W0, hipStream_t st, int n_c
         RTW_TIME_BEGIN(T, RTW_K_TAIL)
         // one tail launch over iteration itx's queue (W's counters: the launch's own)
         auto tail = [&](const rtw_wf& Wd, uint32_t itx) {
-            if constexpr ((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING)) == 0) {
+            if constexpr ((FEAT & RTW_WF_NO_CLDS) == 0) {
                 if (clds && (L.wf_fuse & 2u)) {
                     const rtw_wf& W = Wd;
-                    if (shape == 2)
-                        hipLaunchKernelGGL((wf_tail_clds2<FEAT, 512>), dim3((uint32_t)tgrid[0]), dim3(512), clds, st, L, W, itx);
-                    else if (shape == 3)
-                        hipLaunchKernelGGL((wf_tail_clds2<FEAT, 640>), dim3((uint32_t)tgrid[0]), dim3(640), clds, st, L, W, itx);
-                    else if (shape == 4)
+                    if (two)
                         hipLaunchKernelGGL((wf_tail_clds2<FEAT, 768>), dim3((uint32_t)tgrid[0]), dim3(768), clds, st, L, W, itx);
                     else if (cn == CN_F32_4)
                         hipLaunchKernelGGL((wf_tail_clds<FEAT, CN_F32_4>), dim3((uint32_t)tgrid[0]), dim3(1024), clds, st, L, W, itx);
@@ -2070,7 +1947,7 @@ void wf_run_fused(const rtw_launch& L, const rtw_wf& W0, hipStream_t st, int n_c
 
 template <uint32_t FEAT>
 void wf_run(const rtw_launch& L, const rtw_wf& W0, hipStream_t st, int n_cu, rtw_timer* T) {
-    const WfGrids<FEAT>& g = wf_grids<FEAT>(n_cu);
+    const WfGrids<FEAT> g = wf_grids<FEAT>(n_cu);
     if (L.wf_fuse & 1u) {
         size_t fclds = 0, flds = 0;
         // (textured scenes keep the 32-B node stage: it leaves LDS for the Perlin tables and the
@@ -2253,20 +2130,16 @@ void rtw_wf_run_spheres(const rtw_launch& L, const rtw_wf& W, hipStream_t st, in
 // (waves: the 256-thread shade grids and the compact-LDS kernels' grids, whichever launches more; computed per
 // CU count -- it sizes the stripes, which the kernels do not bound-check)
 uint32_t rtw_wf_spheres_max_waves(int n_cu) {
-    thread_local int key = 0;
-    thread_local uint32_t val = 0;
-    if (key == n_cu) return val;
+    static std::mutex mu;
+    static std::map<int, uint32_t> cache;
+    std::lock_guard<std::mutex> lk(mu);
+    if (auto it = cache.find(n_cu); it != cache.end()) return it->second;
     const uint32_t b = std::max({wf_grids<0u>(n_cu).shade, wf_grids<0u>(n_cu).shade0, wf_grids<RTW_F_CHECKER>(n_cu).shade,
                                  wf_grids<RTW_F_CHECKER>(n_cu).shade0});
-    const uint32_t c2 = std::max({wf_grid(wf_step_clds2<0u, 512>, n_cu, 0, 512) * 8u,
-                                         wf_grid(wf_step_clds2<0u, 640>, n_cu, 0, 640) * 10u,
-                                         wf_grid(wf_step_clds2<0u, 768>, n_cu, 0, 768) * 12u,
-                                         wf_grid(wf_step_clds2<RTW_F_CHECKER, 512>, n_cu, 0, 512) * 8u,
-                                         wf_grid(wf_step_clds2<RTW_F_CHECKER, 640>, n_cu, 0, 640) * 10u,
-                                         wf_grid(wf_step_clds2<RTW_F_CHECKER, 768>, n_cu, 0, 768) * 12u});
+    const uint32_t c2 = std::max(wf_grid(wf_step_clds2<0u, 768>, n_cu, 0, 768), wf_grid(wf_step_clds2<RTW_F_CHECKER, 768>, n_cu, 0, 768)) * 12u;
     const uint32_t c1 = std::max(wf_grid(wf_step_clds<0u>, n_cu, 0, 1024), wf_grid(wf_step_clds<RTW_F_CHECKER>, n_cu, 0, 1024)) * 16u;
-    val = std::max({4u * b, c2, c1});
-    key = n_cu;
+    const uint32_t val = std::max({4u * b, c2, c1});
+    cache[n_cu] = val;
     return val;
 }
 
