@@ -330,8 +330,8 @@ typedef struct rtw_tuning {
     uint32_t wide_walk;        /* 1 = two-wide stack walk for static sphere SAH trees read through L1/L2 (default) */
     uint64_t wf_paths;         /* wavefront batch capacity in paths; 0 = auto (2^29 within 35 % of free memory) */
     uint32_t tile_lists;       /* camera rays of static sphere scenes (fused step) test per-8x8-tile candidate lists:
-                                  0 = off, 1 = default (lists of <= 32 spheres, 64 for trees of > 4096 nodes),
-                                  2..64 = that cap (ABI 4) */
+                                  0 = off, 1 = default (lists of <= 32 spheres, 128 for trees of > 4096 nodes),
+                                  2..128 = that cap (ABI 4; 128 since ABI 8) */
     uint32_t hoist;            /* SAH sphere scenes: spheres whose box dwarfs the rest of the scene (a ground
                                   sphere) are tested first by every walk, ahead of the tree (default 1; ABI 5) */
     uint32_t sort_iters;       /* fused step (trees staged in LDS): wavefront iterations 0 .. sort_iters-1 file

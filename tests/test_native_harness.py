@@ -103,17 +103,19 @@ def test_harness_c1_eight_tasks_vs_oracle(rtw, oracle, tmp_path):
 @pytest.mark.gpu
 def test_harness_tasks_advance_together(rtw, tmp_path):
     """The 8 Tasks on one GPU context advance samples-outer together (camera.zig:98-111): with batches
-    long enough that the device, not host-thread wake-ups, paces them (1200x675, 24-sample batches, ~0.5 ms
-    each), the Tasks' samples done never differ by more than one batch while all of them run, and the frame
-    equals one call over the whole chunk range."""
+    long enough that the device, not host-thread wake-ups, paces them (1200x675, 96-sample batches, ~1.2 ms
+    each, so a round of the 8 Tasks' batches is ~10 ms: a thread woken late by a loaded host still enqueues its
+    next batch within the round; round 6 made the kernels fast enough that 24-sample batches (~0.3 ms) let host
+    jitter show), the Tasks' samples done never differ by more than one batch while all of them run, and the
+    frame equals one call over the whole chunk range."""
     arr = write_scene(rtw, tmp_path / "scene")
-    info, buf = run_harness(tmp_path / "scene", 0, 1200, 192, 24, "full", tmp_path / "big.f32")
+    info, buf = run_harness(tmp_path / "scene", 0, 1200, 768, 96, "full", tmp_path / "big.f32")
     assert info["rc"] == [0] * 8, info
     assert 0 < info["ui_polls"] and info["max_spread_batches"] <= 1.0 + 1e-9, info
     chunk = info["chunk"]
     init = np.zeros_like(buf)
     init[:, 3] = 1
-    ref = direct(rtw, arr, 0, 1200, 0, 192, 0, 8 * chunk, init)
+    ref = direct(rtw, arr, 0, 1200, 0, 768, 0, 8 * chunk, init)
     assert np.array_equal(buf, ref)
 
 

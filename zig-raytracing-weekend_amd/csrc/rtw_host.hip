@@ -393,9 +393,10 @@ int rtw_scene_create_ex(const rtw_scene_desc* d, int device, const rtw_tuning* t
     L.w2nodes = w2.empty() ? nullptr : reinterpret_cast<const uint4*>(dev + o_w2);
     L.w2leaf = w2.empty() ? nullptr : reinterpret_cast<const uint32_t*>(dev + o_w2l);
     L.w2_stack = w2.empty() ? 0u : w2_stack;
-    // default cap: 32 candidates for small trees (flat prepass: C2 16/32/64 -> 5765/5789/5769), 64 for large
-    // ones (frustum-walked prepass: C4 32/64 -> 2440/2458)
-    L.tile_lists = tu.tile_lists == 1 ? (n_nodes <= 4096 ? 32u : 64u) : std::min<uint32_t>(tu.tile_lists, RTW_TL_MAX);
+    // default cap: 32 candidates for small trees (flat prepass: C2 16/32/64 -> 5765/5789/5769), 128 for large
+    // ones (frustum-walked prepass: C4 32/64 -> 2440/2458; round 6, 64/96/128 -> 3147/3156/3166,
+    // profiles/r6_late_rest/)
+    L.tile_lists = tu.tile_lists == 1 ? (n_nodes <= 4096 ? 32u : 128u) : std::min<uint32_t>(tu.tile_lists, RTW_TL_MAX);
     L.cvec = reinterpret_cast<const float4*>(dev + o_cvec);
     L.sph = reinterpret_cast<const rtw_dev_sphere*>(dev + o_sph);
     L.quads = reinterpret_cast<const rtw_dev_quad*>(dev + o_quad);

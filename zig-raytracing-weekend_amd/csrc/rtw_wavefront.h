@@ -11,7 +11,7 @@
 // coherent queues (wf_push_bucketed): a wave keeps one open 64-slot block per direction bucket
 #define RTW_WF_BUCKET_BITS 4
 #define RTW_WF_BUCKETS (1u << RTW_WF_BUCKET_BITS)
-#define RTW_TL_MAX 64          // camera-ray candidate list capacity per 8x8 tile (rtw_tuning.tile_lists caps it)
+#define RTW_TL_MAX 128         // camera-ray candidate list capacity per 8x8 tile (rtw_tuning.tile_lists caps it)
 #define RTW_TL_WALK 0xFFFFFFFFu
 #define RTW_TL_BYTES (RTW_TL_MAX * 32 + 4)  // per tile
 #define RTW_WF_CLDS2_MAX (80u * 1024u)  // their stage (+ materials) per block: half the CU's LDS

@@ -1139,7 +1139,9 @@ __device__ __forceinline__ void wf_shade_body(const rtw_launch& L, const rtw_wf&
 // tail: the paths still queued after the last wavefront iteration, each to
 // completion; a lane whose path ends takes the wave's next path at once.
 // CLDS: the walk reads the compact nodes staged in LDS (`lds`) instead of L1/L2.
-template <uint32_t FEAT, bool CLDS, int CN = CN_F16_8>
+// CNT (every kernel with a counted form): 0 = no device counters (the product launches: their registers and
+// atomics compile away), 1 = the counted pass (rtw_render_opts.counters), 2 = decided per launch by L.counters
+template <uint32_t FEAT, bool CLDS, int CN = CN_F16_8, int CNT = 2>
 __device__ __forceinline__ void wf_tail_body(const rtw_launch& L, const rtw_wf& W, uint32_t it, const uint4* lds,
                                              const float4* nodes = nullptr) {
     const uint32_t lane = __lane_id();
@@ -1221,25 +1223,37 @@ __device__ __forceinline__ void wf_tail_body(const rtw_launch& L, const rtw_wf& 
         int ohit = -1;  // object scenes: the hit shaded after the wave's rejection loop
         float ot = 0.0f;
         if (active) {  // one more iteration of rayColor
-            cnt.rays++;
-            cnt.tail_rays++;
+            if constexpr (CNT != 0) {
+                cnt.rays++;
+                cnt.tail_rays++;
+            }
             float t;
             int hit;
-            if constexpr (CLDS)
+            if constexpr (CLDS && CNT == 2)
                 hit = L.counters ? walk_compact<true, true, CN>(L, lds, r, t, cnt)
                                  : walk_compact<false, true, CN>(L, lds, r, t, cnt);
+            else if constexpr (CLDS)
+                hit = walk_compact<CNT == 1, true, CN>(L, lds, r, t, cnt);
             else
                 hit = nodes ? traverse<FEAT, false>(nodes, L, r, t, cnt, rng.s)  // the LDS stage
                             : wf_traverse_global<FEAT>(L, r, t, cnt, rng.s);
             if (hit < 0) {
                 acc = acc + thr * background(L, r);
             } else if constexpr ((FEAT & ~RTW_F_CHECKER) == 0) {
-                // untextured static sphere scenes: the fused step's split form (hit record, one
-                // randomUnitVector rejection loop for the wave, then the material; C2 tail -10 %,
-                // C4 -5 %; the textured C5 tail +5 %: nested form there)
-                hp = hit_prep<FEAT>(L.nodes, L, r, hit, t);
+                // untextured static sphere scenes: the fused step's split form (C2 tail -10 %, C4 -5 % over the
+                // nested form; the textured C5 tail +5 %: nested form there).  On the compact LDS stage (C2) in the
+                // fused step's order -- the material kind, the wave's rejection loop, then the hit record (-0.9 %
+                // tail time, no scratch left); through L1/L2 (C4, seq_reject) the hit record first (its loads
+                // overlap the loop there: +1.2 % the other way, profiles/r6_late_rest/)
                 hitp = true;
-                need_uv = needs_unit_vector<FEAT>(hp.m.kind);
+                if constexpr (CLDS) {
+                    ohit = hit;
+                    ot = t;
+                    need_uv = needs_unit_vector<FEAT>(hit_material_kind<FEAT>(L.nodes, L, hit));
+                } else {
+                    hp = hit_prep<FEAT>(L.nodes, L, r, hit, t);
+                    need_uv = needs_unit_vector<FEAT>(hp.m.kind);
+                }
             } else if constexpr ((FEAT & RTW_F_GEOM) != 0) {
                 // object scenes: as the fused step's object path, the wave's shared rejection loop
                 // (wf_reject3) before the hit record, on the material kind alone
@@ -1278,6 +1292,9 @@ __device__ __forceinline__ void wf_tail_body(const rtw_launch& L, const rtw_wf& 
             // the wave-cooperative loop (same candidates, same RNG states as seq_reject<3>): C2 +1.4 %
             if constexpr (CLDS) wf_reject3(need_uv, rng, uv3);
             else if (need_uv) seq_reject<3>(rng, uv3);
+            if constexpr (CLDS) {
+                if (hitp) hp = hit_prep<FEAT>(L.nodes, L, r, ohit, ot);
+            }
             if (hitp) {
                 const f3 ruv = need_uv ? unit_vector(mk(uv3[0], uv3[1], uv3[2])) : mk(0, 0, 0);
                 f3 att;
@@ -1295,7 +1312,7 @@ __device__ __forceinline__ void wf_tail_body(const rtw_launch& L, const rtw_wf& 
             active = false;
         }
     }
-    flush_counters(L, cnt, 0);
+    if constexpr (CNT != 0) flush_counters(L, cnt, 0);
 }
 
 template <uint32_t FEAT>
@@ -1304,9 +1321,9 @@ __global__ __launch_bounds__(256) void wf_tail(rtw_launch L, rtw_wf W, uint32_t 
 }
 // untextured static sphere scenes: capped at 96 VGPRs for 5 waves/SIMD (no spills there; the
 // split shading form took it to 98 = 4 waves: C4 tail +3 %); other scene classes would spill
-template <uint32_t FEAT>
+template <uint32_t FEAT, int CNT = 2>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void wf_tail_w5(rtw_launch L, rtw_wf W, uint32_t it) {
-    wf_tail_body<FEAT, false>(L, W, it, nullptr);
+    wf_tail_body<FEAT, false, CN_F16_8, CNT>(L, W, it, nullptr);
 }
 
 // L.shade_lds: the same for the materials | textures | image records (small scenes)
@@ -1323,7 +1340,7 @@ __device__ __forceinline__ rtw_launch stage_shade(const rtw_launch& L, float4* l
 }
 
 // the 32-B node array(s) staged in LDS (small object scenes: Cornell), + L.geom_lds bytes of geometry
-template <uint32_t FEAT>
+template <uint32_t FEAT, int CNT = 2>
 __global__ __launch_bounds__(256) void wf_tail_lds(rtw_launch L, rtw_wf W, uint32_t it) {
     extern __shared__ float4 wf_tail_nodes[];
     const uint32_t n4 = 2u * L.n_nodes * L.n_orders;
@@ -1333,25 +1350,25 @@ __global__ __launch_bounds__(256) void wf_tail_lds(rtw_launch L, rtw_wf W, uint3
     if (sl && gl) {
         const rtw_launch G = stage_geom(stage_shade(L, wf_tail_nodes + n4), wf_tail_nodes + n4 + L.shade_lds / 16u);
         __syncthreads();
-        wf_tail_body<FEAT, false>(G, W, it, nullptr, wf_tail_nodes);
+        wf_tail_body<FEAT, false, CN_F16_8, CNT>(G, W, it, nullptr, wf_tail_nodes);
         return;
     }
     if (sl) {
         const rtw_launch G = stage_shade(L, wf_tail_nodes + n4);
         __syncthreads();
-        wf_tail_body<FEAT, false>(G, W, it, nullptr, wf_tail_nodes);
+        wf_tail_body<FEAT, false, CN_F16_8, CNT>(G, W, it, nullptr, wf_tail_nodes);
         return;
     }
     if constexpr ((FEAT & RTW_F_GEOM) != 0) {
         if (gl) {
             const rtw_launch G = stage_geom(L, wf_tail_nodes + n4);
             __syncthreads();
-            wf_tail_body<FEAT, false>(G, W, it, nullptr, wf_tail_nodes);
+            wf_tail_body<FEAT, false, CN_F16_8, CNT>(G, W, it, nullptr, wf_tail_nodes);
             return;
         }
     }
     __syncthreads();
-    wf_tail_body<FEAT, false>(L, W, it, nullptr, wf_tail_nodes);
+    wf_tail_body<FEAT, false, CN_F16_8, CNT>(L, W, it, nullptr, wf_tail_nodes);
 }
 
 
@@ -1363,13 +1380,13 @@ __global__ __launch_bounds__(1024) void wf_tail_clds(rtw_launch L, rtw_wf W, uin
     wf_tail_body<FEAT, true, CN>(L, W, it, wf_clds);
 }
 // the 4-copy stage (half the LDS) at two blocks of T threads per CU: 2T / 256 waves per SIMD
-template <uint32_t FEAT, uint32_t T>
+template <uint32_t FEAT, uint32_t T, int CNT = 2>
 __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(2 * T / 256)))
 void wf_tail_clds2(rtw_launch L, rtw_wf W, uint32_t it) {
     static_assert((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING)) == 0, "static sphere scenes");
     extern __shared__ uint4 wf_clds[];
     stage_clds(L, wf_clds);
-    wf_tail_body<FEAT, true, CN_F16_4>(L, W, it, wf_clds);
+    wf_tail_body<FEAT, true, CN_F16_4, CNT>(L, W, it, wf_clds);
 }
 
 // Where the fused step's walk reads the tree:
@@ -1382,11 +1399,12 @@ enum { WALK_CLDS = 0, WALK_LDS = 1, WALK_GLOBAL = 2, WALK_CLDS4 = 3, WALK_CLDS32
 template <int WALK>
 constexpr int walk_cn() { return WALK == WALK_CLDS32 ? CN_F32_4 : WALK == WALK_CLDS4 ? CN_F16_4 : CN_F16_8; }
 
-template <uint32_t FEAT, int WALK>
+template <uint32_t FEAT, int WALK, int CNT = 2>
 __device__ __forceinline__ int wf_walk(const rtw_launch& L, const void* lds, const Ray& r, float& t, Counters& cnt,
                                        uint64_t mkey) {
     if constexpr (WALK == WALK_CLDS || WALK == WALK_CLDS4 || WALK == WALK_CLDS32) {
         const uint4* cn = static_cast<const uint4*>(lds);
+        if constexpr (CNT != 2) return walk_compact<CNT == 1, true, walk_cn<WALK>()>(L, cn, r, t, cnt);
         return L.counters ? walk_compact<true, true, walk_cn<WALK>()>(L, cn, r, t, cnt)
                           : walk_compact<false, true, walk_cn<WALK>()>(L, cn, r, t, cnt);
     } else if constexpr (WALK == WALK_LDS) {
@@ -1406,7 +1424,7 @@ __device__ __forceinline__ int wf_walk(const rtw_launch& L, const void* lds, con
 // The stripe counters: this kernel appends to len[(it+1)%3] (zeroed by the
 // previous iteration, or by the host for it = 0) and zeroes len[(it+2)%3],
 // iteration it-1's input, for the next iteration.
-template <uint32_t FEAT, int WALK>
+template <uint32_t FEAT, int WALK, int CNT = 2>
 __device__ __forceinline__ void wf_step_body(const rtw_launch& L, const rtw_wf& W, uint32_t it, const void* lds) {
     const rtw_wf_set& S = W.set[it & 1u];
     const rtw_wf_set& O = W.set[(it + 1u) & 1u];
@@ -1432,19 +1450,43 @@ __device__ __forceinline__ void wf_step_body(const rtw_launch& L, const rtw_wf& 
             float2 txy;
             r = wf_load_ray_it<FEAT>(L, S, slot, it, depth, txy, true);
             live = depth != 0;
-            if (live) {  // issued before the walk: the loads land while it runs
-                uint64_t rs;
-                wf_load_rest<FEAT>(L, S, slot, depth, txy, thr, acc, rs, pid, true);
-                rng.s = rs;
+            if constexpr ((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM)) != 0) {
+                if (live) {  // object scenes: the RNG state keys the media during the walk
+                    uint64_t rs;
+                    wf_load_rest<FEAT>(L, S, slot, depth, txy, thr, acc, rs, pid, true);
+                    rng.s = rs;
+                }
             }
         }
+        // Sphere scenes load the rest of the path state (throughput, path id, RNG state) after the walk, not
+        // before it: its six registers are not live across the walk, which took the fused step's spills from 156
+        // to 140 B/lane at its 80-VGPR cap and C2 +3.5 % (two same-box rounds, profiles/r6_late_rest/); the
+        // loads' latency is now exposed, but five other waves per SIMD cover it
+        auto late_rest = [&]() {
+            if constexpr ((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM)) == 0) {
+                if (it != 0 && live) {
+                    float2 txy;
+                    uint32_t d2;
+                    (void)wf_load_ray_it<FEAT>(L, S, slot, it, d2, txy, true);
+                    uint64_t rs;
+                    wf_load_rest<FEAT>(L, S, slot, depth, txy, thr, acc, rs, pid, true);
+                    rng.s = rs;
+                }
+            }
+        };
         Ray sc;
         if constexpr ((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM)) == 0) {
-            // sphere scenes: hit record, then the randomUnitVector draw of every lane
-            // that needs one (one rejection loop for the wave), then the material --
-            // measured faster than the nested form below (C2 +6 %, C5 +3 %)
+            // sphere scenes: the split form (C2 +6 %, C5 +3 % over the nested form of wf_shade)
+            // The material kind, then the randomUnitVector draw of every lane that needs one (one rejection loop
+            // for the wave), then the hit record and the material.  Building the hit record before the loop (the
+            // form of rounds 2-5, C2 +6 % then over the nested form) kept its ~20 registers live across the loop:
+            // at the 6-wave, 80-VGPR cap that spilled, and this order took the fused step's scratch from 124 to
+            // 64 B/lane -- C2 +2.9 %, C5 +2.3 % (same box, profiles/r6_late_rest/).  The same draws in the same
+            // order: bit-identical.
             HitPrep hp;
             bool hitp = false, need_uv = false;
+            int hhit = -1;
+            float ht = 0.0f;
             if (live) {
                 float t;
                 int hit = -1;
@@ -1453,11 +1495,12 @@ __device__ __forceinline__ void wf_step_body(const rtw_launch& L, const rtw_wf& 
                     // camera rays: the tile's candidate list
                     if (it == 0 && W.tl_count) {
                         const uint32_t tile = (slot >> 6) / W.n_s;
-                        listed = L.counters ? wf_tile_hit<true>(L, W, tile, r, hit, t, cnt)
-                                            : wf_tile_hit<false>(L, W, tile, r, hit, t, cnt);
+                        if constexpr (CNT != 2) listed = wf_tile_hit<CNT == 1>(L, W, tile, r, hit, t, cnt);
+                        else listed = L.counters ? wf_tile_hit<true>(L, W, tile, r, hit, t, cnt)
+                                                 : wf_tile_hit<false>(L, W, tile, r, hit, t, cnt);
                     }
                 }
-                if (!listed) hit = wf_walk<FEAT, WALK>(L, lds, r, t, cnt, rng.s);
+                if (!listed) hit = wf_walk<FEAT, WALK, CNT>(L, lds, r, t, cnt, rng.s);
 #if defined(RTW_ABLATE_WALK2)
                 if (!listed) {  // timing ablation only: the walk twice (the second result is the same)
                     float t2;
@@ -1471,13 +1514,15 @@ __device__ __forceinline__ void wf_step_body(const rtw_launch& L, const rtw_wf& 
                     rtw_diag_rec[2u * slot + 1u] = make_uint4(fbits(r.o.x), fbits(r.o.y), fbits(r.o.z), pid + 1u);
                 }
 #endif
-                cnt.rays++;
+                if constexpr (CNT != 0) cnt.rays++;
+                late_rest();
                 if (hit < 0) {
                     acc = acc + thr * background(L, r);
                 } else {
-                    hp = hit_prep<FEAT>(L.nodes, L, r, hit, t);
+                    hhit = hit;
+                    ht = t;
                     hitp = true;
-                    need_uv = needs_unit_vector<FEAT>(hp.m.kind);
+                    need_uv = needs_unit_vector<FEAT>(hit_material_kind<FEAT>(L.nodes, L, hit));
                 }
             }
             float uv3[3] = {0.0f, 0.0f, 0.0f};
@@ -1485,6 +1530,7 @@ __device__ __forceinline__ void wf_step_body(const rtw_launch& L, const rtw_wf& 
             // image / noise textures, whose step is at its 128-VGPR cap (C5 -2.3 %)
             if constexpr ((FEAT & (RTW_F_IMAGE | RTW_F_NOISE)) == 0) wf_reject3(need_uv, rng, uv3);
             else if (need_uv) seq_reject<3>(rng, uv3);
+            if (hitp) hp = hit_prep<FEAT>(L.nodes, L, r, hhit, ht);
             if (hitp) {
                 const f3 ruv = need_uv ? unit_vector(mk(uv3[0], uv3[1], uv3[2])) : mk(0, 0, 0);
                 f3 att;
@@ -1500,14 +1546,14 @@ __device__ __forceinline__ void wf_step_body(const rtw_launch& L, const rtw_wf& 
             float t = 0.0f;
             int hit = -1;
             if (live) {
-                hit = wf_walk<FEAT, WALK>(L, lds, r, t, cnt, rng.s);
+                hit = wf_walk<FEAT, WALK, CNT>(L, lds, r, t, cnt, rng.s);
 #if defined(RTW_ABLATE_WALK2)
                 {   // timing ablation only: the walk twice (the second result is the same)
                     float t2;
-                    if (wf_walk<FEAT, WALK>(L, lds, r, t2, cnt, rng.s) != hit) t = t2;
+                    if (wf_walk<FEAT, WALK, CNT>(L, lds, r, t2, cnt, rng.s) != hit) t = t2;
                 }
 #endif
-                cnt.rays++;
+                if constexpr (CNT != 0) cnt.rays++;
             }
             const bool need_uv = hit >= 0 && needs_unit_vector<FEAT>(hit_material_kind<FEAT>(L.nodes, L, hit));
             float uv3[3] = {0.0f, 0.0f, 0.0f};
@@ -1532,7 +1578,7 @@ __device__ __forceinline__ void wf_step_body(const rtw_launch& L, const rtw_wf& 
         if (push) wf_store_path<FEAT>(O, out, sc, depth - 1, thr, rng.s, pid, acc, true);
     }
     if (bucketed) wf_close_blocks<FEAT>(W, it, bb, bf, true);
-    flush_counters(L, cnt, 0);
+    if constexpr (CNT != 0) flush_counters(L, cnt, 0);
 }
 
 __device__ __forceinline__ void wf_step_zero_next(const rtw_wf& W, uint32_t it) {
@@ -1540,7 +1586,7 @@ __device__ __forceinline__ void wf_step_zero_next(const rtw_wf& W, uint32_t it) 
 }
 
 // compact nodes of every copy in LDS, then the materials when they fit
-template <uint32_t FEAT, int WALK>
+template <uint32_t FEAT, int WALK, int CNT = 2>
 __device__ __forceinline__ void wf_step_clds_body(const rtw_launch& L, const rtw_wf& W, uint32_t it) {
     wf_step_zero_next(W, it);
     extern __shared__ uint4 wf_clds[];
@@ -1552,10 +1598,10 @@ __device__ __forceinline__ void wf_step_clds_body(const rtw_launch& L, const rtw
         __syncthreads();
         rtw_launch Lm = L;
         Lm.mats = reinterpret_cast<const rtw_dev_material*>(ml);
-        wf_step_body<FEAT, WALK>(Lm, W, it, wf_clds);
+        wf_step_body<FEAT, WALK, CNT>(Lm, W, it, wf_clds);
         return;
     }
-    wf_step_body<FEAT, WALK>(L, W, it, wf_clds);
+    wf_step_body<FEAT, WALK, CNT>(L, W, it, wf_clds);
 }
 
 // one 1024-thread block per CU (the 8-copy stage, 124 KB for C2, allows no second block)
@@ -1570,16 +1616,16 @@ __global__ __launch_bounds__(1024) void wf_step_clds(rtw_launch L, rtw_wf W, uin
 // its dependent ds_read_b128 41 % of the cycles at 4 waves (profiles/r4_stall/): the fifth and sixth waves have
 // ready work to issue in those waits.  (Two blocks of 512 or 640 threads lost their A/Bs -- profiles/r5_occupancy/,
 // diag/walk_variants.patch -- and were removed in round 6.)
-template <uint32_t FEAT, uint32_t T>
+template <uint32_t FEAT, uint32_t T, int CNT = 2>
 __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(2 * T / 256)))
 void wf_step_clds2(rtw_launch L, rtw_wf W, uint32_t it) {
     static_assert((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING)) == 0, "static sphere scenes");
-    wf_step_clds_body<FEAT, WALK_CLDS4>(L, W, it);
+    wf_step_clds_body<FEAT, WALK_CLDS4, CNT>(L, W, it);
 }
 
 // wf_step's LDS extras by mask (bit 0 Perlin tables, 1 materials/textures, 2 geometry); masks a
 // scene class cannot use compile to nothing
-template <uint32_t FEAT, uint32_t MASK>
+template <uint32_t FEAT, uint32_t MASK, int CNT>
 __device__ __forceinline__ void wf_step_staged(const rtw_launch& L, const rtw_wf& W, uint32_t it, float4* nodes,
                                                float4* extra) {
     constexpr bool P = (MASK & 1u) && (FEAT & RTW_F_NOISE), S = (MASK & 2u) != 0, G = (MASK & 4u) && (FEAT & RTW_F_GEOM);
@@ -1597,12 +1643,12 @@ __device__ __forceinline__ void wf_step_staged(const rtw_launch& L, const rtw_wf
         }
         if constexpr (G) Lp = stage_geom(Lp, extra);
         __syncthreads();
-        wf_step_body<FEAT, WALK_LDS>(Lp, W, it, nodes);
+        wf_step_body<FEAT, WALK_LDS, CNT>(Lp, W, it, nodes);
     }
 }
 
 // the 32-B node array (one ordering) in LDS, or the tree through L1/L2
-template <uint32_t FEAT, bool LDS>
+template <uint32_t FEAT, bool LDS, int CNT = 2>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void wf_step(rtw_launch L, rtw_wf W, uint32_t it) {
     wf_step_zero_next(W, it);
     extern __shared__ float4 wf_lds_nodes[];
@@ -1615,19 +1661,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void w
                               (((FEAT & RTW_F_GEOM) && L.geom_lds) ? 4u : 0u);
         float4* extra = wf_lds_nodes + n4;
         switch (mask) {
-            case 1: return wf_step_staged<FEAT, 1>(L, W, it, wf_lds_nodes, extra);
-            case 2: return wf_step_staged<FEAT, 2>(L, W, it, wf_lds_nodes, extra);
-            case 3: return wf_step_staged<FEAT, 3>(L, W, it, wf_lds_nodes, extra);
-            case 4: return wf_step_staged<FEAT, 4>(L, W, it, wf_lds_nodes, extra);
-            case 5: return wf_step_staged<FEAT, 5>(L, W, it, wf_lds_nodes, extra);
-            case 6: return wf_step_staged<FEAT, 6>(L, W, it, wf_lds_nodes, extra);
-            case 7: return wf_step_staged<FEAT, 7>(L, W, it, wf_lds_nodes, extra);
+            case 1: return wf_step_staged<FEAT, 1, CNT>(L, W, it, wf_lds_nodes, extra);
+            case 2: return wf_step_staged<FEAT, 2, CNT>(L, W, it, wf_lds_nodes, extra);
+            case 3: return wf_step_staged<FEAT, 3, CNT>(L, W, it, wf_lds_nodes, extra);
+            case 4: return wf_step_staged<FEAT, 4, CNT>(L, W, it, wf_lds_nodes, extra);
+            case 5: return wf_step_staged<FEAT, 5, CNT>(L, W, it, wf_lds_nodes, extra);
+            case 6: return wf_step_staged<FEAT, 6, CNT>(L, W, it, wf_lds_nodes, extra);
+            case 7: return wf_step_staged<FEAT, 7, CNT>(L, W, it, wf_lds_nodes, extra);
             default: break;
         }
         __syncthreads();
-        wf_step_body<FEAT, WALK_LDS>(L, W, it, wf_lds_nodes);
+        wf_step_body<FEAT, WALK_LDS, CNT>(L, W, it, wf_lds_nodes);
     } else {
-        wf_step_body<FEAT, WALK_GLOBAL>(L, W, it, nullptr);
+        wf_step_body<FEAT, WALK_GLOBAL, CNT>(L, W, it, nullptr);
     }
 }
 
@@ -1712,8 +1758,9 @@ template <uint32_t FEAT>
 void wf_launch_tail(const rtw_launch& L, const rtw_wf& W, hipStream_t st, int n_cu, size_t lds, uint64_t (&cache)[2],
                     uint32_t it) {
     if constexpr ((FEAT & ~RTW_F_CHECKER) == 0)
-        hipLaunchKernelGGL(wf_tail_w5<FEAT>, dim3(wf_grid_cached(wf_tail_w5<FEAT>, n_cu, lds, cache)), dim3(256), lds, st,
-                           L, W, it);
+        { if (L.counters) hipLaunchKernelGGL((wf_tail_w5<FEAT, 1>), dim3(wf_grid_cached(wf_tail_w5<FEAT, 0>, n_cu, lds, cache)), dim3(256),
+                                        lds, st, L, W, it); else hipLaunchKernelGGL((wf_tail_w5<FEAT, 0>), dim3(wf_grid_cached(wf_tail_w5<FEAT, 0>, n_cu, lds, cache)), dim3(256),
+                                        lds, st, L, W, it); }
     else
         hipLaunchKernelGGL(wf_tail<FEAT>, dim3(wf_grid_cached(wf_tail<FEAT>, n_cu, lds, cache)), dim3(256), lds, st, L,
                            W, it);
@@ -1839,8 +1886,8 @@ void wf_run_fused(const rtw_launch& L, const rtw_wf& W0, hipStream_t st, int n_c
         const uint64_t key = wf_key(n_cu, (uint32_t)cdyn2 | (shape << 24) | ((uint32_t)cn << 28));
         if (clds && cgrid[1] != key) {
             if (two) {
-                cgrid[0] = wf_grid(wf_step_clds2<FEAT, 768>, n_cu, cdyn2, 768);
-                tgrid[0] = wf_grid(wf_tail_clds2<FEAT, 768>, n_cu, clds, 768);
+                cgrid[0] = wf_grid(wf_step_clds2<FEAT, 768, 0>, n_cu, cdyn2, 768);
+                tgrid[0] = wf_grid(wf_tail_clds2<FEAT, 768, 0>, n_cu, clds, 768);
             } else if (cn == CN_F32_4) {
                 cgrid[0] = wf_grid(wf_step_clds<FEAT, CN_F32_4>, n_cu, cdyn2, 1024);
                 tgrid[0] = wf_grid(wf_tail_clds<FEAT, CN_F32_4>, n_cu, clds, 1024);
@@ -1858,12 +1905,12 @@ void wf_run_fused(const rtw_launch& L, const rtw_wf& W0, hipStream_t st, int n_c
         grid = (uint32_t)cgrid[0];
     } else if (lds) {
         if (lgrid[1] != wf_key(n_cu, ldyn)) {
-            lgrid[0] = wf_grid(wf_step<FEAT, true>, n_cu, ldyn);
+            lgrid[0] = wf_grid(wf_step<FEAT, true, 0>, n_cu, ldyn);
             lgrid[1] = wf_key(n_cu, ldyn);
         }
         grid = (uint32_t)lgrid[0];
     } else {
-        grid = wf_grid_cached(wf_step<FEAT, false>, n_cu, gdyn, ggrid);
+        grid = wf_grid_cached(wf_step<FEAT, false, 0>, n_cu, gdyn, ggrid);
     }
     // iteration 0 appends to len[1]; every later iteration's output counters are
     // zeroed by the kernel two iterations before (wf_step_zero_next)
@@ -1889,7 +1936,7 @@ void wf_run_fused(const rtw_launch& L, const rtw_wf& W0, hipStream_t st, int n_c
                 rtw_launch Lc = L;  // the materials are staged only when they fit
                 if (cdyn2 == cdyn0) Lc.mat_lds = 0;
                 if (two)
-                    hipLaunchKernelGGL((wf_step_clds2<FEAT, 768>), dim3(grid), dim3(768), cdyn2, st, Lc, Wt, it);
+                    { if (L.counters) hipLaunchKernelGGL((wf_step_clds2<FEAT, 768, 1>), dim3(grid), dim3(768), cdyn2, st, Lc, Wt, it); else hipLaunchKernelGGL((wf_step_clds2<FEAT, 768, 0>), dim3(grid), dim3(768), cdyn2, st, Lc, Wt, it); }
                 else if (cn == CN_F32_4)
                     hipLaunchKernelGGL((wf_step_clds<FEAT, CN_F32_4>), dim3(grid), dim3(1024), cdyn2, st, Lc, Wt, it);
                 else if (cn == CN_F16_4)
@@ -1901,9 +1948,9 @@ void wf_run_fused(const rtw_launch& L, const rtw_wf& W0, hipStream_t st, int n_c
             }
         }
         if (lds)
-            hipLaunchKernelGGL((wf_step<FEAT, true>), dim3(grid), dim3(256), ldyn, st, L, Wt, it);
+            { if (L.counters) hipLaunchKernelGGL((wf_step<FEAT, true, 1>), dim3(grid), dim3(256), ldyn, st, L, Wt, it); else hipLaunchKernelGGL((wf_step<FEAT, true, 0>), dim3(grid), dim3(256), ldyn, st, L, Wt, it); }
         else
-            hipLaunchKernelGGL((wf_step<FEAT, false>), dim3(grid), dim3(256), gdyn, st, L, W, it);
+            { if (L.counters) hipLaunchKernelGGL((wf_step<FEAT, false, 1>), dim3(grid), dim3(256), gdyn, st, L, W, it); else hipLaunchKernelGGL((wf_step<FEAT, false, 0>), dim3(grid), dim3(256), gdyn, st, L, W, it); }
         RTW_TIME_END(T)
     }
     if (iters < L.max_depth) {
@@ -1914,7 +1961,7 @@ void wf_run_fused(const rtw_launch& L, const rtw_wf& W0, hipStream_t st, int n_c
                 if (clds && (L.wf_fuse & 2u)) {
                     const rtw_wf& W = Wd;
                     if (two)
-                        hipLaunchKernelGGL((wf_tail_clds2<FEAT, 768>), dim3((uint32_t)tgrid[0]), dim3(768), clds, st, L, W, itx);
+                        { if (L.counters) hipLaunchKernelGGL((wf_tail_clds2<FEAT, 768, 1>), dim3((uint32_t)tgrid[0]), dim3(768), clds, st, L, W, itx); else hipLaunchKernelGGL((wf_tail_clds2<FEAT, 768, 0>), dim3((uint32_t)tgrid[0]), dim3(768), clds, st, L, W, itx); }
                     else if (cn == CN_F32_4)
                         hipLaunchKernelGGL((wf_tail_clds<FEAT, CN_F32_4>), dim3((uint32_t)tgrid[0]), dim3(1024), clds, st, L, W, itx);
                     else if (cn == CN_F16_4)
@@ -1927,10 +1974,10 @@ void wf_run_fused(const rtw_launch& L, const rtw_wf& W0, hipStream_t st, int n_c
             if (lds && (L.wf_fuse & 2u)) {  // the node array in LDS for the tail too
                 thread_local uint64_t tl[2] = {0, 0};
                 if (tl[1] != wf_key(n_cu, tdyn)) {
-                    tl[0] = wf_grid(wf_tail_lds<FEAT>, n_cu, tdyn);
+                    tl[0] = wf_grid(wf_tail_lds<FEAT, 0>, n_cu, tdyn);
                     tl[1] = wf_key(n_cu, tdyn);
                 }
-                hipLaunchKernelGGL(wf_tail_lds<FEAT>, dim3((uint32_t)tl[0]), dim3(256), tdyn, st, L, Wd, itx);
+                { if (L.counters) hipLaunchKernelGGL((wf_tail_lds<FEAT, 1>), dim3((uint32_t)tl[0]), dim3(256), tdyn, st, L, Wd, itx); else hipLaunchKernelGGL((wf_tail_lds<FEAT, 0>), dim3((uint32_t)tl[0]), dim3(256), tdyn, st, L, Wd, itx); }
                 return;
             }
             wf_launch_tail<FEAT>(L, Wd, st, n_cu, gdyn, wtail, itx);
@@ -2057,10 +2104,10 @@ void wf_run(const rtw_launch& L, const rtw_wf& W0, hipStream_t st, int n_cu, rtw
                 thread_local uint64_t tl[2] = {0, 0};
                 const size_t tdyn = tlds + L.shade_lds;  // wf_tail_lds stages the materials too
                 if (tl[1] != wf_key(n_cu, tdyn)) {
-                    tl[0] = wf_grid(wf_tail_lds<FEAT>, n_cu, tdyn);
+                    tl[0] = wf_grid(wf_tail_lds<FEAT, 0>, n_cu, tdyn);
                     tl[1] = wf_key(n_cu, tdyn);
                 }
-                hipLaunchKernelGGL(wf_tail_lds<FEAT>, dim3((uint32_t)tl[0]), dim3(256), tdyn, st, L, Wx, itx);
+                { if (L.counters) hipLaunchKernelGGL((wf_tail_lds<FEAT, 1>), dim3((uint32_t)tl[0]), dim3(256), tdyn, st, L, Wx, itx); else hipLaunchKernelGGL((wf_tail_lds<FEAT, 0>), dim3((uint32_t)tl[0]), dim3(256), tdyn, st, L, Wx, itx); }
             } else {
                 wf_launch_tail<FEAT>(L, Wx, st, n_cu, w2l, wtail, itx);
             }
@@ -2136,7 +2183,7 @@ uint32_t rtw_wf_spheres_max_waves(int n_cu) {
     if (auto it = cache.find(n_cu); it != cache.end()) return it->second;
     const uint32_t b = std::max({wf_grids<0u>(n_cu).shade, wf_grids<0u>(n_cu).shade0, wf_grids<RTW_F_CHECKER>(n_cu).shade,
                                  wf_grids<RTW_F_CHECKER>(n_cu).shade0});
-    const uint32_t c2 = std::max(wf_grid(wf_step_clds2<0u, 768>, n_cu, 0, 768), wf_grid(wf_step_clds2<RTW_F_CHECKER, 768>, n_cu, 0, 768)) * 12u;
+    const uint32_t c2 = std::max(wf_grid(wf_step_clds2<0u, 768, 0>, n_cu, 0, 768), wf_grid(wf_step_clds2<RTW_F_CHECKER, 768, 0>, n_cu, 0, 768)) * 12u;
     const uint32_t c1 = std::max(wf_grid(wf_step_clds<0u>, n_cu, 0, 1024), wf_grid(wf_step_clds<RTW_F_CHECKER>, n_cu, 0, 1024)) * 16u;
     const uint32_t val = std::max({4u * b, c2, c1});
     cache[n_cu] = val;
