@@ -1,13 +1,13 @@
 #!/bin/bash
-# Round-5 measurement session: ONE build, each part on one box (PART=pmc | bench | extra), output under gpurun_out/r5f/
-# (copied into profiles/ by tools/collect_r5.sh afterwards).
+# The end-of-round measurement session: ONE build, each part on one box (PART=pmc | bench | extra), output under
+# $O (default gpurun_out/final/), copied into profiles/ by `R=<round tag> bash tools/collect_final.sh <part>` afterwards.
 #   pmc:   VALU (SQ) and HBM-traffic PMC passes of bench.py for every config + the per-rank shard passes of C2 at
 #          N = 2, 4, 8 (rank 0), each stamped with rtw_build_id; copied into profiles/ on the box so that
 #   bench: the walk ceiling, then bench lines of every config (their rooflines from this build's passes), the C2
 #          rocprofv3 --kernel-trace --stats summary;
 #   extra: C2 and C4 stall passes, the C2 shard predictions at N = 1, 2, 4, 8 (tools/shard_sim.py).
 set -u
-O=gpurun_out/r5f
+O=${O:-gpurun_out/final}
 mkdir -p "$O"
 export TMPDIR=/tmp
 PART=${PART:-pmc}

@@ -27,6 +27,37 @@
 #include <map>
 #include <mutex>
 
+// Waves-per-SIMD targets of the 256-thread kernels (1 = no target: the registers the code needs;
+// MI355X_MICROARCH.md: <= 96 VGPRs -> 5 waves, <= 80 -> 6, <= 72 -> 7), same-box A/Bs of round 6
+// (profiles/r6_waves/).  Once round 6 had cut the live state (profiles/r6_late_rest/), more waves paid despite
+// a few spills: the split trace (C4: 83 VGPRs, 5 waves) at 6 waves -8.5 % trace time, at 7 a further -3.5 %; the
+// split shade at 6 (C4 +3.5 % with the trace at 6; 5 alone: +-0); the two-wide tail (93 VGPRs) at 6: -3.4 % tail
+// time; the LDS tail of the object scenes (Cornell: 113 VGPRs, 4 waves) at 5: +7 %, at 6 a further +2 % on
+// Cornell but -8 % on Cornell smoke (media: 126 VGPRs), which keeps 5; the fused wf_step at 5 instead of 4:
+// Cornell -3 %, smoke -8 %, C5 -9 % (its spills grow)
+#ifndef RTW_WPE_TRACE
+#define RTW_WPE_TRACE 7
+#endif
+#ifndef RTW_WPE_SHADE
+#define RTW_WPE_SHADE 6
+#endif
+#ifndef RTW_WPE_TAIL_W5
+#define RTW_WPE_TAIL_W5 6
+#endif
+#ifndef RTW_WPE_TAIL_LDS  // media scenes; the others RTW_WPE_TAIL_LDS_OBJ
+#define RTW_WPE_TAIL_LDS 5
+#endif
+#ifndef RTW_WPE_TAIL_LDS_OBJ
+#define RTW_WPE_TAIL_LDS_OBJ 6
+#endif
+template <uint32_t FEAT>
+constexpr int wf_tail_lds_wpe() {  // (sphere scene classes: no target, as before)
+    return (FEAT & RTW_F_MEDIUM) ? RTW_WPE_TAIL_LDS : (FEAT & RTW_F_GEOM) ? RTW_WPE_TAIL_LDS_OBJ : 1;
+}
+#ifndef RTW_WPE_STEP
+#define RTW_WPE_STEP 4
+#endif
+
 namespace {
 
 #if defined(RTW_DIAG_WALK)
@@ -947,7 +978,7 @@ __device__ __forceinline__ bool wf_tile_hit(const rtw_launch& L, const rtw_wf& W
 
 // trace: closest hit per ray of the input set (no shading state in registers)
 template <uint32_t FEAT, bool LDS, bool CAM = false>
-__global__ __launch_bounds__(256) void wf_trace(rtw_launch L, rtw_wf W, uint32_t it) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RTW_WPE_TRACE))) void wf_trace(rtw_launch L, rtw_wf W, uint32_t it) {
     // the stripes shade(it) appends to start empty (they were iteration it-1's input)
     if (blockIdx.x == 0) W.len[(it + 1u) % 3u][threadIdx.x * RTW_WF_LEN_STRIDE] = 0;
     static_assert(RTW_WF_STRIPES == 256, "one block zeroes the stripe counters");
@@ -1052,7 +1083,7 @@ template <uint32_t FEAT, bool CAM>
 __device__ __forceinline__ void wf_shade_body(const rtw_launch& L, const rtw_wf& W, uint32_t it);
 
 template <uint32_t FEAT, bool CAM = false>
-__global__ __launch_bounds__(256) void wf_shade(rtw_launch L, rtw_wf W, uint32_t it) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RTW_WPE_SHADE))) void wf_shade(rtw_launch L, rtw_wf W, uint32_t it) {
     if constexpr ((FEAT & RTW_F_GEOM) != 0) {
         if (L.geom_lds) {  // quads / members / instances in LDS (hit records of object scenes)
             extern __shared__ float4 wf_shade_geom[];
@@ -1322,7 +1353,7 @@ __global__ __launch_bounds__(256) void wf_tail(rtw_launch L, rtw_wf W, uint32_t 
 // untextured static sphere scenes: capped at 96 VGPRs for 5 waves/SIMD (no spills there; the
 // split shading form took it to 98 = 4 waves: C4 tail +3 %); other scene classes would spill
 template <uint32_t FEAT, int CNT = 2>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void wf_tail_w5(rtw_launch L, rtw_wf W, uint32_t it) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RTW_WPE_TAIL_W5))) void wf_tail_w5(rtw_launch L, rtw_wf W, uint32_t it) {
     wf_tail_body<FEAT, false, CN_F16_8, CNT>(L, W, it, nullptr);
 }
 
@@ -1341,7 +1372,7 @@ __device__ __forceinline__ rtw_launch stage_shade(const rtw_launch& L, float4* l
 
 // the 32-B node array(s) staged in LDS (small object scenes: Cornell), + L.geom_lds bytes of geometry
 template <uint32_t FEAT, int CNT = 2>
-__global__ __launch_bounds__(256) void wf_tail_lds(rtw_launch L, rtw_wf W, uint32_t it) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(wf_tail_lds_wpe<FEAT>()))) void wf_tail_lds(rtw_launch L, rtw_wf W, uint32_t it) {
     extern __shared__ float4 wf_tail_nodes[];
     const uint32_t n4 = 2u * L.n_nodes * L.n_orders;
     for (uint32_t k = threadIdx.x; k < n4; k += 256u) wf_tail_nodes[k] = L.nodes[k];
@@ -1424,6 +1455,16 @@ __device__ __forceinline__ int wf_walk(const rtw_launch& L, const void* lds, con
 // The stripe counters: this kernel appends to len[(it+1)%3] (zeroed by the
 // previous iteration, or by the host for it = 0) and zeroes len[(it+2)%3],
 // iteration it-1's input, for the next iteration.
+// the fused step loads a path's throughput / id / RNG state after its walk (late_rest in wf_step_body): every
+// scene class whose walk does not key media draws on the RNG state (object scenes: RTW_OBJ_LATE, an A/B switch)
+#ifndef RTW_OBJ_LATE
+#define RTW_OBJ_LATE 0
+#endif
+template <uint32_t FEAT>
+constexpr bool wf_late_rest() {
+    return (FEAT & RTW_F_MEDIUM) == 0 && ((FEAT & RTW_F_GEOM) == 0 || RTW_OBJ_LATE);
+}
+
 template <uint32_t FEAT, int WALK, int CNT = 2>
 __device__ __forceinline__ void wf_step_body(const rtw_launch& L, const rtw_wf& W, uint32_t it, const void* lds) {
     const rtw_wf_set& S = W.set[it & 1u];
@@ -1450,8 +1491,8 @@ __device__ __forceinline__ void wf_step_body(const rtw_launch& L, const rtw_wf& 
             float2 txy;
             r = wf_load_ray_it<FEAT>(L, S, slot, it, depth, txy, true);
             live = depth != 0;
-            if constexpr ((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM)) != 0) {
-                if (live) {  // object scenes: the RNG state keys the media during the walk
+            if constexpr (!wf_late_rest<FEAT>()) {
+                if (live) {  // media: the RNG state keys the ConstantMedium draws during the walk
                     uint64_t rs;
                     wf_load_rest<FEAT>(L, S, slot, depth, txy, thr, acc, rs, pid, true);
                     rng.s = rs;
@@ -1463,7 +1504,7 @@ __device__ __forceinline__ void wf_step_body(const rtw_launch& L, const rtw_wf& 
         // to 140 B/lane at its 80-VGPR cap and C2 +3.5 % (two same-box rounds, profiles/r6_late_rest/); the
         // loads' latency is now exposed, but five other waves per SIMD cover it
         auto late_rest = [&]() {
-            if constexpr ((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM)) == 0) {
+            if constexpr (wf_late_rest<FEAT>()) {
                 if (it != 0 && live) {
                     float2 txy;
                     uint32_t d2;
@@ -1554,6 +1595,7 @@ __device__ __forceinline__ void wf_step_body(const rtw_launch& L, const rtw_wf& 
                 }
 #endif
                 if constexpr (CNT != 0) cnt.rays++;
+                late_rest();
             }
             const bool need_uv = hit >= 0 && needs_unit_vector<FEAT>(hit_material_kind<FEAT>(L.nodes, L, hit));
             float uv3[3] = {0.0f, 0.0f, 0.0f};
@@ -1649,7 +1691,7 @@ __device__ __forceinline__ void wf_step_staged(const rtw_launch& L, const rtw_wf
 
 // the 32-B node array (one ordering) in LDS, or the tree through L1/L2
 template <uint32_t FEAT, bool LDS, int CNT = 2>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void wf_step(rtw_launch L, rtw_wf W, uint32_t it) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RTW_WPE_STEP))) void wf_step(rtw_launch L, rtw_wf W, uint32_t it) {
     wf_step_zero_next(W, it);
     extern __shared__ float4 wf_lds_nodes[];
     const uint32_t n4 = LDS ? 2u * L.n_nodes * L.n_orders : 0u;
