@@ -229,14 +229,18 @@ def test_resource_report_is_this_build(rtw):
     rep = json.load(open(path))
     assert rep["build_id"] == rtw.lib().rtw_build_id().decode(), "stale: run make -C zig-raytracing-weekend_amd/csrc resources"
     k = rep["kernels"]
-    # the product launches (counters compiled out: the trailing 0) of C2 / C4 / Cornell / C5
-    for name in ("wf_step_clds2<0u, 768u, 0>", "wf_tail_clds2<0u, 768u, 0>", "wf_tail_w5<0u, 0>",
-                 "wf_trace<0u, false, false>", "wf_shade<0u, false>", "wf_step<49u, true, 0>", "wf_tail_lds<49u, 0>",
-                 "wf_step<7u, true, 0>", "wf_reduce"):
+    # the product launches of C2 / C4 / Cornell / C5: counters compiled out (CNT 0), fused steps split into
+    # iteration 0 (IT0 1) and the later iterations (IT0 0)
+    for name in ("wf_step_clds2<0u, 768u, 0, 1>", "wf_step_clds2<0u, 768u, 0, 0>", "wf_tail_clds2<0u, 768u, 0>",
+                 "wf_tail_w5<0u, 0>", "wf_trace<0u, false, false>", "wf_shade<0u, false>", "wf_step<49u, true, 0, 0>",
+                 "wf_tail_lds<49u, 0>", "wf_step<7u, true, 0, 0>", "wf_reduce"):
         assert name in k, name
         assert k[name]["vgpr"] and k[name]["occupancy"], (name, k[name])
     # the 6-wave shapes fit 80 VGPRs (MI355X_MICROARCH.md: 80 allocated -> 6 waves / SIMD); round 6 took the fused
-    # step's spills from 156 to 64 B/lane and the compact-LDS tail's to none (profiles/r6_late_rest/)
-    step, tail = k["wf_step_clds2<0u, 768u, 0>"], k["wf_tail_clds2<0u, 768u, 0>"]
-    assert step["vgpr"] <= 80 and step["occupancy"] == 6 and step["scratch"] <= 64
-    assert tail["vgpr"] <= 80 and tail["scratch"] == 0
+    # step's spills from 156 to 44 / 28 B/lane (iteration 0 / the rest) and the compact-LDS tail's to none
+    # (profiles/r6_late_rest/, profiles/r6_waves/)
+    for it in (0, 1):
+        step = k[f"wf_step_clds2<0u, 768u, 0, {it}>"]
+        assert step["vgpr"] <= 80 and step["occupancy"] == 6 and step["scratch"] <= 44, step
+    tail = k["wf_tail_clds2<0u, 768u, 0>"]
+    assert tail["vgpr"] <= 80 and tail["scratch"] == 0, tail

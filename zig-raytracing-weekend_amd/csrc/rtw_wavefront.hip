@@ -1465,8 +1465,11 @@ constexpr bool wf_late_rest() {
     return (FEAT & RTW_F_MEDIUM) == 0 && ((FEAT & RTW_F_GEOM) == 0 || RTW_OBJ_LATE);
 }
 
-template <uint32_t FEAT, int WALK, int CNT = 2>
+// IT0: 1 = the launch of iteration 0 (camera rays), 0 = a launch of iteration >= 1, 2 = either (runtime `it`)
+template <uint32_t FEAT, int WALK, int CNT = 2, int IT0 = 2>
 __device__ __forceinline__ void wf_step_body(const rtw_launch& L, const rtw_wf& W, uint32_t it, const void* lds) {
+    if constexpr (IT0 == 1) it = 0;  // (the compiler then drops the other iterations' code)
+    const bool first = IT0 == 2 ? it == 0 : IT0 == 1;
     const rtw_wf_set& S = W.set[it & 1u];
     const rtw_wf_set& O = W.set[(it + 1u) & 1u];
     Counters cnt;
@@ -1482,7 +1485,7 @@ __device__ __forceinline__ void wf_step_body(const rtw_launch& L, const rtw_wf& 
         rng.s = 0;
         f3 thr = mk(1, 1, 1), acc = mk(0, 0, 0);
         const bool got = e.get(W, slot);
-        if (it == 0) {  // the camera ray in registers (wf_camera)
+        if (first) {  // the camera ray in registers (wf_camera)
             pid = slot;
             live = wf_camera<FEAT>(L, W, got, slot, r, rng);
             if (got && !live) W.ls[slot] = rtw_rgb{0.0f, 0.0f, 0.0f};  // rayColor(r, 0) = 0
@@ -1505,7 +1508,7 @@ __device__ __forceinline__ void wf_step_body(const rtw_launch& L, const rtw_wf& 
         // loads' latency is now exposed, but five other waves per SIMD cover it
         auto late_rest = [&]() {
             if constexpr (wf_late_rest<FEAT>()) {
-                if (it != 0 && live) {
+                if (!first && live) {
                     float2 txy;
                     uint32_t d2;
                     (void)wf_load_ray_it<FEAT>(L, S, slot, it, d2, txy, true);
@@ -1534,7 +1537,7 @@ __device__ __forceinline__ void wf_step_body(const rtw_launch& L, const rtw_wf& 
                 bool listed = false;
                 if constexpr (WALK != WALK_GLOBAL && (FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING)) == 0) {
                     // camera rays: the tile's candidate list
-                    if (it == 0 && W.tl_count) {
+                    if (first && W.tl_count) {
                         const uint32_t tile = (slot >> 6) / W.n_s;
                         if constexpr (CNT != 2) listed = wf_tile_hit<CNT == 1>(L, W, tile, r, hit, t, cnt);
                         else listed = L.counters ? wf_tile_hit<true>(L, W, tile, r, hit, t, cnt)
@@ -1628,7 +1631,7 @@ __device__ __forceinline__ void wf_step_zero_next(const rtw_wf& W, uint32_t it) 
 }
 
 // compact nodes of every copy in LDS, then the materials when they fit
-template <uint32_t FEAT, int WALK, int CNT = 2>
+template <uint32_t FEAT, int WALK, int CNT = 2, int IT0 = 2>
 __device__ __forceinline__ void wf_step_clds_body(const rtw_launch& L, const rtw_wf& W, uint32_t it) {
     wf_step_zero_next(W, it);
     extern __shared__ uint4 wf_clds[];
@@ -1640,10 +1643,10 @@ __device__ __forceinline__ void wf_step_clds_body(const rtw_launch& L, const rtw
         __syncthreads();
         rtw_launch Lm = L;
         Lm.mats = reinterpret_cast<const rtw_dev_material*>(ml);
-        wf_step_body<FEAT, WALK, CNT>(Lm, W, it, wf_clds);
+        wf_step_body<FEAT, WALK, CNT, IT0>(Lm, W, it, wf_clds);
         return;
     }
-    wf_step_body<FEAT, WALK, CNT>(L, W, it, wf_clds);
+    wf_step_body<FEAT, WALK, CNT, IT0>(L, W, it, wf_clds);
 }
 
 // one 1024-thread block per CU (the 8-copy stage, 124 KB for C2, allows no second block)
@@ -1658,16 +1661,22 @@ __global__ __launch_bounds__(1024) void wf_step_clds(rtw_launch L, rtw_wf W, uin
 // its dependent ds_read_b128 41 % of the cycles at 4 waves (profiles/r4_stall/): the fifth and sixth waves have
 // ready work to issue in those waits.  (Two blocks of 512 or 640 threads lost their A/Bs -- profiles/r5_occupancy/,
 // diag/walk_variants.patch -- and were removed in round 6.)
-template <uint32_t FEAT, uint32_t T, int CNT = 2>
+// Iteration 0 (camera rays: wf_camera, the tile lists) and the later iterations (late_rest) of the fused steps in
+// separate instantiations, so that neither pays for the other's registers: C2's step scratch 64 -> 44 / 28 B,
+// C2 +1.8 % (same box, profiles/r6_waves/i/; C5, Cornell, smoke +-0.6 %).  0 = one instantiation (A/B).
+#ifndef RTW_STEP_IT0
+#define RTW_STEP_IT0 1
+#endif
+template <uint32_t FEAT, uint32_t T, int CNT = 2, int IT0 = 2>
 __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(2 * T / 256)))
 void wf_step_clds2(rtw_launch L, rtw_wf W, uint32_t it) {
     static_assert((FEAT & (RTW_F_GEOM | RTW_F_MEDIUM | RTW_F_MOVING)) == 0, "static sphere scenes");
-    wf_step_clds_body<FEAT, WALK_CLDS4, CNT>(L, W, it);
+    wf_step_clds_body<FEAT, WALK_CLDS4, CNT, IT0>(L, W, it);
 }
 
 // wf_step's LDS extras by mask (bit 0 Perlin tables, 1 materials/textures, 2 geometry); masks a
 // scene class cannot use compile to nothing
-template <uint32_t FEAT, uint32_t MASK, int CNT>
+template <uint32_t FEAT, uint32_t MASK, int CNT, int IT0>
 __device__ __forceinline__ void wf_step_staged(const rtw_launch& L, const rtw_wf& W, uint32_t it, float4* nodes,
                                                float4* extra) {
     constexpr bool P = (MASK & 1u) && (FEAT & RTW_F_NOISE), S = (MASK & 2u) != 0, G = (MASK & 4u) && (FEAT & RTW_F_GEOM);
@@ -1685,12 +1694,12 @@ __device__ __forceinline__ void wf_step_staged(const rtw_launch& L, const rtw_wf
         }
         if constexpr (G) Lp = stage_geom(Lp, extra);
         __syncthreads();
-        wf_step_body<FEAT, WALK_LDS, CNT>(Lp, W, it, nodes);
+        wf_step_body<FEAT, WALK_LDS, CNT, IT0>(Lp, W, it, nodes);
     }
 }
 
 // the 32-B node array (one ordering) in LDS, or the tree through L1/L2
-template <uint32_t FEAT, bool LDS, int CNT = 2>
+template <uint32_t FEAT, bool LDS, int CNT = 2, int IT0 = 2>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RTW_WPE_STEP))) void wf_step(rtw_launch L, rtw_wf W, uint32_t it) {
     wf_step_zero_next(W, it);
     extern __shared__ float4 wf_lds_nodes[];
@@ -1703,19 +1712,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RTW_WPE_STE
                               (((FEAT & RTW_F_GEOM) && L.geom_lds) ? 4u : 0u);
         float4* extra = wf_lds_nodes + n4;
         switch (mask) {
-            case 1: return wf_step_staged<FEAT, 1, CNT>(L, W, it, wf_lds_nodes, extra);
-            case 2: return wf_step_staged<FEAT, 2, CNT>(L, W, it, wf_lds_nodes, extra);
-            case 3: return wf_step_staged<FEAT, 3, CNT>(L, W, it, wf_lds_nodes, extra);
-            case 4: return wf_step_staged<FEAT, 4, CNT>(L, W, it, wf_lds_nodes, extra);
-            case 5: return wf_step_staged<FEAT, 5, CNT>(L, W, it, wf_lds_nodes, extra);
-            case 6: return wf_step_staged<FEAT, 6, CNT>(L, W, it, wf_lds_nodes, extra);
-            case 7: return wf_step_staged<FEAT, 7, CNT>(L, W, it, wf_lds_nodes, extra);
+            case 1: return wf_step_staged<FEAT, 1, CNT, IT0>(L, W, it, wf_lds_nodes, extra);
+            case 2: return wf_step_staged<FEAT, 2, CNT, IT0>(L, W, it, wf_lds_nodes, extra);
+            case 3: return wf_step_staged<FEAT, 3, CNT, IT0>(L, W, it, wf_lds_nodes, extra);
+            case 4: return wf_step_staged<FEAT, 4, CNT, IT0>(L, W, it, wf_lds_nodes, extra);
+            case 5: return wf_step_staged<FEAT, 5, CNT, IT0>(L, W, it, wf_lds_nodes, extra);
+            case 6: return wf_step_staged<FEAT, 6, CNT, IT0>(L, W, it, wf_lds_nodes, extra);
+            case 7: return wf_step_staged<FEAT, 7, CNT, IT0>(L, W, it, wf_lds_nodes, extra);
             default: break;
         }
         __syncthreads();
-        wf_step_body<FEAT, WALK_LDS, CNT>(L, W, it, wf_lds_nodes);
+        wf_step_body<FEAT, WALK_LDS, CNT, IT0>(L, W, it, wf_lds_nodes);
     } else {
-        wf_step_body<FEAT, WALK_GLOBAL, CNT>(L, W, it, nullptr);
+        wf_step_body<FEAT, WALK_GLOBAL, CNT, IT0>(L, W, it, nullptr);
     }
 }
 
@@ -1978,7 +1987,12 @@ void wf_run_fused(const rtw_launch& L, const rtw_wf& W0, hipStream_t st, int n_c
                 rtw_launch Lc = L;  // the materials are staged only when they fit
                 if (cdyn2 == cdyn0) Lc.mat_lds = 0;
                 if (two)
-                    { if (L.counters) hipLaunchKernelGGL((wf_step_clds2<FEAT, 768, 1>), dim3(grid), dim3(768), cdyn2, st, Lc, Wt, it); else hipLaunchKernelGGL((wf_step_clds2<FEAT, 768, 0>), dim3(grid), dim3(768), cdyn2, st, Lc, Wt, it); }
+                    {
+                        if (L.counters) hipLaunchKernelGGL((wf_step_clds2<FEAT, 768, 1>), dim3(grid), dim3(768), cdyn2, st, Lc, Wt, it);
+                        else if (RTW_STEP_IT0 && it == 0) hipLaunchKernelGGL((wf_step_clds2<FEAT, 768, 0, RTW_STEP_IT0 ? 1 : 2>), dim3(grid), dim3(768), cdyn2, st, Lc, Wt, it);
+                        else if (RTW_STEP_IT0) hipLaunchKernelGGL((wf_step_clds2<FEAT, 768, 0, RTW_STEP_IT0 ? 0 : 2>), dim3(grid), dim3(768), cdyn2, st, Lc, Wt, it);
+                        else hipLaunchKernelGGL((wf_step_clds2<FEAT, 768, 0>), dim3(grid), dim3(768), cdyn2, st, Lc, Wt, it);
+                    }
                 else if (cn == CN_F32_4)
                     hipLaunchKernelGGL((wf_step_clds<FEAT, CN_F32_4>), dim3(grid), dim3(1024), cdyn2, st, Lc, Wt, it);
                 else if (cn == CN_F16_4)
@@ -1990,7 +2004,12 @@ void wf_run_fused(const rtw_launch& L, const rtw_wf& W0, hipStream_t st, int n_c
             }
         }
         if (lds)
-            { if (L.counters) hipLaunchKernelGGL((wf_step<FEAT, true, 1>), dim3(grid), dim3(256), ldyn, st, L, Wt, it); else hipLaunchKernelGGL((wf_step<FEAT, true, 0>), dim3(grid), dim3(256), ldyn, st, L, Wt, it); }
+            {
+                if (L.counters) hipLaunchKernelGGL((wf_step<FEAT, true, 1>), dim3(grid), dim3(256), ldyn, st, L, Wt, it);
+                else if (RTW_STEP_IT0 && it == 0) hipLaunchKernelGGL((wf_step<FEAT, true, 0, RTW_STEP_IT0 ? 1 : 2>), dim3(grid), dim3(256), ldyn, st, L, Wt, it);
+                else if (RTW_STEP_IT0) hipLaunchKernelGGL((wf_step<FEAT, true, 0, RTW_STEP_IT0 ? 0 : 2>), dim3(grid), dim3(256), ldyn, st, L, Wt, it);
+                else hipLaunchKernelGGL((wf_step<FEAT, true, 0>), dim3(grid), dim3(256), ldyn, st, L, Wt, it);
+            }
         else
             { if (L.counters) hipLaunchKernelGGL((wf_step<FEAT, false, 1>), dim3(grid), dim3(256), gdyn, st, L, W, it); else hipLaunchKernelGGL((wf_step<FEAT, false, 0>), dim3(grid), dim3(256), gdyn, st, L, W, it); }
         RTW_TIME_END(T)
