@@ -44,6 +44,18 @@
 #ifndef RTW_WPE_TAIL_W5
 #define RTW_WPE_TAIL_W5 6
 #endif
+// The media scenes' LDS tail parks the path state it does not need during the walk in LDS (wf_tail_body PARK):
+// Cornell smoke's tail 112 -> 80 B of scratch, -6.5 % tail time (+3 %); Cornell's (no media) loses 0.7 % with it
+// (same box, profiles/r6_waves/j/)
+#ifndef RTW_TAIL_PARK
+#define RTW_TAIL_PARK 1
+#endif
+// the cooperative rejection loop in the textured fused step too: once round 6 freed its registers (the IT0
+// split, the hit record after the loop) C5 +0.6 % (two rounds, profiles/r6_waves/l/; round 4: -2.3 % at the cap)
+#ifndef RTW_COOP_TEXTURED
+#define RTW_COOP_TEXTURED 1
+#endif
+
 #ifndef RTW_WPE_TAIL_LDS  // media scenes; the others RTW_WPE_TAIL_LDS_OBJ
 #define RTW_WPE_TAIL_LDS 5
 #endif
@@ -1172,9 +1184,11 @@ __device__ __forceinline__ void wf_shade_body(const rtw_launch& L, const rtw_wf&
 // CLDS: the walk reads the compact nodes staged in LDS (`lds`) instead of L1/L2.
 // CNT (every kernel with a counted form): 0 = no device counters (the product launches: their registers and
 // atomics compile away), 1 = the counted pass (rtw_render_opts.counters), 2 = decided per launch by L.counters
-template <uint32_t FEAT, bool CLDS, int CN = CN_F16_8, int CNT = 2>
+// PARK (`park`: 2 x 256 float4 of LDS, 256-thread blocks): the path's throughput, radiance, id and depth wait in
+// LDS while its ray walks, so their registers are free for the walk (object scenes' LDS tail)
+template <uint32_t FEAT, bool CLDS, int CN = CN_F16_8, int CNT = 2, bool PARK = false>
 __device__ __forceinline__ void wf_tail_body(const rtw_launch& L, const rtw_wf& W, uint32_t it, const uint4* lds,
-                                             const float4* nodes = nullptr) {
+                                             const float4* nodes = nullptr, float4* park = nullptr) {
     const uint32_t lane = __lane_id();
     const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     const rtw_wf_set& S = W.set[it & 1u];
@@ -1258,6 +1272,10 @@ __device__ __forceinline__ void wf_tail_body(const rtw_launch& L, const rtw_wf& 
                 cnt.rays++;
                 cnt.tail_rays++;
             }
+            if constexpr (PARK) {
+                park[threadIdx.x] = make_float4(thr.x, thr.y, thr.z, acc.x);
+                park[256u + threadIdx.x] = make_float4(acc.y, acc.z, __uint_as_float(pid), __uint_as_float(depth));
+            }
             float t;
             int hit;
             if constexpr (CLDS && CNT == 2)
@@ -1268,23 +1286,26 @@ __device__ __forceinline__ void wf_tail_body(const rtw_launch& L, const rtw_wf& 
             else
                 hit = nodes ? traverse<FEAT, false>(nodes, L, r, t, cnt, rng.s)  // the LDS stage
                             : wf_traverse_global<FEAT>(L, r, t, cnt, rng.s);
+            if constexpr (PARK) {
+                asm volatile("" ::: "memory");  // (no forwarding of the stores past the walk: the reload is real)
+                const float4 p0 = park[threadIdx.x], p1 = park[256u + threadIdx.x];
+                thr = mk(p0.x, p0.y, p0.z);
+                acc = mk(p0.w, p1.x, p1.y);
+                pid = fbits(p1.z);
+                depth = fbits(p1.w);
+            }
             if (hit < 0) {
                 acc = acc + thr * background(L, r);
             } else if constexpr ((FEAT & ~RTW_F_CHECKER) == 0) {
                 // untextured static sphere scenes: the fused step's split form (C2 tail -10 %, C4 -5 % over the
-                // nested form; the textured C5 tail +5 %: nested form there).  On the compact LDS stage (C2) in the
-                // fused step's order -- the material kind, the wave's rejection loop, then the hit record (-0.9 %
-                // tail time, no scratch left); through L1/L2 (C4, seq_reject) the hit record first (its loads
-                // overlap the loop there: +1.2 % the other way, profiles/r6_late_rest/)
+                // nested form; the textured C5 tail +5 %: nested form there), in the fused step's order -- the
+                // material kind, the wave's rejection loop, then the hit record: the compact-LDS tail (C2) -0.9 %
+                // tail time and no scratch left; the two-wide tail (C4), once at 6 waves, -2.1 % (at 5 waves it had
+                // lost 1.2 %: profiles/r6_late_rest/f/, profiles/r6_waves/k/)
                 hitp = true;
-                if constexpr (CLDS) {
-                    ohit = hit;
-                    ot = t;
-                    need_uv = needs_unit_vector<FEAT>(hit_material_kind<FEAT>(L.nodes, L, hit));
-                } else {
-                    hp = hit_prep<FEAT>(L.nodes, L, r, hit, t);
-                    need_uv = needs_unit_vector<FEAT>(hp.m.kind);
-                }
+                ohit = hit;
+                ot = t;
+                need_uv = needs_unit_vector<FEAT>(hit_material_kind<FEAT>(L.nodes, L, hit));
             } else if constexpr ((FEAT & RTW_F_GEOM) != 0) {
                 // object scenes: as the fused step's object path, the wave's shared rejection loop
                 // (wf_reject3) before the hit record, on the material kind alone
@@ -1322,10 +1343,8 @@ __device__ __forceinline__ void wf_tail_body(const rtw_launch& L, const rtw_wf& 
             float uv3[3] = {0.0f, 0.0f, 0.0f};
             // the wave-cooperative loop (same candidates, same RNG states as seq_reject<3>): C2 +1.4 %
             if constexpr (CLDS) wf_reject3(need_uv, rng, uv3);
-            else if (need_uv) seq_reject<3>(rng, uv3);
-            if constexpr (CLDS) {
-                if (hitp) hp = hit_prep<FEAT>(L.nodes, L, r, ohit, ot);
-            }
+            else if (need_uv) seq_reject<3>(rng, uv3);  // (the cooperative loop here: +-0, profiles/r6_waves/k/)
+            if (hitp) hp = hit_prep<FEAT>(L.nodes, L, r, ohit, ot);
             if (hitp) {
                 const f3 ruv = need_uv ? unit_vector(mk(uv3[0], uv3[1], uv3[2])) : mk(0, 0, 0);
                 f3 att;
@@ -1374,6 +1393,9 @@ __device__ __forceinline__ rtw_launch stage_shade(const rtw_launch& L, float4* l
 template <uint32_t FEAT, int CNT = 2>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(wf_tail_lds_wpe<FEAT>()))) void wf_tail_lds(rtw_launch L, rtw_wf W, uint32_t it) {
     extern __shared__ float4 wf_tail_nodes[];
+    constexpr bool kPark = RTW_TAIL_PARK && (FEAT & RTW_F_MEDIUM) != 0;
+    __shared__ float4 park_lds[kPark ? 512 : 1];
+    float4* park = park_lds;
     const uint32_t n4 = 2u * L.n_nodes * L.n_orders;
     for (uint32_t k = threadIdx.x; k < n4; k += 256u) wf_tail_nodes[k] = L.nodes[k];
     // then materials, then geometry: one call per combination (statically LDS pointers)
@@ -1381,25 +1403,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(wf_tail_lds
     if (sl && gl) {
         const rtw_launch G = stage_geom(stage_shade(L, wf_tail_nodes + n4), wf_tail_nodes + n4 + L.shade_lds / 16u);
         __syncthreads();
-        wf_tail_body<FEAT, false, CN_F16_8, CNT>(G, W, it, nullptr, wf_tail_nodes);
+        wf_tail_body<FEAT, false, CN_F16_8, CNT, kPark>(G, W, it, nullptr, wf_tail_nodes, park);
         return;
     }
     if (sl) {
         const rtw_launch G = stage_shade(L, wf_tail_nodes + n4);
         __syncthreads();
-        wf_tail_body<FEAT, false, CN_F16_8, CNT>(G, W, it, nullptr, wf_tail_nodes);
+        wf_tail_body<FEAT, false, CN_F16_8, CNT, kPark>(G, W, it, nullptr, wf_tail_nodes, park);
         return;
     }
     if constexpr ((FEAT & RTW_F_GEOM) != 0) {
         if (gl) {
             const rtw_launch G = stage_geom(L, wf_tail_nodes + n4);
             __syncthreads();
-            wf_tail_body<FEAT, false, CN_F16_8, CNT>(G, W, it, nullptr, wf_tail_nodes);
+            wf_tail_body<FEAT, false, CN_F16_8, CNT, kPark>(G, W, it, nullptr, wf_tail_nodes, park);
             return;
         }
     }
     __syncthreads();
-    wf_tail_body<FEAT, false, CN_F16_8, CNT>(L, W, it, nullptr, wf_tail_nodes);
+    wf_tail_body<FEAT, false, CN_F16_8, CNT, kPark>(L, W, it, nullptr, wf_tail_nodes, park);
 }
 
 
@@ -1570,9 +1592,8 @@ __device__ __forceinline__ void wf_step_body(const rtw_launch& L, const rtw_wf& 
                 }
             }
             float uv3[3] = {0.0f, 0.0f, 0.0f};
-            // the wave-cooperative loop (same candidates, same RNG states as seq_reject<3>): C2 +1.4 %; not with
-            // image / noise textures, whose step is at its 128-VGPR cap (C5 -2.3 %)
-            if constexpr ((FEAT & (RTW_F_IMAGE | RTW_F_NOISE)) == 0) wf_reject3(need_uv, rng, uv3);
+            // the wave-cooperative loop (same candidates, same RNG states as seq_reject<3>): C2 +1.4 %, C5 +0.6 %
+            if constexpr ((FEAT & (RTW_F_IMAGE | RTW_F_NOISE)) == 0 || RTW_COOP_TEXTURED) wf_reject3(need_uv, rng, uv3);
             else if (need_uv) seq_reject<3>(rng, uv3);
             if (hitp) hp = hit_prep<FEAT>(L.nodes, L, r, hhit, ht);
             if (hitp) {
