@@ -56,15 +56,24 @@
 #define RTW_COOP_TEXTURED 1
 #endif
 
-#ifndef RTW_WPE_TAIL_LDS  // media scenes; the others RTW_WPE_TAIL_LDS_OBJ
+#ifndef RTW_WPE_TAIL_LDS  // object classes with media / textures / motion; the plain one RTW_WPE_TAIL_LDS_OBJ
 #define RTW_WPE_TAIL_LDS 5
 #endif
 #ifndef RTW_WPE_TAIL_LDS_OBJ
 #define RTW_WPE_TAIL_LDS_OBJ 6
 #endif
+// the split trace / shade targets apply to the untextured static sphere classes they were measured on (C4);
+// the other classes' split kernels (large object or textured trees: 100-200 VGPRs) keep no target
 template <uint32_t FEAT>
-constexpr int wf_tail_lds_wpe() {  // (sphere scene classes: no target, as before)
-    return (FEAT & RTW_F_MEDIUM) ? RTW_WPE_TAIL_LDS : (FEAT & RTW_F_GEOM) ? RTW_WPE_TAIL_LDS_OBJ : 1;
+constexpr int wf_split_wpe(int w) { return (FEAT & ~RTW_F_CHECKER) == 0 ? w : 1; }
+template <uint32_t FEAT>
+constexpr int wf_tail_lds_wpe() {
+    // the object class without media, textures or motion (Cornell) at 6; the media class (Cornell smoke, 126 VGPRs)
+    // at 5; every other class keeps no target -- simple_light's all-features tail at 5 or 6 waves spilled 184 B and
+    // lost 27 % of its tail time (profiles/r6_waves/o/, q/)
+    constexpr uint32_t tex = RTW_F_IMAGE | RTW_F_NOISE | RTW_F_MOVING;
+    if constexpr (!(FEAT & RTW_F_GEOM) || (FEAT & tex)) return 1;
+    return (FEAT & RTW_F_MEDIUM) ? RTW_WPE_TAIL_LDS : RTW_WPE_TAIL_LDS_OBJ;
 }
 #ifndef RTW_WPE_STEP
 #define RTW_WPE_STEP 4
@@ -990,7 +999,7 @@ __device__ __forceinline__ bool wf_tile_hit(const rtw_launch& L, const rtw_wf& W
 
 // trace: closest hit per ray of the input set (no shading state in registers)
 template <uint32_t FEAT, bool LDS, bool CAM = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RTW_WPE_TRACE))) void wf_trace(rtw_launch L, rtw_wf W, uint32_t it) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(wf_split_wpe<FEAT>(RTW_WPE_TRACE)))) void wf_trace(rtw_launch L, rtw_wf W, uint32_t it) {
     // the stripes shade(it) appends to start empty (they were iteration it-1's input)
     if (blockIdx.x == 0) W.len[(it + 1u) % 3u][threadIdx.x * RTW_WF_LEN_STRIDE] = 0;
     static_assert(RTW_WF_STRIPES == 256, "one block zeroes the stripe counters");
@@ -1095,7 +1104,7 @@ template <uint32_t FEAT, bool CAM>
 __device__ __forceinline__ void wf_shade_body(const rtw_launch& L, const rtw_wf& W, uint32_t it);
 
 template <uint32_t FEAT, bool CAM = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RTW_WPE_SHADE))) void wf_shade(rtw_launch L, rtw_wf W, uint32_t it) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(wf_split_wpe<FEAT>(RTW_WPE_SHADE)))) void wf_shade(rtw_launch L, rtw_wf W, uint32_t it) {
     if constexpr ((FEAT & RTW_F_GEOM) != 0) {
         if (L.geom_lds) {  // quads / members / instances in LDS (hit records of object scenes)
             extern __shared__ float4 wf_shade_geom[];
@@ -1393,7 +1402,9 @@ __device__ __forceinline__ rtw_launch stage_shade(const rtw_launch& L, float4* l
 template <uint32_t FEAT, int CNT = 2>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(wf_tail_lds_wpe<FEAT>()))) void wf_tail_lds(rtw_launch L, rtw_wf W, uint32_t it) {
     extern __shared__ float4 wf_tail_nodes[];
-    constexpr bool kPark = RTW_TAIL_PARK && (FEAT & RTW_F_MEDIUM) != 0;
+    // (the media class only: the all-features class of simple_light carries the medium bit too, and lost with it)
+    constexpr bool kPark = RTW_TAIL_PARK && (FEAT & RTW_F_MEDIUM) != 0 &&
+                           (FEAT & (RTW_F_IMAGE | RTW_F_NOISE | RTW_F_MOVING)) == 0;
     __shared__ float4 park_lds[kPark ? 512 : 1];
     float4* park = park_lds;
     const uint32_t n4 = 2u * L.n_nodes * L.n_orders;
