@@ -294,8 +294,11 @@ def main():
         "unit": "Tlane-op/s",
         "frac": round(achieved_valu / VALU_PEAK_TLOPS, 4) if achieved_valu is not None else None,
         "traffic": traffic,
-        # the dominant kernel's instantiation as the committed PMC pass of this config recorded it
-        "kernel": (valu["kernels"][0] if valu and valu.get("kernels") else knames.get(dom, dom)),
+        # the dominant kernel's instantiations as the committed PMC pass of this config recorded them (round 6:
+        # iteration 0 and the later iterations of a step are two instantiations; the launch time and the PMC
+        # figures are averages over both)
+        "kernel": (" + ".join(valu["kernels"]) if valu and valu.get("kernels") else knames.get(dom, dom)),
+        "kernels": (list(valu["kernels"]) if valu and valu.get("kernels") else [knames.get(dom, dom)]),
         "fused_step": fused,
         "avg_launch_ms": round(dom_launch_s * 1e3, 4),
         "launches_per_step": kcalls[dom] / args.steps,

@@ -40,7 +40,7 @@ def main():
         # (counted passes, warm-up) may run other instantiations, so counting calls per name is not enough.
         rf = bench["roofline"]
         n_dom = int(round(bench["steps"] * rf["launches_per_step"]))
-        dom = [i for i, (_, _, n) in enumerate(rows) if n.split("(")[0].endswith(rf["kernel"]) or rf["kernel"] in n]
+        dom = [i for i, (_, _, n) in enumerate(rows) if is_dominant(n, rf)]
         if len(dom) >= n_dom > 0:
             first = dom[-n_dom]
             j = first
@@ -59,8 +59,18 @@ def main():
               f"{min(d) / 1e3:9.1f} {max(d) / 1e3:9.1f}")
     if bench:
         rf = bench["roofline"]
+        fam = [d for n, ds in per.items() if is_dominant(n, rf) for d in ds]
+        if fam and t0 is not None:
+            print(f"dominant family in the timed region: {len(fam)} calls, mean {sum(fam) / len(fam) / 1e3:.1f} us "
+                  f"({rf['kernel']})")
         print(f"bench.py HIP events: dominant kernel {rf['kernel']} avg {rf['avg_launch_ms'] * 1e3:.1f} us "
               f"over {rf['launches_per_step']} launches/step")
+
+
+def is_dominant(name, rf):
+    """One of the dominant kernel's instantiations (bench.py's roofline.kernels; a round-5 line names one)."""
+    base = name.split("(")[0]
+    return any(base.endswith(k) or k in name for k in rf.get("kernels") or [rf["kernel"]])
 
 
 if __name__ == "__main__":
