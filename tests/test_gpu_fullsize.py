@@ -77,10 +77,11 @@ def check_three_ways(rtw, arr, cam, batches):
     return ref
 
 
-@pytest.mark.parametrize("name,batches", [("c2", 1), ("c4", 1), ("c5", 2)])
+@pytest.mark.parametrize("name,batches", [("c2", 1), ("c4", 1), ("c5", 2), ("c3", 16)])
 def test_sphere_config_full_batch(rtw, oracle, earth_rgba, name, batches):
     """C2 (fused compact-LDS step + LDS tail), C4 (split trace / shade through L1/L2, sort_iters_split, the
-    96-VGPR tail) and C5 (fused textured step, every bounce a wavefront iteration) at bench size."""
+    two-wide tail), C5 (fused textured step, every bounce a wavefront iteration) and C3 (BASELINE's 8-GPU frame,
+    3840x2160x1024, on one GPU: 16 sample batches of the C2 kernels, each bucketed) at bench size."""
     arr, cam = scene(rtw, name, earth_rgba)
     ref = check_three_ways(rtw, arr, cam, batches)
     pix = np.sort(np.random.default_rng(7).choice(cam.size, N_PIX, replace=False)).astype(np.uint32)
@@ -90,9 +91,10 @@ def test_sphere_config_full_batch(rtw, oracle, earth_rgba, name, batches):
     assert ok.all(), (pix[~ok][:5], np.abs(ref[pix, :3] - want[:, :3]).max())
 
 
-@pytest.mark.parametrize("name", ["cornell", "cornell_smoke"])
+@pytest.mark.parametrize("name", ["cornell", "cornell_smoke", "simple_light"])
 def test_object_config_full_batch(rtw, oracle, earth_rgba, name):
-    """Cornell (depth 200, fused LDS step + wf_tail_lds) and Cornell smoke (media) at 600x600x200."""
+    """Cornell (depth 200, fused LDS step + wf_tail_lds), Cornell smoke (media) at 600x600x200 and simple_light
+    (Perlin texture, quad and sphere lights: every feature class) at 800x450x100."""
     arr, cam = scene(rtw, name, earth_rgba)
     ref = check_three_ways(rtw, arr, cam, 1)
     ocam = ocamera(oracle, cam)
